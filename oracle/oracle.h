@@ -1,0 +1,106 @@
+/* oracle/oracle.h -- TEST INFRASTRUCTURE ONLY.
+ *
+ * CPU restatement of ForSt's block-checksum hot path (the parity oracle and the
+ * "port" CPU baseline).  Only tests/, __graft_entry__.smoke() and bench.py's
+ * cpu_baseline leg may load this library.  The product path (forst_amd/) never
+ * links it and has no CPU fallback.
+ *
+ * Every function cites the reference file:line whose behaviour it restates
+ * (paths relative to the ForSt tree, RocksDB 8.10.0 fork).
+ */
+#ifndef FORST_ORACLE_H
+#define FORST_ORACLE_H
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* include/rocksdb/table.h:54-60 */
+enum { OR_kNoChecksum = 0, OR_kCRC32c = 1, OR_kxxHash = 2, OR_kxxHash64 = 3,
+       OR_kXXH3 = 4 };
+
+/* ---- CRC32C (util/crc32c.h, util/crc32c.cc) ---- */
+uint32_t oracle_crc32c_extend(uint32_t crc, const void* p, size_t n);   /* portable slicing-by-8 */
+uint32_t oracle_crc32c_extend_fast(uint32_t crc, const void* p, size_t n); /* SSE4.2 3-way */
+uint32_t oracle_crc32c_value(const void* p, size_t n);
+uint32_t oracle_crc32c_combine(uint32_t crc1, uint32_t crc2, size_t len2);
+uint32_t oracle_crc32c_mask(uint32_t crc);
+uint32_t oracle_crc32c_unmask(uint32_t masked);
+/* x^(8*nbytes) shift of a raw CRC state (GF(2)); used to derive GPU tables. */
+uint32_t oracle_crc32c_shift(uint32_t state, uint64_t nbytes);
+
+/* ---- xxHash v0.8.1 (util/xxhash.h) ---- */
+uint64_t oracle_xxh3_64(const void* p, size_t n);
+uint32_t oracle_xxh32(const void* p, size_t n, uint32_t seed);
+uint64_t oracle_xxh64(const void* p, size_t n, uint64_t seed);
+
+/* ---- block checksum dispatcher (table/format.cc, table/format.h) ---- */
+uint32_t oracle_compute_builtin_checksum(int type, const void* p, size_t n);
+uint32_t oracle_compute_builtin_checksum_with_last_byte(int type, const void* p,
+                                                        size_t n, uint8_t last);
+uint32_t oracle_checksum_modifier_for_context(uint32_t base, uint64_t offset);
+/* table/block_based/reader_common.cc:26.  Returns 1 if OK.  *computed and
+ * *stored receive the values the reference would report (unmasked for CRC,
+ * stored with context removed). */
+int oracle_verify_block_checksum(int type, const void* data, size_t block_size,
+                                 uint32_t modifier, uint32_t* computed,
+                                 uint32_t* stored);
+
+/* ---- batch forms (same layout as the C-ABI in include/forst_checksum.h) ---- */
+/* compute (write side, a7 + a8): out[i] = ComputeBuiltinChecksumWithLastByte(
+ *   type, base+off[i], size[i], last ? last[i] : base[off[i]+size[i]]) + mod[i] */
+void oracle_block_checksum_batch(int type, const uint8_t* base,
+                                 const uint64_t* offsets, const uint32_t* sizes,
+                                 const uint8_t* last_bytes,
+                                 const uint32_t* modifiers, uint32_t* out,
+                                 size_t n, int nthreads);
+/* verify (read side, a9); returns number of mismatches */
+uint64_t oracle_block_verify_batch(int type, const uint8_t* base,
+                                   const uint64_t* offsets,
+                                   const uint32_t* sizes,
+                                   const uint32_t* modifiers,
+                                   uint32_t* computed, uint8_t* ok, size_t n,
+                                   int nthreads);
+void oracle_crc32c_batch(const uint8_t* base, const uint64_t* offsets,
+                         const uint32_t* lengths, uint32_t* out, size_t n,
+                         int nthreads);
+void oracle_xxh3_batch(const uint8_t* base, const uint64_t* offsets,
+                       const uint32_t* lengths, uint64_t* out, size_t n,
+                       int nthreads);
+
+/* ---- WAL (db/log_format.h, db/log_writer.cc, db/log_reader.cc) ---- */
+/* masked record CRC as EmitPhysicalRecord writes it (db/log_writer.cc:228) */
+uint32_t oracle_wal_record_crc(int type, uint32_t log_number,
+                               const void* payload, size_t n);
+/* Frame `n` logical records into log blocks the way log::Writer::AddRecord
+ * does (db/log_writer.cc:65-160, no compression).  `dst` must hold
+ * oracle_wal_framed_size(...) bytes.  Returns bytes written.  Physical record
+ * headers are recorded in rec_offsets/rec_lengths (may be NULL) -- offset of
+ * the header and the payload length of each physical record. */
+uint64_t oracle_wal_framed_size(const uint32_t* lengths, size_t n,
+                                int recyclable);
+uint64_t oracle_wal_frame(const uint8_t* payloads, const uint32_t* lengths,
+                          size_t n, int recyclable, uint32_t log_number,
+                          uint8_t* dst, uint64_t* rec_offsets,
+                          uint32_t* rec_lengths, uint64_t* n_phys);
+/* Verify every physical record CRC of log blocks [0, nbytes) the way
+ * log::Reader::ReadPhysicalRecord checks it (db/log_reader.cc:450-531),
+ * per 32 KiB log block.  Walks headers; status per physical record written
+ * to ok[] in order (1 = CRC ok).  Returns number of physical records seen;
+ * *bad receives the count of CRC mismatches. */
+uint64_t oracle_wal_verify(const uint8_t* buf, uint64_t nbytes, uint8_t* ok,
+                           uint64_t ok_cap, uint64_t* bad, int nthreads);
+
+/* ---- synthetic data ---- */
+uint64_t oracle_splitmix64(uint64_t x);
+/* byte i of the stream = byte (i & 7) of splitmix64(seed + (i>>3 + 1)*gamma) */
+void oracle_fill_stream(uint8_t* dst, uint64_t start, uint64_t nbytes,
+                        uint64_t seed);
+
+#ifdef __cplusplus
+}
+#endif
+#endif

@@ -1,0 +1,218 @@
+"""oracle/oracle.py -- TEST INFRASTRUCTURE ONLY.
+
+ctypes bindings for the CPU restatement in oracle/oracle.c.  Imported only by
+tests/, __graft_entry__.smoke() and bench.py's cpu_baseline leg -- never by the
+product package (forst_amd/), which has no CPU fallback.
+"""
+import ctypes
+import os
+import subprocess
+
+import numpy as np
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+_LIB_PATH = os.path.join(_HERE, "build", "liboracle.so")
+_lib = None
+
+kNoChecksum, kCRC32c, kxxHash, kxxHash64, kXXH3 = 0, 1, 2, 3, 4
+
+_u8p = ctypes.c_void_p
+
+
+def build():
+    subprocess.check_call(["make", "-s", "-C", _HERE])
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        if not os.path.exists(_LIB_PATH):
+            build()
+        L = ctypes.CDLL(_LIB_PATH)
+        u32, u64, sz, vp, i = (ctypes.c_uint32, ctypes.c_uint64, ctypes.c_size_t,
+                               ctypes.c_void_p, ctypes.c_int)
+        sigs = {
+            "oracle_crc32c_extend": (u32, [u32, vp, sz]),
+            "oracle_crc32c_extend_fast": (u32, [u32, vp, sz]),
+            "oracle_crc32c_value": (u32, [vp, sz]),
+            "oracle_crc32c_combine": (u32, [u32, u32, sz]),
+            "oracle_crc32c_mask": (u32, [u32]),
+            "oracle_crc32c_unmask": (u32, [u32]),
+            "oracle_crc32c_shift": (u32, [u32, u64]),
+            "oracle_xxh3_64": (u64, [vp, sz]),
+            "oracle_xxh32": (u32, [vp, sz, u32]),
+            "oracle_xxh64": (u64, [vp, sz, u64]),
+            "oracle_compute_builtin_checksum": (u32, [i, vp, sz]),
+            "oracle_compute_builtin_checksum_with_last_byte": (u32, [i, vp, sz, ctypes.c_uint8]),
+            "oracle_checksum_modifier_for_context": (u32, [u32, u64]),
+            "oracle_verify_block_checksum": (i, [i, vp, sz, u32, vp, vp]),
+            "oracle_block_checksum_batch": (None, [i, vp, vp, vp, vp, vp, vp, sz, i]),
+            "oracle_block_verify_batch": (u64, [i, vp, vp, vp, vp, vp, vp, sz, i]),
+            "oracle_crc32c_batch": (None, [vp, vp, vp, vp, sz, i]),
+            "oracle_xxh3_batch": (None, [vp, vp, vp, vp, sz, i]),
+            "oracle_wal_record_crc": (u32, [i, u32, vp, sz]),
+            "oracle_wal_framed_size": (u64, [vp, sz, i]),
+            "oracle_wal_frame": (u64, [vp, vp, sz, i, u32, vp, vp, vp, vp]),
+            "oracle_wal_verify": (u64, [vp, u64, vp, u64, vp, i]),
+            "oracle_splitmix64": (u64, [u64]),
+            "oracle_fill_stream": (None, [vp, u64, u64, u64]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype = res
+            f.argtypes = args
+        _lib = L
+    return _lib
+
+
+def _ptr(a):
+    if a is None:
+        return None
+    if isinstance(a, (bytes, bytearray)):
+        return ctypes.cast(ctypes.c_char_p(bytes(a)), ctypes.c_void_p).value
+    return a.ctypes.data
+
+
+def _buf(data):
+    """Return (pointer, length, keepalive) for bytes / numpy uint8 data."""
+    if isinstance(data, np.ndarray):
+        return data.ctypes.data, data.nbytes, data
+    b = ctypes.create_string_buffer(bytes(data), len(data) or 1)
+    return ctypes.addressof(b), len(data), b
+
+
+def crc32c_value(data):
+    p, n, _k = _buf(data)
+    return lib().oracle_crc32c_value(p, n)
+
+
+def crc32c_extend(crc, data, fast=False):
+    p, n, _k = _buf(data)
+    f = lib().oracle_crc32c_extend_fast if fast else lib().oracle_crc32c_extend
+    return f(crc, p, n)
+
+
+def crc32c_combine(a, b, blen):
+    return lib().oracle_crc32c_combine(a, b, blen)
+
+
+def crc32c_shift(state, nbytes):
+    return lib().oracle_crc32c_shift(state, nbytes)
+
+
+def mask(c):
+    return lib().oracle_crc32c_mask(c)
+
+
+def unmask(c):
+    return lib().oracle_crc32c_unmask(c)
+
+
+def xxh3_64(data):
+    p, n, _k = _buf(data)
+    return lib().oracle_xxh3_64(p, n)
+
+
+def xxh32(data, seed=0):
+    p, n, _k = _buf(data)
+    return lib().oracle_xxh32(p, n, seed)
+
+
+def xxh64(data, seed=0):
+    p, n, _k = _buf(data)
+    return lib().oracle_xxh64(p, n, seed)
+
+
+def compute_builtin_checksum(ctype, data):
+    p, n, _k = _buf(data)
+    return lib().oracle_compute_builtin_checksum(ctype, p, n)
+
+
+def compute_builtin_checksum_with_last_byte(ctype, data, last):
+    p, n, _k = _buf(data)
+    return lib().oracle_compute_builtin_checksum_with_last_byte(ctype, p, n, last & 0xFF)
+
+
+def checksum_modifier_for_context(base, offset):
+    return lib().oracle_checksum_modifier_for_context(base, offset)
+
+
+def verify_block_checksum(ctype, data, block_size, modifier=0):
+    p, _n, _k = _buf(data)
+    c = ctypes.c_uint32()
+    s = ctypes.c_uint32()
+    ok = lib().oracle_verify_block_checksum(ctype, p, block_size, modifier,
+                                            ctypes.byref(c), ctypes.byref(s))
+    return bool(ok), c.value, s.value
+
+
+def block_checksum_batch(ctype, base, offsets, sizes, last_bytes=None, modifiers=None,
+                         nthreads=1):
+    out = np.zeros(len(offsets), dtype=np.uint32)
+    lib().oracle_block_checksum_batch(ctype, _ptr(base), _ptr(offsets), _ptr(sizes),
+                                      _ptr(last_bytes), _ptr(modifiers), _ptr(out),
+                                      len(offsets), nthreads)
+    return out
+
+
+def block_verify_batch(ctype, base, offsets, sizes, modifiers=None, nthreads=1):
+    computed = np.zeros(len(offsets), dtype=np.uint32)
+    ok = np.zeros(len(offsets), dtype=np.uint8)
+    bad = lib().oracle_block_verify_batch(ctype, _ptr(base), _ptr(offsets), _ptr(sizes),
+                                          _ptr(modifiers), _ptr(computed), _ptr(ok),
+                                          len(offsets), nthreads)
+    return computed, ok, bad
+
+
+def crc32c_batch(base, offsets, lengths, nthreads=1):
+    out = np.zeros(len(offsets), dtype=np.uint32)
+    lib().oracle_crc32c_batch(_ptr(base), _ptr(offsets), _ptr(lengths), _ptr(out),
+                              len(offsets), nthreads)
+    return out
+
+
+def xxh3_batch(base, offsets, lengths, nthreads=1):
+    out = np.zeros(len(offsets), dtype=np.uint64)
+    lib().oracle_xxh3_batch(_ptr(base), _ptr(offsets), _ptr(lengths), _ptr(out),
+                            len(offsets), nthreads)
+    return out
+
+
+def wal_record_crc(rtype, log_number, payload):
+    p, n, _k = _buf(payload)
+    return lib().oracle_wal_record_crc(rtype, log_number, p, n)
+
+
+def wal_frame(payloads, lengths, recyclable=False, log_number=0):
+    """Frame logical records like log::Writer::AddRecord.  Returns
+    (buffer, phys_offsets, phys_lengths)."""
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    payloads = np.ascontiguousarray(payloads, dtype=np.uint8)
+    total = lib().oracle_wal_framed_size(_ptr(lengths), len(lengths), int(recyclable))
+    dst = np.zeros(total, dtype=np.uint8)
+    # upper bound on physical records: one per 32 KiB block + one per record
+    cap = len(lengths) + total // 32768 + 2
+    offs = np.zeros(cap, dtype=np.uint64)
+    lens = np.zeros(cap, dtype=np.uint32)
+    nphys = ctypes.c_uint64()
+    lib().oracle_wal_frame(_ptr(payloads), _ptr(lengths), len(lengths), int(recyclable),
+                           log_number, _ptr(dst), _ptr(offs), _ptr(lens),
+                           ctypes.byref(nphys))
+    n = nphys.value
+    return dst, offs[:n].copy(), lens[:n].copy()
+
+
+def wal_verify(buf, nthreads=1):
+    bad = ctypes.c_uint64()
+    n = lib().oracle_wal_verify(_ptr(buf), buf.nbytes, None, 0, ctypes.byref(bad), nthreads)
+    return n, bad.value
+
+
+def splitmix64(x):
+    return lib().oracle_splitmix64(x)
+
+
+def fill_stream(start, nbytes, seed):
+    out = np.empty(nbytes, dtype=np.uint8)
+    lib().oracle_fill_stream(_ptr(out), start, nbytes, seed)
+    return out

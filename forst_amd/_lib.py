@@ -1,0 +1,72 @@
+"""Loader for the in-tree HIP library forst_amd/lib/libforst_checksum.so.
+
+The product path has no CPU fallback: if the library (gfx950 code object) is
+missing or cannot be loaded, every entry point raises.
+"""
+import ctypes
+import os
+import subprocess
+
+_HERE = os.path.dirname(os.path.abspath(__file__))
+LIB_PATH = os.path.join(_HERE, "lib", "libforst_checksum.so")
+CSRC = os.path.join(_HERE, "csrc")
+
+_lib = None
+
+
+class ForstError(RuntimeError):
+    pass
+
+
+def build(jobs=8):
+    """Compile the HIP library for gfx950 (hipcc cross-compiles without a GPU)."""
+    subprocess.check_call(["make", "-s", "-C", CSRC, f"-j{jobs}"])
+
+
+def exported_symbols():
+    """C-ABI names declared in include/forst_checksum.h."""
+    import re
+
+    hdr = os.path.join(os.path.dirname(_HERE), "include", "forst_checksum.h")
+    with open(hdr) as f:
+        text = f.read()
+    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(forst_\w+)\(", text, re.M)))
+
+
+def lib():
+    global _lib
+    if _lib is not None:
+        return _lib
+    if not os.path.exists(LIB_PATH):
+        raise ForstError(
+            f"{LIB_PATH} is missing: build it with `make -C forst_amd/csrc` "
+            "(or __graft_entry__.build()); there is no CPU fallback")
+    L = ctypes.CDLL(LIB_PATH)
+    vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+    sigs = {
+        "forst_version": (ctypes.c_char_p, []),
+        "forst_last_error": (ctypes.c_char_p, []),
+        "forst_last_kernel": (ctypes.c_char_p, []),
+        "forst_init_device": (i, []),
+        "forst_block_checksum_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
+        "forst_block_trailer_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
+        "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
+        "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
+        "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
+        "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
+        "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
+        "forst_fill_stream": (i, [vp, u64, u64, u64, vp]),
+    }
+    for name, (res, args) in sigs.items():
+        f = getattr(L, name)
+        f.restype = res
+        f.argtypes = args
+    _lib = L
+    return L
+
+
+def check(rc):
+    if rc != 0:
+        msg = lib().forst_last_error().decode(errors="replace")
+        raise ForstError(f"forst call failed ({rc}): {msg}")
+    return rc

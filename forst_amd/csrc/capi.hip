@@ -1,0 +1,269 @@
+// forst_amd/csrc/capi.hip -- the C ABI (include/forst_checksum.h).
+//
+// Argument validation, per-device info cache and dispatch to the kernel
+// launchers.  No entry point allocates, copies or synchronises, so callers
+// may capture them into hipGraphs (cdna_hip_programming.md Guideline 9).
+#include <hip/hip_runtime.h>
+
+#include <cstdio>
+#include <cstring>
+#include <mutex>
+#include <string>
+
+#include "../../include/forst_checksum.h"
+#include "engine.h"
+
+#define FORST_API extern "C" __attribute__((visibility("default")))
+
+namespace forst {
+namespace {
+
+thread_local std::string g_last_error;
+thread_local const char* g_last_kernel = "";
+
+constexpr int kMaxDevices = 64;
+DeviceInfo g_info[kMaxDevices];
+std::once_flag g_once[kMaxDevices];
+
+int set_error(int code, const std::string& msg) {
+  g_last_error = msg;
+  return code;
+}
+
+int hip_status(hipError_t e, const char* what) {
+  if (e == hipSuccess) return FORST_OK;
+  return set_error(FORST_EHIP, std::string(what) + ": " + hipGetErrorString(e));
+}
+
+}  // namespace
+
+const DeviceInfo& device_info() {
+  static DeviceInfo none{-1, 0, false};
+  int dev = 0;
+  if (hipGetDevice(&dev) != hipSuccess || dev < 0 || dev >= kMaxDevices)
+    return none;
+  std::call_once(g_once[dev], [dev] {
+    DeviceInfo& d = g_info[dev];
+    d.device = dev;
+    d.num_cus = 0;
+    d.ok = false;
+    hipDeviceProp_t prop;
+    if (hipGetDeviceProperties(&prop, dev) == hipSuccess) {
+      d.num_cus = prop.multiProcessorCount > 0 ? prop.multiProcessorCount : 1;
+      d.ok = std::strncmp(prop.gcnArchName, "gfx950", 6) == 0;
+    }
+  });
+  return g_info[dev];
+}
+
+namespace {
+
+int check_device() {
+  const DeviceInfo& d = device_info();
+  if (d.device < 0) return set_error(FORST_ENODEV, "no HIP device");
+  if (!d.ok)
+    return set_error(FORST_ENODEV,
+                     "device is not gfx950 (MI355X); this engine ships gfx950 code only");
+  return FORST_OK;
+}
+
+bool aligned4(const void* p) { return (reinterpret_cast<uintptr_t>(p) & 3) == 0; }
+
+int check_block_args(const uint8_t* base, const uint64_t* offsets, const uint32_t* sizes,
+                     uint64_t n) {
+  if (n == 0) return FORST_OK;
+  if (!base || !offsets || !sizes)
+    return set_error(FORST_EINVAL, "base/offsets/sizes must be non-null");
+  if (!aligned4(base)) return set_error(FORST_EINVAL, "base must be 4-byte aligned");
+  return FORST_OK;
+}
+
+int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
+  int rc = check_device();
+  if (rc) return rc;
+  hipStream_t s = static_cast<hipStream_t>(stream);
+  hipError_t e;
+  switch (type) {
+    case FORST_kCRC32c:
+      e = launch_crc32c_blocks(mode, a, s, &g_last_kernel);
+      break;
+    case FORST_kXXH3:
+      e = launch_xxh3_blocks(mode, a, s, &g_last_kernel);
+      break;
+    case FORST_kNoChecksum:
+      e = launch_noop_blocks(mode, a, s, &g_last_kernel);
+      break;
+    case FORST_kxxHash:
+    case FORST_kxxHash64:
+      return set_error(FORST_EUNSUPPORTED,
+                       "kxxHash/kxxHash64 are not implemented by the GPU engine yet");
+    default:
+      // options_helper.h:34 IsSupportedChecksumType rejects > kXXH3
+      return set_error(FORST_EINVAL, "unknown ChecksumType " + std::to_string(type));
+  }
+  return hip_status(e, "kernel launch");
+}
+
+}  // namespace
+}  // namespace forst
+
+using namespace forst;
+
+FORST_API const char* forst_version(void) { return "forst-mi355x 0.1.0 (gfx950)"; }
+FORST_API const char* forst_last_error(void) { return g_last_error.c_str(); }
+FORST_API const char* forst_last_kernel(void) { return g_last_kernel; }
+
+FORST_API int forst_init_device(void) { return check_device(); }
+
+FORST_API int forst_block_checksum_batch(int checksum_type, const uint8_t* base,
+                                         uint64_t base_len, const uint64_t* offsets,
+                                         const uint32_t* sizes, const uint8_t* last_bytes,
+                                         const uint32_t* modifiers, uint32_t* out,
+                                         uint64_t n_blocks, void* stream) {
+  int rc = check_block_args(base, offsets, sizes, n_blocks);
+  if (rc) return rc;
+  if (n_blocks && !out) return set_error(FORST_EINVAL, "out must be non-null");
+  BlockArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = offsets;
+  a.sizes = sizes;
+  a.last_bytes = last_bytes;
+  a.modifiers = modifiers;
+  a.out32 = out;
+  a.n = n_blocks;
+  return dispatch_blocks(checksum_type, kModeCompute, a, stream);
+}
+
+FORST_API int forst_block_trailer_batch(int checksum_type, uint8_t* base, uint64_t base_len,
+                                        const uint64_t* offsets, const uint32_t* sizes,
+                                        const uint8_t* last_bytes, const uint32_t* modifiers,
+                                        uint32_t* out, uint64_t n_blocks, void* stream) {
+  int rc = check_block_args(base, offsets, sizes, n_blocks);
+  if (rc) return rc;
+  if (n_blocks && !last_bytes)
+    return set_error(FORST_EINVAL, "trailer mode needs last_bytes (compression types)");
+  BlockArgs a{};
+  a.base = base;
+  a.base_w = base;
+  a.base_len = base_len;
+  a.offsets = offsets;
+  a.sizes = sizes;
+  a.last_bytes = last_bytes;
+  a.modifiers = modifiers;
+  a.out32 = out;
+  a.n = n_blocks;
+  return dispatch_blocks(checksum_type, kModeTrailer, a, stream);
+}
+
+FORST_API int forst_block_verify_batch(int checksum_type, const uint8_t* base,
+                                       uint64_t base_len, const uint64_t* offsets,
+                                       const uint32_t* sizes, const uint32_t* modifiers,
+                                       uint32_t* computed, uint32_t* stored, uint8_t* ok,
+                                       unsigned long long* mismatches, uint64_t n_blocks,
+                                       void* stream) {
+  int rc = check_block_args(base, offsets, sizes, n_blocks);
+  if (rc) return rc;
+  BlockArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = offsets;
+  a.sizes = sizes;
+  a.modifiers = modifiers;
+  a.out32 = computed;
+  a.stored_out = stored;
+  a.ok_out = ok;
+  a.mismatches = mismatches;
+  a.n = n_blocks;
+  return dispatch_blocks(checksum_type, kModeVerify, a, stream);
+}
+
+FORST_API int forst_crc32c_batch(const uint8_t* base, uint64_t base_len,
+                                 const uint64_t* offsets, const uint32_t* lengths,
+                                 const uint32_t* init_crcs, uint32_t* out,
+                                 uint64_t n_buffers, void* stream) {
+  int rc = check_block_args(base, offsets, lengths, n_buffers);
+  if (rc) return rc;
+  if (n_buffers && !out) return set_error(FORST_EINVAL, "out must be non-null");
+  BlockArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = offsets;
+  a.sizes = lengths;
+  a.init_crcs = init_crcs;
+  a.out32 = out;
+  a.n = n_buffers;
+  return dispatch_blocks(FORST_kCRC32c, kModeRaw, a, stream);
+}
+
+FORST_API int forst_xxh3_64_batch(const uint8_t* base, uint64_t base_len,
+                                  const uint64_t* offsets, const uint32_t* lengths,
+                                  uint64_t* out, uint64_t n_buffers, void* stream) {
+  int rc = check_block_args(base, offsets, lengths, n_buffers);
+  if (rc) return rc;
+  if (n_buffers && !out) return set_error(FORST_EINVAL, "out must be non-null");
+  BlockArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = offsets;
+  a.sizes = lengths;
+  a.out64 = out;
+  a.n = n_buffers;
+  return dispatch_blocks(FORST_kXXH3, kModeRaw, a, stream);
+}
+
+FORST_API int forst_wal_verify_batch(const uint8_t* log, uint64_t log_len, uint64_t first_block,
+                                     uint64_t n_blocks, uint32_t log_number, uint8_t* status_out,
+                                     uint32_t* nrec_out, uint32_t* fail_off_out,
+                                     unsigned long long* bad_blocks, void* stream) {
+  if (n_blocks == 0) return FORST_OK;
+  if (!log || !aligned4(log)) return set_error(FORST_EINVAL, "log must be non-null, 4-byte aligned");
+  const uint64_t total_blocks = (log_len + 32767) / 32768;
+  if (first_block > total_blocks || n_blocks > total_blocks - first_block)
+    return set_error(FORST_EINVAL, "log block range outside log_len");
+  int rc = check_device();
+  if (rc) return rc;
+  WalArgs a{};
+  a.log = log;
+  a.log_len = log_len;
+  a.first_block = first_block;
+  a.n_blocks = n_blocks;
+  a.log_number = log_number;
+  a.status_out = status_out;
+  a.nrec_out = nrec_out;
+  a.fail_off_out = fail_off_out;
+  a.bad_blocks = bad_blocks;
+  return hip_status(launch_wal_verify(a, static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "wal_verify launch");
+}
+
+FORST_API int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
+                                         const uint64_t* header_offsets, uint64_t n_records,
+                                         int write_in_place, uint32_t* crc_out, void* stream) {
+  if (n_records == 0) return FORST_OK;
+  if (!log || !aligned4(log) || !header_offsets)
+    return set_error(FORST_EINVAL, "log/header_offsets must be non-null, log 4-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  WalArgs a{};
+  a.log = log;
+  a.log_w = log;
+  a.log_len = log_len;
+  a.header_offsets = header_offsets;
+  a.n_records = n_records;
+  a.write_in_place = write_in_place;
+  a.crc_out = crc_out;
+  return hip_status(launch_wal_record_crc(a, static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "wal_record_crc launch");
+}
+
+FORST_API int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
+                                void* stream) {
+  if (n == 0) return FORST_OK;
+  if (!dev || (reinterpret_cast<uintptr_t>(dev) & 7))
+    return set_error(FORST_EINVAL, "fill_stream needs an 8-byte aligned dev pointer");
+  int rc = check_device();
+  if (rc) return rc;
+  return hip_status(launch_fill_stream(dev, start, n, seed, static_cast<hipStream_t>(stream)),
+                    "fill_stream launch");
+}

@@ -1,0 +1,80 @@
+// forst_amd/csrc/device_common.h -- gfx950 device helpers shared by the kernels.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace forst {
+
+// Wave-uniform value (forces an SGPR; the compiler cannot prove that
+// threadIdx.x >> 6 is uniform on its own -- cdna_hip_programming.md T20).
+__device__ __forceinline__ uint32_t uniform(uint32_t v) {
+  return __builtin_amdgcn_readfirstlane(v);
+}
+__device__ __forceinline__ uint64_t uniform64(uint64_t v) {
+  uint32_t lo = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v));
+  uint32_t hi = __builtin_amdgcn_readfirstlane(static_cast<uint32_t>(v >> 32));
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// 16-byte vector with only 4-byte alignment: lowers to one global_load_dwordx4
+// on gfx950 (dword-aligned multi-dword loads are legal), so lane segments that
+// start at any dword boundary are read with one instruction.
+typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+
+__device__ __forceinline__ u32x4a4 ld16_a4(const uint8_t* p) {
+  return *reinterpret_cast<const u32x4a4*>(p);
+}
+__device__ __forceinline__ uint32_t ld4_a4(const uint8_t* p) {
+  return *reinterpret_cast<const uint32_t*>(p);
+}
+
+// Little-endian 32/64-bit read at any byte address, touching only the
+// dword-aligned words that overlap [p, p+4) / [p, p+8) (never a word that lies
+// entirely outside the requested bytes, so it cannot fault past a buffer end).
+// (Pointers are always derived from the kernel's buffer argument by pointer
+// arithmetic -- never rebuilt from integers -- so the compiler keeps them in
+// the global address space and emits global_load, not flat_load.)
+__device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
+  const uint32_t m = reinterpret_cast<uint64_t>(p) & 3;
+  const uint8_t* q = p - m;
+  const uint32_t lo = ld4_a4(q);
+  if (m == 0) return lo;
+  const uint32_t hi = ld4_a4(q + 4);
+  return __builtin_amdgcn_alignbyte(hi, lo, m);
+}
+__device__ __forceinline__ uint64_t ldu64(const uint8_t* p) {
+  const uint32_t m = reinterpret_cast<uint64_t>(p) & 3;
+  const uint8_t* q = p - m;
+  const uint32_t w0 = ld4_a4(q), w1 = ld4_a4(q + 4);
+  if (m == 0) return (static_cast<uint64_t>(w1) << 32) | w0;
+  const uint32_t w2 = ld4_a4(q + 8);
+  const uint32_t lo = __builtin_amdgcn_alignbyte(w1, w0, m);
+  const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, m);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+__device__ __forceinline__ uint32_t ldu8(const uint8_t* p) { return *p; }
+
+// util/crc32c.h:44-53
+__device__ __forceinline__ uint32_t crc_mask(uint32_t crc) {
+  return ((crc >> 15) | (crc << 17)) + 0xa282ead8u;
+}
+__device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {
+  const uint32_t rot = m - 0xa282ead8u;
+  return (rot >> 17) | (rot << 15);
+}
+// table/format.cc:559 ModifyChecksumForLastByte
+__device__ __forceinline__ uint32_t modify_for_last_byte(uint32_t v,
+                                                         uint32_t last) {
+  return v ^ ((last & 0xffu) * 0x6b9083d9u);
+}
+
+// Byte stores of a little-endian u32 at any address (trailer / WAL header).
+__device__ __forceinline__ void stu32_bytes(uint8_t* p, uint32_t v) {
+  p[0] = static_cast<uint8_t>(v);
+  p[1] = static_cast<uint8_t>(v >> 8);
+  p[2] = static_cast<uint8_t>(v >> 16);
+  p[3] = static_cast<uint8_t>(v >> 24);
+}
+
+}  // namespace forst

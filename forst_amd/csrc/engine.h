@@ -1,0 +1,74 @@
+// forst_amd/csrc/engine.h -- host-side launch interface between the C ABI
+// (capi.hip) and the kernel translation units.
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+namespace forst {
+
+// What a block launch does with each descriptor.
+enum BlockMode : int {
+  kModeCompute = 0,  // out = checksum(data, size, last) + modifier
+  kModeTrailer = 1,  // compute + write [last][LE32] at data+size
+  kModeVerify = 2,   // computed vs stored trailer (reader_common.cc:26)
+  kModeRaw = 3,      // crc32c::Extend(init, data, len) / XXH3_64bits
+};
+
+struct BlockArgs {
+  const uint8_t* base;
+  uint8_t* base_w;          // same buffer, writable (trailer mode)
+  uint64_t base_len;
+  const uint64_t* offsets;
+  const uint32_t* sizes;
+  const uint8_t* last_bytes;   // nullable
+  const uint32_t* modifiers;   // nullable
+  const uint32_t* init_crcs;   // nullable (raw CRC mode)
+  uint32_t* out32;             // nullable
+  uint64_t* out64;             // nullable (raw XXH3 mode)
+  uint32_t* stored_out;        // nullable (verify)
+  uint8_t* ok_out;             // nullable (verify)
+  unsigned long long* mismatches;  // nullable (verify)
+  uint64_t n;
+};
+
+struct WalArgs {
+  const uint8_t* log;
+  uint8_t* log_w;
+  uint64_t log_len;
+  uint64_t first_block;
+  uint64_t n_blocks;
+  uint32_t log_number;
+  uint8_t* status_out;
+  uint32_t* nrec_out;
+  uint32_t* fail_off_out;
+  unsigned long long* bad_blocks;
+  // writer side
+  const uint64_t* header_offsets;
+  uint64_t n_records;
+  int write_in_place;
+  uint32_t* crc_out;
+};
+
+struct DeviceInfo {
+  int device;
+  int num_cus;
+  bool ok;
+};
+const DeviceInfo& device_info();  // current device (lazily initialised)
+
+// Launchers (return hipError_t). `kernel_name` receives a static string.
+hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
+                                hipStream_t stream, const char** kernel_name);
+hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a,
+                              hipStream_t stream, const char** kernel_name);
+hipError_t launch_noop_blocks(int mode, const BlockArgs& a,
+                              hipStream_t stream, const char** kernel_name);
+hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
+                             const char** kernel_name);
+hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,
+                                 const char** kernel_name);
+hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n,
+                              uint64_t seed, hipStream_t stream);
+
+}  // namespace forst

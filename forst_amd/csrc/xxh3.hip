@@ -1,0 +1,461 @@
+// forst_amd/csrc/xxh3.hip -- XXH3_64bits (xxHash 0.8.1, seed 0) block kernels
+// for gfx950, one 64-lane wavefront per block.
+//
+// Long inputs (> 240 B, util/xxhash.h:5123-5208): each XXH3 accumulate step
+// adds a per-stripe contribution to 8 u64 accumulators, and within one
+// 1 KiB XXH3-block those additions commute (sums mod 2^64, xxhash.h:
+// 4924-4927).  So lane L takes 16 bytes (stripe L/4, accumulator pair L%4)
+// of every XXH3-block -- one fully coalesced 1 KiB global_load_dwordx4 per
+// XXH3-block -- and a 4-level xor butterfly sums the 16 stripes.  The
+// non-linear scramble (xxhash.h:4962-4977) is applied in order, per
+// accumulator, by the lanes that own it.  Short inputs (<= 240 B) run the
+// reference's length-class formulas redundantly on all lanes.
+#include "device_common.h"
+#include "engine.h"
+
+namespace forst {
+namespace {
+
+constexpr uint32_t kWaves = 4;  // 256-thread workgroups, no LDS
+constexpr uint32_t kThreads = kWaves * 64;
+
+#define P32_1 0x9E3779B1u
+#define P32_2 0x85EBCA77u
+#define P32_3 0xC2B2AE3Du
+#define P64_1 0x9E3779B185EBCA87ull
+#define P64_2 0xC2B2AE3D27D4EB4Full
+#define P64_3 0x165667B19E3779F9ull
+#define P64_4 0x85EBCA77C2B2AE63ull
+#define P64_5 0x27D4EB2F165667C5ull
+
+// util/xxhash.h:3644 XXH3_kSecret
+__device__ __constant__ const uint8_t kSecret[192] = {
+    0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c,
+    0xf7, 0x21, 0xad, 0x1c, 0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb,
+    0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3, 0x67, 0x1f, 0xcb, 0x79, 0xe6, 0x4e,
+    0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc, 0xff, 0x72, 0x21,
+    0xb8, 0x08, 0x46, 0x74, 0xf7, 0x43, 0x24, 0x8e, 0xe0, 0x35, 0x90, 0xe6,
+    0x81, 0x3a, 0x26, 0x4c, 0x3c, 0x28, 0x52, 0xbb, 0x91, 0xc3, 0x00, 0xcb,
+    0x88, 0xd0, 0x65, 0x8b, 0x1b, 0x53, 0x2e, 0xa3, 0x71, 0x64, 0x48, 0x97,
+    0xa2, 0x0d, 0xf9, 0x4e, 0x38, 0x19, 0xef, 0x46, 0xa9, 0xde, 0xac, 0xd8,
+    0xa8, 0xfa, 0x76, 0x3f, 0xe3, 0x9c, 0x34, 0x3f, 0xf9, 0xdc, 0xbb, 0xc7,
+    0xc7, 0x0b, 0x4f, 0x1d, 0x8a, 0x51, 0xe0, 0x4b, 0xcd, 0xb4, 0x59, 0x31,
+    0xc8, 0x9f, 0x7e, 0xc9, 0xd9, 0x78, 0x73, 0x64, 0xea, 0xc5, 0xac, 0x83,
+    0x34, 0xd3, 0xeb, 0xc3, 0xc5, 0x81, 0xa0, 0xff, 0xfa, 0x13, 0x63, 0xeb,
+    0x17, 0x0d, 0xdd, 0x51, 0xb7, 0xf0, 0xda, 0x49, 0xd3, 0x16, 0x55, 0x26,
+    0x29, 0xd4, 0x68, 0x9e, 0x2b, 0x16, 0xbe, 0x58, 0x7d, 0x47, 0xa1, 0xfc,
+    0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce, 0x45, 0xcb, 0x3a, 0x8f,
+    0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e,
+};
+
+__device__ __forceinline__ uint64_t sec64(uint32_t off) {
+  uint64_t v = 0;
+#pragma unroll
+  for (int i = 7; i >= 0; --i) v = (v << 8) | kSecret[off + i];
+  return v;
+}
+
+__device__ __forceinline__ uint64_t rotl64(uint64_t x, int r) {
+  return (x << r) | (x >> (64 - r));
+}
+__device__ __forceinline__ uint64_t mul128_fold64(uint64_t a, uint64_t b) {
+  const unsigned __int128 p = static_cast<unsigned __int128>(a) * b;
+  return static_cast<uint64_t>(p) ^ static_cast<uint64_t>(p >> 64);
+}
+__device__ __forceinline__ uint64_t mul32to64(uint64_t v) {
+  return static_cast<uint64_t>(static_cast<uint32_t>(v)) *
+         static_cast<uint64_t>(static_cast<uint32_t>(v >> 32));
+}
+__device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
+  h ^= h >> 33;
+  h *= P64_2;
+  h ^= h >> 29;
+  h *= P64_3;
+  h ^= h >> 32;
+  return h;
+}
+__device__ __forceinline__ uint64_t xxh3_avalanche(uint64_t h) {
+  h ^= h >> 37;
+  h *= 0x165667919E3779F9ull;
+  h ^= h >> 32;
+  return h;
+}
+__device__ __forceinline__ uint64_t rrmxmx(uint64_t h, uint64_t len) {
+  h ^= rotl64(h, 49) ^ rotl64(h, 24);
+  h *= 0x9FB21C651E98DF25ull;
+  h ^= (h >> 35) + len;
+  h *= 0x9FB21C651E98DF25ull;
+  return h ^ (h >> 28);
+}
+__device__ __forceinline__ uint64_t mix16B(const uint8_t* in, uint32_t s) {
+  return mul128_fold64(ldu64(in) ^ sec64(s), ldu64(in + 8) ^ sec64(s + 8));
+}
+
+// util/xxhash.h:3918-4139, seed 0 (uniform scalar code on every lane)
+__device__ uint64_t xxh3_short(const uint8_t* in, uint32_t len) {
+  if (len <= 16) {
+    if (len > 8) {
+      const uint64_t lo = ldu64(in) ^ (sec64(24) ^ sec64(32));
+      const uint64_t hi = ldu64(in + len - 8) ^ (sec64(40) ^ sec64(48));
+      const uint64_t acc = len + __builtin_bswap64(lo) + hi + mul128_fold64(lo, hi);
+      return xxh3_avalanche(acc);
+    }
+    if (len >= 4) {
+      const uint32_t in1 = ldu32(in), in2 = ldu32(in + len - 4);
+      const uint64_t in64 = in2 + (static_cast<uint64_t>(in1) << 32);
+      return rrmxmx(in64 ^ (sec64(8) ^ sec64(16)), len);
+    }
+    if (len) {
+      const uint32_t c1 = in[0], c2 = in[len >> 1], c3 = in[len - 1];
+      const uint32_t combined = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
+      const uint32_t bf = static_cast<uint32_t>(sec64(0)) ^
+                          static_cast<uint32_t>(sec64(4));
+      return xxh64_avalanche(static_cast<uint64_t>(combined ^ bf));
+    }
+    return xxh64_avalanche(sec64(56) ^ sec64(64));
+  }
+  if (len <= 128) {
+    uint64_t acc = len * P64_1, acc_end;
+    acc += mix16B(in, 0);
+    acc_end = mix16B(in + len - 16, 16);
+    if (len > 32) {
+      acc += mix16B(in + 16, 32);
+      acc_end += mix16B(in + len - 32, 48);
+      if (len > 64) {
+        acc += mix16B(in + 32, 64);
+        acc_end += mix16B(in + len - 48, 80);
+        if (len > 96) {
+          acc += mix16B(in + 48, 96);
+          acc_end += mix16B(in + len - 64, 112);
+        }
+      }
+    }
+    return xxh3_avalanche(acc + acc_end);
+  }
+  uint64_t acc = len * P64_1, acc_end;
+  const uint32_t nbRounds = len / 16;
+  for (uint32_t i = 0; i < 8; ++i) acc += mix16B(in + 16 * i, 16 * i);
+  acc_end = mix16B(in + len - 16, 136 - 17);
+  acc = xxh3_avalanche(acc);
+  for (uint32_t i = 8; i < nbRounds; ++i)
+    acc_end += mix16B(in + 16 * i, 16 * (i - 8) + 3);
+  return xxh3_avalanche(acc + acc_end);
+}
+
+// 16 bytes at an arbitrary address with dword-aligned loads + alignbyte.
+// `m` = address & 3 (wave-uniform), q = address & ~3.
+__device__ __forceinline__ void ld16u(const uint8_t* q, uint32_t m,
+                                      uint64_t& d0, uint64_t& d1) {
+  const u32x4a4 v = ld16_a4(q);
+  uint32_t x0 = v.x, x1 = v.y, x2 = v.z, x3 = v.w;
+  if (m) {
+    const uint32_t x4 = ld4_a4(q + 16);
+    x0 = __builtin_amdgcn_alignbyte(x1, x0, m);
+    x1 = __builtin_amdgcn_alignbyte(x2, x1, m);
+    x2 = __builtin_amdgcn_alignbyte(x3, x2, m);
+    x3 = __builtin_amdgcn_alignbyte(x4, x3, m);
+  }
+  d0 = (static_cast<uint64_t>(x1) << 32) | x0;
+  d1 = (static_cast<uint64_t>(x3) << 32) | x2;
+}
+
+__device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
+  const uint32_t lo = __shfl_xor(static_cast<uint32_t>(v), mask);
+  const uint32_t hi = __shfl_xor(static_cast<uint32_t>(v >> 32), mask);
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+
+// sum over the 16 lanes that share L%4 (lane bits 2..5)
+__device__ __forceinline__ uint64_t stripe_sum(uint64_t v) {
+  v += shfl_xor64(v, 4);
+  v += shfl_xor64(v, 8);
+  v += shfl_xor64(v, 16);
+  v += shfl_xor64(v, 32);
+  return v;
+}
+
+struct LaneKeys {
+  uint64_t k0, k1;    // accumulate keys for (stripe L/4, pair L%4)
+  uint64_t kl0, kl1;  // last-stripe keys (XXH_SECRET_LASTACC_START = 7)
+  uint64_t ks0, ks1;  // scramble keys for accumulators 2p, 2p+1
+  uint64_t km0, km1;  // merge keys (XXH_SECRET_MERGEACCS_START = 11)
+  uint64_t init0, init1;
+};
+
+__device__ __forceinline__ LaneKeys lane_keys(uint32_t lane) {
+  const uint32_t s = lane >> 2, p = lane & 3;
+  LaneKeys k;
+  k.k0 = sec64(8 * s + 16 * p);
+  k.k1 = sec64(8 * s + 16 * p + 8);
+  k.kl0 = sec64(192 - 64 - 7 + 16 * p);
+  k.kl1 = sec64(192 - 64 - 7 + 16 * p + 8);
+  k.ks0 = sec64(192 - 64 + 16 * p);
+  k.ks1 = sec64(192 - 64 + 16 * p + 8);
+  k.km0 = sec64(11 + 16 * p);
+  k.km1 = sec64(11 + 16 * p + 8);
+  // XXH3_INIT_ACC (xxhash.h:5188)
+  const uint64_t init[8] = {P32_3, P64_1, P64_2, P64_3,
+                            P64_4, P32_2, P64_5, P32_1};
+  k.init0 = p == 0 ? init[0] : p == 1 ? init[2] : p == 2 ? init[4] : init[6];
+  k.init1 = p == 0 ? init[1] : p == 1 ? init[3] : p == 2 ? init[5] : init[7];
+  return k;
+}
+
+__device__ __forceinline__ uint64_t scramble(uint64_t a, uint64_t key) {
+  a ^= a >> 47;
+  a ^= key;
+  return a * P32_1;
+}
+
+// XXH3_64bits(p, len); all arguments wave-uniform, every lane returns it.
+__device__ uint64_t wave_xxh3_64(const uint8_t* p, uint32_t len, uint32_t lane,
+                                 const LaneKeys& K) {
+  if (len <= 240) return xxh3_short(p, len);
+  const uint32_t s = lane >> 2;
+  const uint32_t nb = (len - 1) / 1024;
+  const uint32_t nbStripes = ((len - 1) - 1024 * nb) / 64;
+  const uint64_t A = reinterpret_cast<uint64_t>(p);
+  const uint32_t m = static_cast<uint32_t>(A & 3);
+  const uint8_t* q = p - m + 16 * lane;  // keeps the global address space
+  uint64_t acc0 = K.init0, acc1 = K.init1;
+  // full XXH3-blocks, 4 per round so 4 loads are in flight per lane
+  uint32_t g = 0;
+  for (; g + 4 <= nb; g += 4) {
+    uint64_t c0[4], c1[4];
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      uint64_t d0, d1;
+      ld16u(q + 1024 * (g + j), m, d0, d1);
+      const uint64_t dk0 = d0 ^ K.k0, dk1 = d1 ^ K.k1;
+      c0[j] = mul32to64(dk0) + d1;  // acc[2p]   += lo*hi(dk0) ; acc[2p] += d1
+      c1[j] = d0 + mul32to64(dk1);  // acc[2p+1] += d0 ; += lo*hi(dk1)
+    }
+#pragma unroll
+    for (int j = 0; j < 4; ++j) {
+      acc0 = scramble(acc0 + stripe_sum(c0[j]), K.ks0);
+      acc1 = scramble(acc1 + stripe_sum(c1[j]), K.ks1);
+    }
+  }
+  for (; g < nb; ++g) {
+    uint64_t d0, d1;
+    ld16u(q + 1024 * g, m, d0, d1);
+    const uint64_t dk0 = d0 ^ K.k0, dk1 = d1 ^ K.k1;
+    acc0 = scramble(acc0 + stripe_sum(mul32to64(dk0) + d1), K.ks0);
+    acc1 = scramble(acc1 + stripe_sum(d0 + mul32to64(dk1)), K.ks1);
+  }
+  // last partial XXH3-block: stripes [0, nbStripes), no scramble
+  {
+    uint64_t c0 = 0, c1 = 0;
+    if (s < nbStripes) {
+      uint64_t d0, d1;
+      ld16u(q + 1024 * nb, m, d0, d1);
+      const uint64_t dk0 = d0 ^ K.k0, dk1 = d1 ^ K.k1;
+      c0 = mul32to64(dk0) + d1;
+      c1 = d0 + mul32to64(dk1);
+    }
+    acc0 += stripe_sum(c0);
+    acc1 += stripe_sum(c1);
+  }
+  // last stripe at len-64 (xxhash.h:5146-5151), every lane does its pair
+  {
+    const uint8_t* lp = p + len - 64 + 16 * (lane & 3);
+    const uint32_t ml = static_cast<uint32_t>((A + len) & 3);  // == lp & 3
+    uint64_t d0, d1;
+    ld16u(lp - ml, ml, d0, d1);
+    const uint64_t dk0 = d0 ^ K.kl0, dk1 = d1 ^ K.kl1;
+    acc0 += mul32to64(dk0) + d1;
+    acc1 += d0 + mul32to64(dk1);
+  }
+  // XXH3_mergeAccs (xxhash.h:5164)
+  uint64_t t = mul128_fold64(acc0 ^ K.km0, acc1 ^ K.km1);
+  t += shfl_xor64(t, 1);
+  t += shfl_xor64(t, 2);
+  return xxh3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) xxh3_block_kernel(BlockArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const LaneKeys K = lane_keys(lane);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kWaves + wave; i < a.n;
+       i += nw) {
+    const uint64_t off = a.offsets[i];
+    const uint32_t size = a.sizes[i];
+    const uint8_t* p = a.base + off;
+    uint64_t need = size;
+    if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
+    if (MODE == kModeCompute && a.last_bytes == nullptr) need += 1;
+    const bool inb = off <= a.base_len && need <= a.base_len - off;
+    if (!inb) {
+      if (lane == 0) {
+        if (a.out32) a.out32[i] = 0;
+        if (MODE == kModeRaw && a.out64) a.out64[i] = 0;
+        if (MODE == kModeVerify) {
+          if (a.ok_out) a.ok_out[i] = 0;
+          if (a.stored_out) a.stored_out[i] = 0;
+          if (a.mismatches) atomicAdd(a.mismatches, 1ull);
+        }
+      }
+      continue;
+    }
+    const uint64_t h = wave_xxh3_64(p, size, lane, K);
+    if (MODE == kModeRaw) {
+      if (lane == 0) a.out64[i] = h;
+    } else if (MODE == kModeVerify) {
+      // ComputeBuiltinChecksum(kXXH3, data, size+1), format.cc:577-586
+      const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), p[size]);
+      const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
+      const uint32_t stored = ldu32(p + size + 1) - mod;
+      const bool ok = stored == computed;
+      if (lane == 0) {
+        if (a.out32) a.out32[i] = computed;
+        if (a.stored_out) a.stored_out[i] = stored;
+        if (a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
+      }
+    } else {
+      const uint32_t last = a.last_bytes ? a.last_bytes[i] : p[size];
+      const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
+      const uint32_t c = modify_for_last_byte(static_cast<uint32_t>(h), last) + mod;
+      if (lane == 0) {
+        if (a.out32) a.out32[i] = c;
+        if (MODE == kModeTrailer) {
+          uint8_t* w = a.base_w + off + size;
+          w[0] = static_cast<uint8_t>(last);
+          stu32_bytes(w + 1, c);
+        }
+      }
+    }
+  }
+}
+
+// kNoChecksum: computed value is always 0 (format.cc:588-590); the stored
+// trailer then only carries the context modifier.
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) noop_block_kernel(BlockArgs a) {
+  const uint64_t i0 = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x;
+  for (uint64_t i = i0; i < a.n; i += static_cast<uint64_t>(gridDim.x) * kThreads) {
+    const uint64_t off = a.offsets[i];
+    const uint32_t size = a.sizes[i];
+    uint64_t need = size;
+    if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
+    if (MODE == kModeCompute && a.last_bytes == nullptr) need += 1;
+    const bool inb = off <= a.base_len && need <= a.base_len - off;
+    const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
+    if (MODE == kModeVerify) {
+      const uint32_t stored = inb ? ldu32(a.base + off + size + 1) - mod : 1u;
+      const bool ok = inb && stored == 0;
+      if (a.out32) a.out32[i] = 0;
+      if (a.stored_out) a.stored_out[i] = inb ? stored : 0;
+      if (a.ok_out) a.ok_out[i] = ok;
+      if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
+    } else {
+      if (a.out32) a.out32[i] = inb ? mod : 0;
+      if (MODE == kModeTrailer && inb) {
+        uint8_t* w = a.base_w + off + size;
+        w[0] = a.last_bytes ? a.last_bytes[i] : w[0];
+        stu32_bytes(w + 1, mod);
+      }
+    }
+  }
+}
+
+}  // namespace
+
+hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
+                              const char** name) {
+  const DeviceInfo& di = device_info();
+  if (a.n == 0) return hipSuccess;
+  const uint64_t want = (a.n + kWaves - 1) / kWaves;
+  const uint32_t grid = static_cast<uint32_t>(
+      std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
+  switch (mode) {
+    case kModeCompute:
+      *name = "xxh3_block_kernel<compute>";
+      hipLaunchKernelGGL(xxh3_block_kernel<kModeCompute>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case kModeTrailer:
+      *name = "xxh3_block_kernel<trailer>";
+      hipLaunchKernelGGL(xxh3_block_kernel<kModeTrailer>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case kModeVerify:
+      *name = "xxh3_block_kernel<verify>";
+      hipLaunchKernelGGL(xxh3_block_kernel<kModeVerify>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    default:
+      *name = "xxh3_block_kernel<raw>";
+      hipLaunchKernelGGL(xxh3_block_kernel<kModeRaw>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+  }
+  return hipGetLastError();
+}
+
+hipError_t launch_noop_blocks(int mode, const BlockArgs& a, hipStream_t stream,
+                              const char** name) {
+  const DeviceInfo& di = device_info();
+  if (a.n == 0) return hipSuccess;
+  const uint64_t want = (a.n + kThreads - 1) / kThreads;
+  const uint32_t grid = static_cast<uint32_t>(
+      std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
+  switch (mode) {
+    case kModeCompute:
+      *name = "noop_block_kernel<compute>";
+      hipLaunchKernelGGL(noop_block_kernel<kModeCompute>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case kModeTrailer:
+      *name = "noop_block_kernel<trailer>";
+      hipLaunchKernelGGL(noop_block_kernel<kModeTrailer>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    default:
+      *name = "noop_block_kernel<verify>";
+      hipLaunchKernelGGL(noop_block_kernel<kModeVerify>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+  }
+  return hipGetLastError();
+}
+
+// ---------------------------------------------------------------------------
+// synthetic stream fill (bench/test utility)
+// ---------------------------------------------------------------------------
+namespace {
+__device__ __forceinline__ uint64_t splitmix64(uint64_t z) {
+  z = (z ^ (z >> 30)) * 0xBF58476D1CE4E5B9ull;
+  z = (z ^ (z >> 27)) * 0x94D049BB133111EBull;
+  return z ^ (z >> 31);
+}
+__global__ void __launch_bounds__(256) fill_stream_kernel(uint8_t* dst, uint64_t start,
+                                                          uint64_t n, uint64_t seed) {
+  // each thread produces one aligned 8-byte word of the stream
+  const uint64_t w0 = start >> 3;
+  const uint64_t w1 = (start + n + 7) >> 3;
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * blockDim.x;
+  for (uint64_t w = w0 + static_cast<uint64_t>(blockIdx.x) * blockDim.x + threadIdx.x;
+       w < w1; w += stride) {
+    const uint64_t v = splitmix64(seed + (w + 1) * 0x9E3779B97F4A7C15ull);
+    const uint64_t b0 = w << 3;
+    if (b0 >= start && b0 + 8 <= start + n && ((b0 - start) & 7) == 0) {
+      *reinterpret_cast<uint64_t*>(dst + (b0 - start)) = v;
+    } else {
+      for (int k = 0; k < 8; ++k) {
+        const uint64_t b = b0 + k;
+        if (b >= start && b < start + n) dst[b - start] = static_cast<uint8_t>(v >> (8 * k));
+      }
+    }
+  }
+}
+}  // namespace
+
+hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
+                              hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  const DeviceInfo& di = device_info();
+  const uint64_t words = (n + 15) / 8;
+  const uint32_t grid = static_cast<uint32_t>(
+      std::max<uint64_t>(1, std::min<uint64_t>((words + 255) / 256, uint64_t(di.num_cus) * 16)));
+  hipLaunchKernelGGL(fill_stream_kernel, dim3(grid), dim3(256), 0, stream, dev, start, n, seed);
+  return hipGetLastError();
+}
+
+}  // namespace forst

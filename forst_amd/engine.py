@@ -1,0 +1,183 @@
+"""Python mirror of the reference's checksum interface over the HIP engine.
+
+Names follow the reference (table/format.h, table/block_based/reader_common.h,
+util/crc32c.h, util/xxhash.h, db/log_reader.cc); every function is the batched
+GPU form of the reference's per-block CPU call and runs the gfx950 kernels in
+forst_amd/lib/libforst_checksum.so.  Device buffers are torch CUDA tensors
+(torch is only plumbing for device memory and streams).  Calls are enqueued on
+torch's current stream.
+"""
+import enum
+
+import torch
+
+from ._lib import check, lib
+
+
+class ChecksumType(enum.IntEnum):
+    """include/rocksdb/table.h:54-60"""
+    kNoChecksum = 0
+    kCRC32c = 1
+    kxxHash = 2
+    kxxHash64 = 3
+    kXXH3 = 4
+
+
+class WalStatus(enum.IntEnum):
+    """per-log-block outcome of forst_wal_verify_batch"""
+    OK = 0
+    BAD_CHECKSUM = 1
+    BAD_LENGTH = 2
+    ZERO_RECORD = 3
+    OLD_RECORD = 4
+
+
+GPU_CHECKSUM_TYPES = (ChecksumType.kNoChecksum, ChecksumType.kCRC32c, ChecksumType.kXXH3)
+
+
+def _p(t):
+    return None if t is None else t.data_ptr()
+
+
+def _stream(stream):
+    if stream is None:
+        return torch.cuda.current_stream().cuda_stream
+    if isinstance(stream, torch.cuda.Stream):
+        return stream.cuda_stream
+    return stream
+
+
+def _dev_u8(base):
+    assert base.is_cuda and base.dtype == torch.uint8 and base.is_contiguous()
+    return base
+
+
+def _desc(offsets, sizes):
+    assert offsets.is_cuda and offsets.dtype in (torch.int64, torch.uint64)
+    assert sizes.is_cuda and sizes.dtype in (torch.int32, torch.uint32)
+    assert offsets.is_contiguous() and sizes.is_contiguous()
+    assert offsets.numel() == sizes.numel()
+    return offsets.numel()
+
+
+def init_device():
+    check(lib().forst_init_device())
+
+
+def version():
+    return lib().forst_version().decode()
+
+
+def last_kernel():
+    return lib().forst_last_kernel().decode()
+
+
+def block_checksum_batch(ctype, base, offsets, sizes, last_bytes=None, modifiers=None,
+                         out=None, stream=None):
+    """ComputeBuiltinChecksumWithLastByte + ChecksumModifierForContext per block
+    (table/format.cc:594, table/format.h:119) -> uint32 tensor."""
+    n = _desc(offsets, sizes)
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=base.device)
+    check(lib().forst_block_checksum_batch(int(ctype), base.data_ptr(), base.numel(),
+                                           offsets.data_ptr(), sizes.data_ptr(),
+                                           _p(last_bytes), _p(modifiers), out.data_ptr(),
+                                           n, _stream(stream)))
+    return out
+
+
+def block_trailer_batch(ctype, base, offsets, sizes, last_bytes, modifiers=None, out=None,
+                        stream=None):
+    """Writes [type][LE32 checksum] after each block in place, as
+    BlockBasedTableBuilder::WriteMaybeCompressedBlock appends it."""
+    n = _desc(offsets, sizes)
+    _dev_u8(base)
+    check(lib().forst_block_trailer_batch(int(ctype), base.data_ptr(), base.numel(),
+                                          offsets.data_ptr(), sizes.data_ptr(),
+                                          last_bytes.data_ptr(), _p(modifiers), _p(out),
+                                          n, _stream(stream)))
+    return out
+
+
+def block_verify_batch(ctype, base, offsets, sizes, modifiers=None, computed=True,
+                       stored=True, ok=True, mismatches=None, stream=None):
+    """VerifyBlockChecksum per block (table/block_based/reader_common.cc:26).
+    Returns (computed, stored, ok, mismatches) tensors (None where not asked)."""
+    n = _desc(offsets, sizes)
+    _dev_u8(base)
+    dev = base.device
+    c = torch.empty(n, dtype=torch.uint32, device=dev) if computed is True else computed
+    s = torch.empty(n, dtype=torch.uint32, device=dev) if stored is True else stored
+    o = torch.empty(n, dtype=torch.uint8, device=dev) if ok is True else ok
+    if mismatches is None:
+        mismatches = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(lib().forst_block_verify_batch(int(ctype), base.data_ptr(), base.numel(),
+                                         offsets.data_ptr(), sizes.data_ptr(), _p(modifiers),
+                                         _p(c), _p(s), _p(o), _p(mismatches), n,
+                                         _stream(stream)))
+    return c, s, o, mismatches
+
+
+def crc32c_batch(base, offsets, lengths, init_crcs=None, out=None, stream=None):
+    """crc32c::Extend(init, data, n) per buffer (util/crc32c.h:25), unmasked."""
+    n = _desc(offsets, lengths)
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=base.device)
+    check(lib().forst_crc32c_batch(base.data_ptr(), base.numel(), offsets.data_ptr(),
+                                   lengths.data_ptr(), _p(init_crcs), out.data_ptr(), n,
+                                   _stream(stream)))
+    return out
+
+
+def xxh3_64_batch(base, offsets, lengths, out=None, stream=None):
+    """XXH3_64bits per buffer (util/xxhash.h:5311)."""
+    n = _desc(offsets, lengths)
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint64, device=base.device)
+    check(lib().forst_xxh3_64_batch(base.data_ptr(), base.numel(), offsets.data_ptr(),
+                                    lengths.data_ptr(), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def wal_verify_batch(log, log_number=0, first_block=0, n_blocks=None, bad_blocks=None,
+                     stream=None):
+    """Physical-record CRC verification of 32 KiB log blocks
+    (db/log_reader.cc:450-531).  Returns (status, nrec, fail_off, bad_blocks)."""
+    _dev_u8(log)
+    total = (log.numel() + 32767) // 32768
+    if n_blocks is None:
+        n_blocks = total - first_block
+    dev = log.device
+    status = torch.empty(n_blocks, dtype=torch.uint8, device=dev)
+    nrec = torch.empty(n_blocks, dtype=torch.uint32, device=dev)
+    fail = torch.empty(n_blocks, dtype=torch.uint32, device=dev)
+    if bad_blocks is None:
+        bad_blocks = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(lib().forst_wal_verify_batch(log.data_ptr(), log.numel(), first_block, n_blocks,
+                                       log_number, status.data_ptr(), nrec.data_ptr(),
+                                       fail.data_ptr(), bad_blocks.data_ptr(), _stream(stream)))
+    return status, nrec, fail, bad_blocks
+
+
+def wal_record_crc_batch(log, header_offsets, write_in_place=True, out=None, stream=None):
+    """log::Writer::EmitPhysicalRecord CRC (db/log_writer.cc:228-263) for
+    headers already laid out in `log`."""
+    _dev_u8(log)
+    n = header_offsets.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=log.device)
+    check(lib().forst_wal_record_crc_batch(log.data_ptr(), log.numel(),
+                                           header_offsets.data_ptr(), n, int(write_in_place),
+                                           out.data_ptr(), _stream(stream)))
+    return out
+
+
+def fill_stream(dev_u8, start, seed, stream=None):
+    """Synthetic splitmix64 byte stream written on the device."""
+    _dev_u8(dev_u8)
+    check(lib().forst_fill_stream(dev_u8.data_ptr(), start, dev_u8.numel(), seed,
+                                  _stream(stream)))
+    return dev_u8

@@ -1,0 +1,99 @@
+"""SST- and WAL-shaped synthetic batches on the device.
+
+Blocks are packed back-to-back exactly as BlockBasedTableBuilder writes them
+(payload n_i bytes, compression-type byte, LE32 checksum; offset_{i+1} =
+offset_i + n_i + 5), so block starts are deliberately unaligned.  Payload
+bytes are the splitmix64 stream of the config's seed (byte i of the buffer is
+byte i of the stream); trailers are written by the engine's own trailer kernel
+(write side) and then read back by the verify kernel (read side).
+"""
+from dataclasses import dataclass
+
+import numpy as np
+import torch
+
+from . import engine
+
+TRAILER = 5  # table/block_based/block_based_table_reader.h:75 kBlockTrailerSize
+
+# BASELINE.json configs (seeds from SURVEY.md §8d)
+SEEDS = {"C1": 0xF0E5700001, "C2": 0xF0E5700002, "C3": 0xF0E5700003,
+         "C4": 0xF0E5700004, "C5": 0xF0E5700005}
+
+
+def _splitmix(z):
+    z = np.asarray(z, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        z = (z ^ (z >> np.uint64(30))) * np.uint64(0xBF58476D1CE4E5B9)
+        z = (z ^ (z >> np.uint64(27))) * np.uint64(0x94D049BB133111EB)
+        return z ^ (z >> np.uint64(31))
+
+
+def block_sizes(n, spec, seed):
+    """n block payload sizes.
+    spec: int            -> all equal
+          tuple of ints  -> equal shares of each class, shuffled (C3)
+          ("dev", b)     -> uniform in [0.9 b, b] (block_size_deviation=10, C3b)
+    """
+    idx = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        keys = _splitmix(np.uint64(seed ^ 0x5EED5EED5EED) + idx * np.uint64(0x9E3779B97F4A7C15))
+    if isinstance(spec, int):
+        return np.full(n, spec, dtype=np.uint32)
+    if isinstance(spec, tuple) and spec and spec[0] == "dev":
+        b = int(spec[1])
+        lo = (b * 9) // 10
+        return (lo + (keys % np.uint64(b - lo + 1))).astype(np.uint32)
+    classes = np.array(spec, dtype=np.uint32)
+    perm = np.argsort(keys, kind="stable")
+    out = np.empty(n, dtype=np.uint32)
+    out[perm] = classes[np.arange(n) % len(classes)]
+    return out
+
+
+@dataclass
+class SstBatch:
+    base: torch.Tensor      # uint8 [total]  (device)
+    offsets: torch.Tensor   # int64 [n]      (device)
+    sizes: torch.Tensor     # int32 [n]      (device)
+    types: torch.Tensor     # uint8 [n]      (device) compression type bytes
+    n: int
+    total: int
+    payload_bytes: int      # sum of sizes
+    seed: int
+
+    @property
+    def checksummed_bytes(self):
+        """bytes covered by the block checksums: payload + type byte"""
+        return self.payload_bytes + self.n
+
+
+def make_sst_batch(n, spec, seed, ctype=engine.ChecksumType.kCRC32c, device="cuda",
+                   write_trailers=True, modifiers=None, sizes=None):
+    if sizes is None:
+        sizes = block_sizes(n, spec, seed)
+    sizes = np.asarray(sizes, dtype=np.uint32)
+    offs = np.zeros(n, dtype=np.int64)
+    if n > 1:
+        offs[1:] = np.cumsum(sizes[:-1].astype(np.int64) + TRAILER)
+    total = int(offs[-1]) + int(sizes[-1]) + TRAILER if n else 0
+    alloc = max(16, (total + 255) // 256 * 256)
+    base = torch.empty(alloc, dtype=torch.uint8, device=device)
+    engine.fill_stream(base, 0, seed)
+    base = base[:total] if total else base[:0]
+    d_offs = torch.from_numpy(offs).to(device)
+    d_sizes = torch.from_numpy(sizes.astype(np.int32)).to(device)
+    types = torch.zeros(n, dtype=torch.uint8, device=device)  # kNoCompression
+    b = SstBatch(base, d_offs, d_sizes, types, n, total, int(sizes.astype(np.int64).sum()), seed)
+    if write_trailers and n:
+        engine.block_trailer_batch(ctype, base, d_offs, d_sizes, types, modifiers)
+    return b
+
+
+def log_uniform_lengths(n, lo, hi, seed):
+    """WAL record lengths, log-uniform in [lo, hi] (config C5)."""
+    idx = np.arange(n, dtype=np.uint64)
+    with np.errstate(over="ignore"):
+        k = _splitmix(np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15))
+    u = (k >> np.uint64(11)).astype(np.float64) / float(1 << 53)
+    return np.exp(np.log(lo) + u * (np.log(hi) - np.log(lo))).astype(np.uint32)

@@ -1,0 +1,139 @@
+// include/forst/checksum_engine.h -- C++ host shim over the C ABI, in the
+// reference's own vocabulary (namespace forstdb, ChecksumType, Status), so a
+// ForSt call site can switch from the per-block CPU functions to batched GPU
+// launches without changing types:
+//
+//   reference (per block, CPU)                      this shim (per batch, GPU)
+//   ComputeBuiltinChecksumWithLastByte + modifier   BlockChecksumEngine::ComputeChecksums
+//     (table/format.cc:594, format.h:119)
+//   WriteMaybeCompressedBlock trailer               BlockChecksumEngine::WriteTrailers
+//     (block_based_table_builder.cc:1340-1360)
+//   VerifyBlockChecksum (reader_common.cc:26)       BlockChecksumEngine::VerifyBlocks
+//   crc32c::Mask/Unmask (util/crc32c.h:44-53),      forstdb::crc32c::Mask/Unmask,
+//   ChecksumModifierForContext (format.h:119)       forstdb::ChecksumModifierForContext
+//
+// Statistics hooks mirror BLOCK_CHECKSUM_COMPUTE_COUNT / _MISMATCH_COUNT
+// (include/rocksdb/statistics.h:440,444).
+#pragma once
+
+#include <cstdint>
+#include <string>
+#include <vector>
+
+#include "../forst_checksum.h"
+
+namespace forstdb {
+
+// include/rocksdb/table.h:54-60
+enum ChecksumType : char {
+  kNoChecksum = 0x0,
+  kCRC32c = 0x1,
+  kxxHash = 0x2,
+  kxxHash64 = 0x3,
+  kXXH3 = 0x4,
+};
+
+// Minimal Status with the reference's code names and ToString() format
+// ("Corruption: <msg>", include/rocksdb/status.h / util/status.cc).
+class Status {
+ public:
+  enum Code { kOk = 0, kCorruption = 2, kNotSupported = 3, kInvalidArgument = 4,
+              kIOError = 5 };
+  Status() : code_(kOk) {}
+  static Status OK() { return Status(); }
+  static Status Corruption(const std::string& m) { return Status(kCorruption, m); }
+  static Status NotSupported(const std::string& m) { return Status(kNotSupported, m); }
+  static Status InvalidArgument(const std::string& m) { return Status(kInvalidArgument, m); }
+  static Status IOError(const std::string& m) { return Status(kIOError, m); }
+  bool ok() const { return code_ == kOk; }
+  bool IsCorruption() const { return code_ == kCorruption; }
+  Code code() const { return code_; }
+  const std::string& message() const { return msg_; }
+  std::string ToString() const;
+
+ private:
+  Status(Code c, std::string m) : code_(c), msg_(std::move(m)) {}
+  Code code_;
+  std::string msg_;
+};
+
+namespace crc32c {
+inline uint32_t Mask(uint32_t crc) { return ((crc >> 15) | (crc << 17)) + 0xa282ead8ul; }
+inline uint32_t Unmask(uint32_t m) {
+  uint32_t rot = m - 0xa282ead8ul;
+  return (rot >> 17) | (rot << 15);
+}
+}  // namespace crc32c
+
+// table/format.h:119
+inline uint32_t ChecksumModifierForContext(uint32_t base_context_checksum, uint64_t offset) {
+  uint32_t all_or_nothing = uint32_t{0} - (base_context_checksum != 0);
+  uint32_t modifier =
+      base_context_checksum ^ (static_cast<uint32_t>(offset) + static_cast<uint32_t>(offset >> 32));
+  return modifier & all_or_nothing;
+}
+
+// options/options_helper.h:34 IsSupportedChecksumType
+inline bool IsSupportedChecksumType(ChecksumType t) { return t >= kNoChecksum && t <= kXXH3; }
+// ... and what the GPU engine implements today
+bool GpuSupportsChecksumType(ChecksumType t);
+
+// reader_common.cc:55-60 message, CRC values unmasked by the caller.
+std::string BlockChecksumMismatchMessage(ChecksumType type, uint32_t stored, uint32_t computed,
+                                         bool context_removed, const std::string& file_name,
+                                         uint64_t offset, uint64_t block_size);
+
+struct ChecksumStats {
+  uint64_t block_checksum_compute_count = 0;   // BLOCK_CHECKSUM_COMPUTE_COUNT
+  uint64_t block_checksum_mismatch_count = 0;  // BLOCK_CHECKSUM_MISMATCH_COUNT
+};
+
+// A batch of blocks resident in device memory.  Block i occupies
+// base[offsets[i] .. offsets[i] + sizes[i] + 5) (payload, type byte, LE32).
+struct DeviceBlockBatch {
+  const uint8_t* base = nullptr;      // device
+  uint64_t base_len = 0;
+  const uint64_t* offsets = nullptr;  // device
+  const uint32_t* sizes = nullptr;    // device
+  uint64_t n = 0;
+};
+
+class BlockChecksumEngine {
+ public:
+  explicit BlockChecksumEngine(void* hip_stream = nullptr) : stream_(hip_stream) {}
+  ~BlockChecksumEngine();
+  BlockChecksumEngine(const BlockChecksumEngine&) = delete;
+  BlockChecksumEngine& operator=(const BlockChecksumEngine&) = delete;
+
+  // Write side.  last_bytes / modifiers are device arrays (modifiers may be
+  // null for format_version <= 5).  out is a device array of n.
+  Status ComputeChecksums(ChecksumType type, const DeviceBlockBatch& b, const uint8_t* last_bytes,
+                          const uint32_t* modifiers, uint32_t* out);
+  Status WriteTrailers(ChecksumType type, const DeviceBlockBatch& b, const uint8_t* last_bytes,
+                       const uint32_t* modifiers, uint32_t* out);
+
+  // Read side: VerifyBlockChecksum over the batch.  file_offsets/modifiers
+  // describe each block's position in `file_name` (host arrays, used for the
+  // context modifier and the error message).  Synchronises the stream.
+  // Returns OK, or the exact Corruption status the reference returns for the
+  // FIRST failing block; every failing index is appended to *failed.
+  Status VerifyBlocks(ChecksumType type, uint32_t base_context_checksum, const DeviceBlockBatch& b,
+                      const std::string& file_name, const std::vector<uint64_t>& file_offsets,
+                      std::vector<uint64_t>* failed = nullptr);
+
+  const ChecksumStats& stats() const { return stats_; }
+
+ private:
+  Status EnsureScratch(uint64_t n);
+  void* stream_;
+  ChecksumStats stats_;
+  // device scratch for verify
+  uint32_t* d_computed_ = nullptr;
+  uint32_t* d_stored_ = nullptr;
+  uint8_t* d_ok_ = nullptr;
+  uint32_t* d_mod_ = nullptr;
+  unsigned long long* d_bad_ = nullptr;
+  uint64_t cap_ = 0;
+};
+
+}  // namespace forstdb

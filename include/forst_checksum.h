@@ -1,0 +1,171 @@
+/* include/forst_checksum.h -- C ABI of the MI355X (gfx950) block-checksum engine.
+ *
+ * Drop-in device boundary for ForSt's built-in checksum hot path.  Each entry
+ * point replaces a per-block (or per-record) CPU call of the reference with one
+ * batched, stream-ordered GPU launch over thousands of independent blocks:
+ *
+ *   forst_block_checksum_batch  <- ComputeBuiltinChecksumWithLastByte +
+ *                                  ChecksumModifierForContext
+ *                                  (table/format.h:309, table/format.h:119),
+ *                                  as called by BlockBasedTableBuilder::
+ *                                  WriteMaybeCompressedBlock
+ *                                  (table/block_based/block_based_table_builder.cc:1340-1345)
+ *   forst_block_trailer_batch   <- the same + EncodeFixed32 of the 5-byte
+ *                                  trailer [type][LE32 checksum]
+ *                                  (block_based_table_builder.cc:1340-1360)
+ *   forst_block_verify_batch    <- VerifyBlockChecksum
+ *                                  (table/block_based/reader_common.h:33,
+ *                                  reader_common.cc:26-62) as called by
+ *                                  BlockFetcher::ProcessTrailerIfPresent
+ *                                  (table/block_fetcher.cc:32) and the batch
+ *                                  sites BlockBasedTable::VerifyChecksumInBlocks
+ *                                  (block_based_table_reader.cc:2491) and
+ *                                  RetrieveMultipleBlocks
+ *                                  (block_based_table_reader_sync_and_async.h:225)
+ *   forst_crc32c_batch          <- crc32c::Extend / crc32c::Value
+ *                                  (util/crc32c.h:25, :35)
+ *   forst_xxh3_64_batch         <- XXH3_64bits (util/xxhash.h:933/:5311)
+ *   forst_wal_verify_batch      <- log::Reader::ReadPhysicalRecord CRC check
+ *                                  (db/log_reader.cc:450-531), one 32 KiB log
+ *                                  block per wave
+ *   forst_wal_record_crc_batch  <- log::Writer::EmitPhysicalRecord CRC
+ *                                  (db/log_writer.cc:228-263)
+ *
+ * Conventions
+ *  - All array/buffer pointers are DEVICE pointers (hipMalloc'd, or host
+ *    memory registered/mapped so the GPU can read it).  The caller owns every
+ *    buffer.  `stream` is a hipStream_t (NULL = default stream).  Calls are
+ *    asynchronous and stream-ordered; no call allocates, copies or
+ *    synchronises, so a caller may capture them in a hipGraph.
+ *  - `base` must be 4-byte aligned; blocks live at base + offsets[i] and may
+ *    start at any byte (SST blocks are packed back-to-back with 5-byte
+ *    trailers, so starts are unaligned).  base_len bounds every access: a
+ *    descriptor that reaches past base_len is reported as a failure
+ *    (ok[i] = 0, counted in *mismatches) instead of being read.
+ *  - Per-block checksum mismatch is data, not an error.  Return values are
+ *    FORST_OK or a negative FORST_E* code for invalid arguments / HIP errors.
+ *  - Thread safety: every entry point is reentrant; concurrent calls on
+ *    different streams are independent (no global mutable state besides the
+ *    immutable per-device table cache set up by forst_init_device()).
+ */
+#ifndef FORST_CHECKSUM_H_
+#define FORST_CHECKSUM_H_
+
+#include <stddef.h>
+#include <stdint.h>
+
+#ifdef __cplusplus
+extern "C" {
+#endif
+
+/* ChecksumType values -- include/rocksdb/table.h:54-60 (on-disk footer byte). */
+enum forst_checksum_type {
+  FORST_kNoChecksum = 0,
+  FORST_kCRC32c = 1,
+  FORST_kxxHash = 2,
+  FORST_kxxHash64 = 3,
+  FORST_kXXH3 = 4
+};
+
+/* return codes */
+#define FORST_OK 0
+#define FORST_EINVAL (-1)        /* bad pointer / size / alignment */
+#define FORST_EUNSUPPORTED (-2)  /* ChecksumType not handled by the GPU engine */
+#define FORST_EHIP (-3)          /* HIP runtime error (see forst_last_error) */
+#define FORST_ENODEV (-4)        /* no gfx950 device / code object not loadable */
+
+/* WAL per-log-block status (forst_wal_verify_batch) -- mirrors the reader's
+ * outcomes of ReadPhysicalRecord (db/log_reader.h kBadRecord*, kEof). */
+#define FORST_WAL_OK 0           /* all records good up to padding / block end */
+#define FORST_WAL_BAD_CHECKSUM 1 /* kBadRecordChecksum: rest of block dropped */
+#define FORST_WAL_BAD_LENGTH 2   /* kBadRecordLen: header+length past block end */
+#define FORST_WAL_ZERO_RECORD 3  /* kZeroType && length==0 (preallocated space) */
+#define FORST_WAL_OLD_RECORD 4   /* recyclable header with another log number */
+
+/* Library / device management. */
+const char* forst_version(void);
+const char* forst_last_error(void); /* thread-local message of the last failure */
+/* Optional eager init of the current device (loads code object, caches the
+ * CU count).  Every entry point does this lazily; call it up front to keep
+ * first-call latency out of a timed region. */
+int forst_init_device(void);
+
+/* Write side (a7 + a8): out[i] = ComputeBuiltinChecksumWithLastByte(type,
+ *   base+offsets[i], sizes[i], last) + modifiers[i]
+ * where last = last_bytes ? last_bytes[i] : base[offsets[i] + sizes[i]] and
+ * modifiers may be NULL (format_version <= 5). */
+int forst_block_checksum_batch(int checksum_type, const uint8_t* base,
+                               uint64_t base_len, const uint64_t* offsets,
+                               const uint32_t* sizes, const uint8_t* last_bytes,
+                               const uint32_t* modifiers, uint32_t* out,
+                               uint64_t n_blocks, void* stream);
+
+/* Write side with the trailer materialised in place: for every block writes
+ * base[off+size] = last_bytes[i] and base[off+size+1 .. +5) = LE32(checksum)
+ * (the bytes WriteMaybeCompressedBlock appends).  `out` may be NULL. */
+int forst_block_trailer_batch(int checksum_type, uint8_t* base,
+                              uint64_t base_len, const uint64_t* offsets,
+                              const uint32_t* sizes, const uint8_t* last_bytes,
+                              const uint32_t* modifiers, uint32_t* out,
+                              uint64_t n_blocks, void* stream);
+
+/* Read side (a9): for every block (serialized size sizes[i] + 5 at
+ * base+offsets[i]): computed = ComputeBuiltinChecksum(type, data, size+1);
+ * stored = DecodeFixed32(data+size+1) - modifiers[i]; ok = stored==computed.
+ * computed / stored / ok may be NULL.  *mismatches (device counter, may be
+ * NULL) is INCREMENTED by the number of failing blocks. */
+int forst_block_verify_batch(int checksum_type, const uint8_t* base,
+                             uint64_t base_len, const uint64_t* offsets,
+                             const uint32_t* sizes, const uint32_t* modifiers,
+                             uint32_t* computed, uint32_t* stored, uint8_t* ok,
+                             unsigned long long* mismatches, uint64_t n_blocks,
+                             void* stream);
+
+/* out[i] = crc32c::Extend(init_crcs ? init_crcs[i] : 0, base+offsets[i],
+ * lengths[i])  (unmasked, as util/crc32c.h returns it). */
+int forst_crc32c_batch(const uint8_t* base, uint64_t base_len,
+                       const uint64_t* offsets, const uint32_t* lengths,
+                       const uint32_t* init_crcs, uint32_t* out,
+                       uint64_t n_buffers, void* stream);
+
+/* out[i] = XXH3_64bits(base+offsets[i], lengths[i])  (xxHash 0.8.1, seed 0). */
+int forst_xxh3_64_batch(const uint8_t* base, uint64_t base_len,
+                        const uint64_t* offsets, const uint32_t* lengths,
+                        uint64_t* out, uint64_t n_buffers, void* stream);
+
+/* WAL replay (a13): log blocks [first_block, first_block + n_blocks) of the
+ * log image `log` (log_len bytes; the last block may be short).  One entry
+ * per log block: status_out (FORST_WAL_*), nrec_out = physical records whose
+ * CRC verified before the first failure, fail_off_out = byte offset in the
+ * block of the failing header (or of the end of parsing).  Any out may be
+ * NULL.  *bad_blocks (device counter, may be NULL) += blocks with status !=
+ * FORST_WAL_OK && != FORST_WAL_ZERO_RECORD. */
+int forst_wal_verify_batch(const uint8_t* log, uint64_t log_len,
+                           uint64_t first_block, uint64_t n_blocks,
+                           uint32_t log_number, uint8_t* status_out,
+                           uint32_t* nrec_out, uint32_t* fail_off_out,
+                           unsigned long long* bad_blocks, void* stream);
+
+/* WAL write side (a12): masked record CRC for physical records whose header
+ * (7 or 11 bytes, type already in byte 6, log number in 7..10 when
+ * recyclable) starts at log + header_offsets[i] and whose payload follows
+ * it; writes the CRC into header bytes 0..3 when write_in_place != 0 and to
+ * crc_out[i] when crc_out != NULL. */
+int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
+                               const uint64_t* header_offsets,
+                               uint64_t n_records, int write_in_place,
+                               uint32_t* crc_out, void* stream);
+
+/* Bench/test utility: fill dev[0 .. n) with bytes [start, start+n) of the
+ * splitmix64 stream `seed` (SURVEY.md §8d synthetic inputs). */
+int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
+                      void* stream);
+
+/* Kernel timing hooks for bench.py: name of the kernel launched by the last
+ * call on this thread and the launch configuration used. */
+const char* forst_last_kernel(void);
+
+#ifdef __cplusplus
+}
+#endif
+#endif /* FORST_CHECKSUM_H_ */

@@ -1,0 +1,337 @@
+"""GPU parity: HIP kernels (through the C ABI) vs the pinned CPU oracle.
+
+Bit-exact for every case (integer/byte work).  Covers the reference's edge
+cases: empty batches and zero-length blocks, unaligned starts (every start
+alignment), lengths around every internal boundary (16/32/64/240/1024/4096),
+blocks at the very start/end of the buffer, context modifiers (fv6),
+corruption detection, out-of-range descriptors, WAL framing with all record
+types, and the full-size configs through size-independent properties.
+"""
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from forst_amd import engine, workload  # noqa: E402
+from forst_amd.engine import ChecksumType as CT  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+
+DEV = "cuda"
+
+
+def d(a, dtype=None):
+    t = torch.from_numpy(np.ascontiguousarray(a))
+    if dtype is not None:
+        t = t.to(dtype)
+    return t.to(DEV)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+@pytest.fixture(scope="module")
+def golden(ref_vectors):
+    v, blob = ref_vectors
+    arr = np.frombuffer(blob, dtype=np.uint8).copy()
+    offs = np.array([r["off"] for r in v["vectors"]], dtype=np.int64)
+    lens = np.array([r["n"] for r in v["vectors"]], dtype=np.int32)
+    return v, arr, d(arr), d(offs), d(lens)
+
+
+def test_library_loads_and_reports_gfx950():
+    engine.init_device()
+    assert "gfx950" in engine.version()
+
+
+def test_crc32c_raw_golden(golden):
+    v, arr, base, offs, lens = golden
+    out = host(engine.crc32c_batch(base, offs, lens)).astype(np.uint64)
+    want = np.array([r["crc32c"] for r in v["vectors"]], dtype=np.uint64)
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, [(v["vectors"][i]["n"], v["vectors"][i]["off"]) for i in bad[:10]]
+
+
+def test_crc32c_extend_with_init(golden):
+    v, arr, base, offs, lens = golden
+    rng = np.random.default_rng(11)
+    init = rng.integers(0, 2**32, len(v["vectors"]), dtype=np.uint64).astype(np.uint32)
+    out = host(engine.crc32c_batch(base, offs, lens, init_crcs=d(init.view(np.int32))))
+    for k, r in enumerate(v["vectors"]):
+        want = O.crc32c_extend(int(init[k]), arr[r["off"]:r["off"] + r["n"]])
+        assert int(out[k]) == want, (r["n"], r["off"])
+
+
+def test_xxh3_raw_golden(golden):
+    v, arr, base, offs, lens = golden
+    out = host(engine.xxh3_64_batch(base, offs, lens)).view(np.uint64)
+    want = np.array([r["xxh3"] for r in v["vectors"]], dtype=np.uint64)
+    bad = np.nonzero(out != want)[0]
+    assert bad.size == 0, [v["vectors"][i]["n"] for i in bad[:10]]
+
+
+@pytest.mark.parametrize("ctype", [CT.kCRC32c, CT.kXXH3, CT.kNoChecksum])
+def test_block_checksum_with_last_byte_golden(golden, ctype):
+    v, arr, base, offs, lens = golden
+    # last byte read from memory (base[off+n]) and passed explicitly
+    out_mem = host(engine.block_checksum_batch(ctype, base, offs, lens)).astype(np.uint64)
+    lasts = np.array([arr[r["off"] + r["n"]] for r in v["vectors"]], dtype=np.uint8)
+    out_arr = host(engine.block_checksum_batch(ctype, base, offs, lens,
+                                               last_bytes=d(lasts))).astype(np.uint64)
+    want = np.array([r["with_last"][int(ctype)] for r in v["vectors"]], dtype=np.uint64)
+    assert (out_mem == want).all()
+    assert (out_arr == want).all()
+
+
+@pytest.mark.parametrize("ctype", [CT.kCRC32c, CT.kXXH3])
+def test_verify_computed_matches_builtin_golden(golden, ctype):
+    v, arr, base, offs, lens = golden
+    comp, stored, ok, bad = engine.block_verify_batch(ctype, base, offs, lens)
+    comp = host(comp).astype(np.uint64)
+    want = np.array([r["builtin_plus1"][int(ctype)] for r in v["vectors"]], dtype=np.uint64)
+    assert (comp == want).all()
+    # stored = LE32 at off+n+1 (random bytes here) -> ok iff equal
+    st = host(stored).astype(np.uint64)
+    exp_st = np.array([struct.unpack("<I", arr[r["off"] + r["n"] + 1:r["off"] + r["n"] + 5]
+                                     .tobytes())[0] for r in v["vectors"]], dtype=np.uint64)
+    assert (st == exp_st).all()
+    assert (host(ok).astype(bool) == (exp_st == want)).all()
+    assert int(host(bad)[0]) == int((exp_st != want).sum())
+
+
+def test_table_test_kats_on_gpu(kats):
+    k = kats["table_test"]
+    for t_str, expected in k["expected_hex"].items():
+        t = int(t_str)
+        if t not in (0, 1, 4):
+            continue
+        datas = []
+        for name, ct in k["cases"]:
+            b = k["inputs"][name].encode()
+            if ct is not None:
+                b = b[:-1] + bytes([ct])
+            datas.append(b)
+        # lay out as blocks: payload = data[:-1], type byte = data[-1]
+        buf = bytearray()
+        offs, sizes = [], []
+        for b in datas[1:]:
+            offs.append(len(buf))
+            sizes.append(len(b) - 1)
+            buf += b + b"\0\0\0\0"
+        arr = np.frombuffer(bytes(buf), dtype=np.uint8).copy()
+        comp, _, _, _ = engine.block_verify_batch(t, d(arr), d(np.array(offs, np.int64)),
+                                                  d(np.array(sizes, np.int32)))
+        got = [struct.pack("<I", int(x)).hex().upper() for x in host(comp)]
+        assert got == expected[1:], t
+
+
+def _host_layout(sizes, seed):
+    sizes = np.asarray(sizes, dtype=np.uint32)
+    offs = np.zeros(len(sizes), dtype=np.int64)
+    if len(sizes) > 1:
+        offs[1:] = np.cumsum(sizes[:-1].astype(np.int64) + 5)
+    total = int(offs[-1]) + int(sizes[-1]) + 5
+    rng = np.random.default_rng(seed)
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    return base, offs, sizes
+
+
+EDGE_SIZES = ([0, 1, 2, 3, 4, 5, 7, 8, 15, 16, 17, 30, 31, 32, 33, 63, 64, 65, 127, 128, 129,
+               239, 240, 241, 255, 256, 1023, 1024, 1025, 4090, 4091, 4092, 4093, 4094, 4095,
+               4096, 4097, 4098, 8191, 8192, 8193, 16383, 16384, 16385, 65535, 65536, 65537])
+
+
+@pytest.mark.parametrize("ctype", [CT.kCRC32c, CT.kXXH3, CT.kNoChecksum])
+def test_edge_sizes_every_alignment(ctype):
+    # every size at every start alignment mod 16
+    sizes = []
+    for s in EDGE_SIZES:
+        sizes += [s] * 16
+    # perturb offsets so that starts walk through all alignments
+    base, offs, sizes = _host_layout(sizes, 7)
+    for i in range(len(offs)):
+        offs[i] += 0  # packed layout already gives varied alignment
+    rng = np.random.default_rng(1)
+    lasts = rng.integers(0, 256, len(sizes), dtype=np.uint8)
+    mods = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    want = O.block_checksum_batch(int(ctype), base, offs, sizes, last_bytes=lasts,
+                                  modifiers=mods, nthreads=4)
+    got = host(engine.block_checksum_batch(ctype, d(base), d(offs), d(sizes.astype(np.int32)),
+                                           last_bytes=d(lasts), modifiers=d(mods.view(np.int32))))
+    bad = np.nonzero(got.astype(np.uint64) != want.astype(np.uint64))[0]
+    assert bad.size == 0, [(int(sizes[i]), int(offs[i]) & 15) for i in bad[:10]]
+    assert {int(o) & 15 for o in offs} == set(range(16)) or len(offs) < 64
+
+
+@pytest.mark.parametrize("ctype", [CT.kCRC32c, CT.kXXH3, CT.kNoChecksum])
+def test_trailer_then_verify_roundtrip_and_corruption(ctype):
+    rng = np.random.default_rng(2)
+    sizes = rng.integers(0, 20000, 3000).astype(np.uint32)
+    sizes[:len(EDGE_SIZES)] = EDGE_SIZES
+    base, offs, sizes = _host_layout(sizes, 3)
+    types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
+    base_ctx = 0x9E3779B1
+    mods = np.array([O.checksum_modifier_for_context(base_ctx, int(o)) for o in offs],
+                    dtype=np.uint32)
+    dbase, doffs, dsz = d(base), d(offs), d(sizes.astype(np.int32))
+    out = torch.empty(len(sizes), dtype=torch.uint32, device=DEV)
+    engine.block_trailer_batch(ctype, dbase, doffs, dsz, d(types), d(mods.view(np.int32)), out)
+    hb = host(dbase)
+    # trailers exactly as WriteMaybeCompressedBlock would write them
+    want = O.block_checksum_batch(int(ctype), base, offs, sizes, last_bytes=types,
+                                  modifiers=mods, nthreads=4)
+    assert (host(out).astype(np.uint64) == want.astype(np.uint64)).all()
+    for i in range(0, len(sizes), 37):
+        o, n = int(offs[i]), int(sizes[i])
+        assert hb[o + n] == types[i]
+        assert struct.unpack("<I", hb[o + n + 1:o + n + 5].tobytes())[0] == int(want[i])
+    # verify: all ok, oracle agrees
+    comp, st, ok, bad = engine.block_verify_batch(ctype, dbase, doffs, dsz,
+                                                  modifiers=d(mods.view(np.int32)))
+    assert int(host(bad)[0]) == 0 and host(ok).all()
+    _, ook, obad = O.block_verify_batch(int(ctype), hb, offs, sizes, modifiers=mods, nthreads=4)
+    assert obad == 0
+    # corrupt a set of blocks (payload, type byte, stored checksum) -> exactly those fail
+    victims = sorted(set(rng.integers(0, len(sizes), 40).tolist()))
+    hb2 = hb.copy()
+    for j, i in enumerate(victims):
+        o, n = int(offs[i]), int(sizes[i])
+        where = [o + n, o + n + 1 + (j % 4)]
+        if n:
+            where.append(o + (j * 7919) % n)
+        hb2[where[j % len(where)]] ^= 1 << (j % 8)
+    comp, st, ok, bad = engine.block_verify_batch(ctype, d(hb2), doffs, dsz,
+                                                  modifiers=d(mods.view(np.int32)))
+    okh = host(ok).astype(bool)
+    ocomp, ook, obad = O.block_verify_batch(int(ctype), hb2, offs, sizes, modifiers=mods,
+                                            nthreads=4)
+    assert (okh == ook.astype(bool)).all()
+    assert (host(comp).astype(np.uint64) == ocomp.astype(np.uint64)).all()
+    assert int(host(bad)[0]) == obad
+    if ctype != CT.kNoChecksum:
+        assert set(np.nonzero(~okh)[0].tolist()) == set(victims)
+
+
+def test_out_of_range_descriptors_are_reported_not_read():
+    base = d(np.zeros(1000, dtype=np.uint8))
+    offs = d(np.array([0, 990, 5000, 100], dtype=np.int64))
+    sizes = d(np.array([10, 10, 1, 0], dtype=np.int32))
+    for ct in (CT.kCRC32c, CT.kXXH3):
+        _, _, ok, bad = engine.block_verify_batch(ct, base, offs, sizes)
+        okh = host(ok)
+        assert okh[1] == 0 and okh[2] == 0
+        assert int(host(bad)[0]) >= 2
+
+
+def test_empty_batch_and_unsupported_type():
+    base = d(np.zeros(64, dtype=np.uint8))
+    e64 = torch.empty(0, dtype=torch.int64, device=DEV)
+    e32 = torch.empty(0, dtype=torch.int32, device=DEV)
+    engine.block_checksum_batch(CT.kCRC32c, base, e64, e32)
+    from forst_amd import ForstError
+    with pytest.raises(ForstError):
+        engine.block_checksum_batch(CT.kxxHash, base, d(np.array([0], np.int64)),
+                                    d(np.array([4], np.int32)))
+    with pytest.raises(ForstError):
+        engine.block_checksum_batch(9, base, d(np.array([0], np.int64)),
+                                    d(np.array([4], np.int32)))
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_verify_and_writer_crc(recyclable):
+    lens = workload.log_uniform_lengths(4000, 32, 32768, 0xF0E5700005)
+    lens[:6] = [0, 1, 7, 32761, 32762, 70000]
+    rng = np.random.default_rng(4)
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=recyclable, log_number=0xABC)
+    dlog = d(buf)
+    status, nrec, fail, bad = engine.wal_verify_batch(dlog, log_number=0xABC)
+    assert int(host(bad)[0]) == 0
+    assert (host(status) == 0).all()
+    assert int(host(nrec).astype(np.int64).sum()) == len(poffs)
+    # corrupt one record payload in block b -> that block BAD_CHECKSUM with nrec = records
+    # before it in the block
+    k = len(poffs) // 2
+    hs = 11 if recyclable else 7
+    buf2 = buf.copy()
+    buf2[int(poffs[k]) + hs + max(0, int(plens[k]) - 1)] ^= 0x80
+    if plens[k] == 0:
+        buf2[int(poffs[k]) + 6] ^= 0x01  # type byte is covered by the CRC
+    status, nrec, fail, bad = engine.wal_verify_batch(d(buf2), log_number=0xABC)
+    blk = int(poffs[k]) // 32768
+    st = host(status)
+    assert st[blk] == 1 and int(host(bad)[0]) == 1
+    before = int((((poffs // 32768) == blk) & (poffs < poffs[k])).sum())
+    assert int(host(nrec)[blk]) == before
+    assert int(host(fail)[blk]) == int(poffs[k]) - blk * 32768
+    # writer side: wipe all CRC fields, recompute in place -> identical image
+    buf3 = buf.copy()
+    for o in poffs:
+        buf3[int(o):int(o) + 4] = 0
+    d3 = d(buf3)
+    crcs = engine.wal_record_crc_batch(d3, d(poffs.astype(np.int64)))
+    assert (host(d3) == buf).all()
+    want = [struct.unpack("<I", buf[int(o):int(o) + 4].tobytes())[0] for o in poffs]
+    assert (host(crcs).astype(np.uint64) == np.array(want, dtype=np.uint64)).all()
+
+
+def test_wal_old_record_and_zero_type():
+    lens = np.array([100, 200, 300], dtype=np.uint32)
+    payload = np.arange(600, dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=True, log_number=5)
+    status, nrec, fail, bad = engine.wal_verify_batch(d(buf), log_number=6)
+    assert host(status)[0] == 4 and host(nrec)[0] == 0
+    z = np.zeros(32768, dtype=np.uint8)
+    status, nrec, fail, bad = engine.wal_verify_batch(d(z))
+    assert host(status)[0] == 3 and int(host(bad)[0]) == 0
+
+
+@pytest.mark.parametrize("spec,ctype", [(4096, CT.kCRC32c), ((4096, 16384, 65536), CT.kXXH3),
+                                        (("dev", 16384), CT.kCRC32c),
+                                        (("dev", 4096), CT.kXXH3)])
+def test_sst_batches_vs_oracle(spec, ctype):
+    n = 6000
+    b = workload.make_sst_batch(n, spec, 0xF0E5700003, ctype=ctype)
+    hb = host(b.base)
+    offs = host(b.offsets)
+    sizes = host(b.sizes).astype(np.uint32)
+    comp, st, ok, bad = engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes)
+    assert int(host(bad)[0]) == 0
+    ocomp, ook, obad = O.block_verify_batch(int(ctype), hb, offs, sizes, nthreads=8)
+    assert obad == 0
+    assert (host(comp).astype(np.uint64) == ocomp.astype(np.uint64)).all()
+    # payload is the splitmix stream of the seed
+    import stream as S
+    assert (hb[:4096] == S.stream(b.seed, 0, 4096)).all() or sizes[0] < 4096
+
+
+def test_full_size_c2_properties():
+    """C2: 1 M x 4 KiB kCRC32c, compute + verify at full size.  Checked by
+    (1) round trip: trailers written by the compute kernel verify clean,
+    (2) a 4096-block random sample against the oracle,
+    (3) exact detection of injected corruptions."""
+    n = 1 << 20
+    b = workload.make_sst_batch(n, 4096, workload.SEEDS["C2"], ctype=CT.kCRC32c)
+    comp, st, ok, bad = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
+    assert int(host(bad)[0]) == 0
+    rng = np.random.default_rng(5)
+    sample = np.unique(np.concatenate([[0, 1, n - 1], rng.integers(0, n, 4096)]))
+    offs = host(b.offsets)
+    compd = host(comp)
+    for i in sample:
+        o = int(offs[i])
+        blk = host(b.base[o:o + 4096 + 5])
+        assert int(compd[i]) == O.compute_builtin_checksum(1, blk[:4097])
+    victims = rng.choice(n, 64, replace=False)
+    flip = torch.from_numpy(offs[victims] + 17).to(DEV)
+    b.base[flip] ^= 0x10
+    _, _, ok, bad = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
+    okh = host(ok)
+    assert int(host(bad)[0]) == 64
+    assert set(np.nonzero(okh == 0)[0].tolist()) == set(victims.tolist())

@@ -21,6 +21,9 @@
 //    compression-type byte on the write side) are appended byte-wise.
 // The combine constants are block-size independent, so mixed 4/16/64 KiB
 // batches run in one launch.  See DESIGN.md for the roofline analysis.
+#include <cstdlib>
+#include <string>
+
 #include "crc32c_tables.h"
 #include "device_common.h"
 #include "engine.h"
@@ -203,9 +206,259 @@ __device__ __forceinline__ void fill_tables(uint32_t* L) {
   __syncthreads();
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined block kernel: a wave walks its blocks as a stream of (block,
+// round) items and issues the global loads of the NEXT item (next round of
+// the same block, or round 0 of its next block, plus that block's tail and
+// trailer words) before it runs the LDS-table CRC of the current item, so
+// every wave keeps ~4 KiB in flight while it computes.
+// ---------------------------------------------------------------------------
+struct CrcJob {
+  uint64_t i;         // descriptor index (>= n: no job)
+  const uint8_t* p;   // message start
+  const uint8_t* seg; // this lane's round-0 segment
+  uint32_t R;         // rounds; 0 => short message (byte-serial path)
+  uint32_t len;       // message length (short path)
+  uint32_t LA, jA, m; // head lane / head dword / head misalignment
+  uint32_t nt;        // tail bytes after the last round
+  uint32_t tail0, tail1;
+  uint32_t extra, nextra;
+  uint32_t init;
+  uint32_t stored;    // verify: trailer value (context not yet removed)
+  uint32_t mod;
+  uint32_t last;      // compute/trailer: compression type byte
+  bool valid;         // descriptor inside the buffer
+  bool safe;          // round-0 window inside the buffer
+};
+
+template <int MODE>
+__device__ __forceinline__ CrcJob crc_job_setup(const BlockArgs& a, uint64_t i,
+                                                uint32_t lane) {
+  CrcJob j;
+  j.i = i;
+  j.R = 0;
+  j.len = 0;
+  j.valid = false;
+  j.safe = true;
+  j.LA = j.jA = j.m = j.nt = 0;
+  j.tail0 = j.tail1 = 0;
+  j.extra = 0;
+  j.nextra = 0;
+  j.init = 0;
+  j.stored = 0;
+  j.mod = 0;
+  j.last = 0;
+  j.p = a.base;
+  j.seg = a.base;
+  if (i >= a.n) return j;
+  const uint64_t off = a.offsets[i];
+  const uint32_t size = a.sizes[i];
+  uint64_t need = size;
+  if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
+  if (MODE == kModeCompute && a.last_bytes == nullptr) need += 1;
+  j.valid = off <= a.base_len && need <= a.base_len - off;
+  if (!j.valid) return j;
+  const uint8_t* p = a.base + off;
+  j.p = p;
+  j.mod = a.modifiers ? a.modifiers[i] : 0u;
+  uint64_t len = size;
+  if (MODE == kModeVerify) {
+    len = uint64_t(size) + 1;  // reader_common.cc:36 (type byte is checksummed)
+    j.stored = ldu32(p + size + 1);
+  } else if (MODE == kModeRaw) {
+    j.init = a.init_crcs ? a.init_crcs[i] : 0u;
+  } else {
+    j.last = a.last_bytes ? a.last_bytes[i] : p[size];
+    j.extra = j.last;
+    j.nextra = 1;
+  }
+  j.len = static_cast<uint32_t>(len);
+  if (len < kSmall) return j;  // R = 0
+  const uint64_t A = reinterpret_cast<uint64_t>(p);
+  const uint64_t E = A + len;
+  const uint64_t Aal = A & ~3ull;
+  j.m = static_cast<uint32_t>(A & 3);
+  uint64_t Wend = E & ~3ull;
+  const uint64_t D = Wend - Aal;
+  uint32_t R = static_cast<uint32_t>((D + kRB - 1) / kRB);
+  if (R > 1 && (D % kRB) == 4) {
+    Wend -= 4;
+    --R;
+  }
+  const uint64_t Wstart = Wend - static_cast<uint64_t>(R) * kRB;
+  const uint32_t hA = static_cast<uint32_t>(Aal - Wstart);
+  j.R = R;
+  j.LA = hA >> 6;
+  j.jA = (hA >> 2) & 15u;
+  j.safe = Wstart >= reinterpret_cast<uint64_t>(a.base);
+  j.seg = p - static_cast<int64_t>(A - Wstart) + lane * 64;
+  j.nt = static_cast<uint32_t>(E - Wend);
+  const uint8_t* t = p + (Wend - A);
+  if (j.nt > 0) j.tail0 = ld4_a4(t);
+  if (j.nt > 4) j.tail1 = ld4_a4(t + 4);
+  return j;
+}
+
+template <int MODE>
+__device__ __forceinline__ void crc_job_finish(const BlockArgs& a, const CrcJob& j,
+                                               uint32_t lane, uint32_t crc) {
+  if (lane != 0) return;
+  if (!j.valid) {
+    if (a.out32) a.out32[j.i] = 0;
+    if (MODE == kModeVerify) {
+      if (a.ok_out) a.ok_out[j.i] = 0;
+      if (a.stored_out) a.stored_out[j.i] = 0;
+      if (a.mismatches) atomicAdd(a.mismatches, 1ull);
+    }
+    return;
+  }
+  if (MODE == kModeRaw) {
+    a.out32[j.i] = crc;
+  } else if (MODE == kModeVerify) {
+    const uint32_t computed = crc_mask(crc);
+    const uint32_t stored = j.stored - j.mod;
+    const bool ok = stored == computed;
+    if (a.out32) a.out32[j.i] = computed;
+    if (a.stored_out) a.stored_out[j.i] = stored;
+    if (a.ok_out) a.ok_out[j.i] = ok ? 1 : 0;
+    if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
+  } else {
+    const uint32_t c = crc_mask(crc) + j.mod;
+    if (a.out32) a.out32[j.i] = c;
+    if (MODE == kModeTrailer) {
+      uint8_t* q = a.base_w + (j.p - a.base) + (j.len);
+      q[0] = static_cast<uint8_t>(j.last);
+      stu32_bytes(q + 1, c);
+    }
+  }
+}
+
+// byte-serial CRC of a short message (len < kSmall)
+__device__ __forceinline__ uint32_t crc_short(const uint32_t* __restrict__ L, uint32_t lb,
+                                              const CrcJob& j) {
+  uint32_t s = ~j.init;
+  for (uint32_t k = 0; k < j.len; ++k) s = crc_byte(L, lb, s, j.p[k]);
+  if (j.nextra) s = crc_byte(L, lb, s, j.extra);
+  return ~s;
+}
+
+// load the segment of item (job, round r) into w
+__device__ __forceinline__ void crc_job_load(uint32_t (&w)[16], const CrcJob& j, uint32_t r,
+                                             uint64_t lo) {
+  if (j.R == 0) return;
+  const uint8_t* seg = j.seg + static_cast<uint64_t>(r) * kRB;
+  if (r == 0 && !j.safe)
+    load_seg_checked(w, seg, lo);
+  else
+    load_seg(w, seg);
+}
+
+// round r of job j on data w; returns the lane state
+__device__ __forceinline__ uint32_t crc_job_round(const uint32_t* __restrict__ L, uint32_t lb,
+                                                  uint32_t lane, const CrcJob& j, uint32_t r,
+                                                  uint32_t s, const uint32_t (&w)[16]) {
+  if (r == 0) {
+    s = 0;
+#pragma unroll
+    for (int k = 0; k < 16; ++k) {
+      if (static_cast<uint32_t>(k) == j.jA) {
+        if (j.m == 0) {
+          const uint32_t s0 = (lane == j.LA) ? ~j.init : s;
+          s = crc_g(L, lb, s0 ^ w[k]);
+        } else {
+          const uint32_t sn = crc_g(L, lb, s ^ w[k]);
+          uint32_t sb = ~j.init;
+          uint32_t wb = w[k] >> (8 * j.m);
+          for (uint32_t b = j.m; b < 4; ++b) {
+            sb = crc_byte(L, lb, sb, wb & 0xffu);
+            wb >>= 8;
+          }
+          s = (lane == j.LA) ? sb : sn;
+        }
+      } else {
+        s = crc_g(L, lb, s ^ w[k]);
+      }
+    }
+    s = (lane < j.LA) ? 0u : s;
+  } else {
+    s = crc_shift(L, kOffJump, s);
+#pragma unroll
+    for (int k = 0; k < 16; ++k) s = crc_g(L, lb, s ^ w[k]);
+  }
+  return s;
+}
+
+// 64-lane combine + tail + extra byte; every lane returns the finalized CRC
+__device__ __forceinline__ uint32_t crc_job_combine(const uint32_t* __restrict__ L, uint32_t lb,
+                                                    uint32_t lane, const CrcJob& j, uint32_t s) {
+#pragma unroll
+  for (int k = 0; k < FORST_CRC_TREE_LEVELS; ++k) {
+    const uint32_t other = __shfl_xor(s, 1 << k);
+    const bool right = (lane >> k) & 1;
+    const uint32_t left_v = right ? other : s;
+    const uint32_t right_v = right ? s : other;
+    s = crc_shift(L, kOffTree + 1024u * k, left_v) ^ right_v;
+  }
+  uint32_t t = j.tail0;
+  for (uint32_t k = 0; k < j.nt; ++k) {
+    if (k == 4) t = j.tail1;
+    s = crc_byte(L, lb, s, t & 0xffu);
+    t >>= 8;
+  }
+  if (j.nextra) s = crc_byte(L, lb, s, j.extra);
+  return ~s;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) crc32c_block_kernel(BlockArgs a) {
+  __shared__ uint32_t L[kLdsDwords];
+  fill_tables(L);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t lb = (lane & 31) << 2;
+  const uint64_t lo = reinterpret_cast<uint64_t>(a.base);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+
+  CrcJob cur = crc_job_setup<MODE>(a, static_cast<uint64_t>(blockIdx.x) * kWaves + wave, lane);
+  uint32_t wA[16], wB[16];
+  crc_job_load(wA, cur, 0, lo);
+  uint32_t r = 0, s = 0;
+
+  // one pipeline step: compute (cur, r) on `wc` while item after it is loaded into `wn`
+  auto step = [&](uint32_t (&wc)[16], uint32_t (&wn)[16]) {
+    const bool same = cur.valid && cur.R > 0 && r + 1 < cur.R;
+    CrcJob nxt = cur;
+    if (same) {
+      crc_job_load(wn, cur, r + 1, lo);
+    } else {
+      nxt = crc_job_setup<MODE>(a, cur.i + nw, lane);
+      crc_job_load(wn, nxt, 0, lo);
+    }
+    if (!cur.valid) {
+      crc_job_finish<MODE>(a, cur, lane, 0);
+    } else if (cur.R == 0) {
+      crc_job_finish<MODE>(a, cur, lane, crc_short(L, lb, cur));
+    } else {
+      s = crc_job_round(L, lb, lane, cur, r, s, wc);
+      if (!same) crc_job_finish<MODE>(a, cur, lane, crc_job_combine(L, lb, lane, cur, s));
+    }
+    if (same) {
+      ++r;
+    } else {
+      cur = nxt;
+      r = 0;
+    }
+  };
+  while (cur.i < a.n) {
+    step(wA, wB);
+    if (cur.i >= a.n) break;
+    step(wB, wA);
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kThreads)
-    crc32c_block_kernel(BlockArgs a) {
+    crc32c_block_kernel_simple(BlockArgs a) {
   __shared__ uint32_t L[kLdsDwords];
   fill_tables(L);
   const uint32_t lane = threadIdx.x & 63;
@@ -274,32 +527,39 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
                                 hipStream_t stream, const char** name) {
   const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
-  uint64_t waves = (a.n + 0);
   uint32_t grid = static_cast<uint32_t>(
-      std::min<uint64_t>((waves + kWaves - 1) / kWaves, di.num_cus));
+      std::min<uint64_t>((a.n + kWaves - 1) / kWaves, di.num_cus));
   if (grid == 0) grid = 1;
+  // FORST_CRC_VARIANT=simple selects the unpipelined kernel (A/B reference)
+  const char* variant = std::getenv("FORST_CRC_VARIANT");
+  const bool simple = variant && std::string(variant) == "simple";
+#define FORST_LAUNCH_CRC(M, TAG)                                                         \
+  do {                                                                                   \
+    if (simple) {                                                                        \
+      *name = "crc32c_block_kernel_simple<" TAG ">";                                     \
+      hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,   \
+                         stream, a);                                                     \
+    } else {                                                                             \
+      *name = "crc32c_block_kernel<" TAG ">";                                            \
+      hipLaunchKernelGGL(crc32c_block_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \
+                         a);                                                             \
+    }                                                                                    \
+  } while (0)
   switch (mode) {
     case kModeCompute:
-      *name = "crc32c_block_kernel<compute>";
-      hipLaunchKernelGGL(crc32c_block_kernel<kModeCompute>, dim3(grid),
-                         dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_CRC(kModeCompute, "compute");
       break;
     case kModeTrailer:
-      *name = "crc32c_block_kernel<trailer>";
-      hipLaunchKernelGGL(crc32c_block_kernel<kModeTrailer>, dim3(grid),
-                         dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_CRC(kModeTrailer, "trailer");
       break;
     case kModeVerify:
-      *name = "crc32c_block_kernel<verify>";
-      hipLaunchKernelGGL(crc32c_block_kernel<kModeVerify>, dim3(grid),
-                         dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_CRC(kModeVerify, "verify");
       break;
     default:
-      *name = "crc32c_block_kernel<raw>";
-      hipLaunchKernelGGL(crc32c_block_kernel<kModeRaw>, dim3(grid),
-                         dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_CRC(kModeRaw, "raw");
       break;
   }
+#undef FORST_LAUNCH_CRC
   return hipGetLastError();
 }
 

@@ -120,7 +120,7 @@ __device__ __forceinline__ uint32_t wave_crc32c(const uint32_t* __restrict__ L,
   if (len < kSmall) {
     s = ~init;
     for (uint32_t i = 0; i < static_cast<uint32_t>(len); ++i)
-      s = crc_byte(L, lb, s, p[i]);
+      s = crc_byte(L, lb, s, ldu8(p + i));
   } else {
     const uint64_t A = reinterpret_cast<uint64_t>(p);
     const uint64_t E = A + len;
@@ -191,7 +191,7 @@ __device__ __forceinline__ uint32_t wave_crc32c(const uint32_t* __restrict__ L,
     // ---- tail bytes [Wend, E) ----
     const uint8_t* t = p + (Wend - A);
     const uint32_t nt = static_cast<uint32_t>(E - Wend);
-    for (uint32_t i = 0; i < nt; ++i) s = crc_byte(L, lb, s, t[i]);
+    for (uint32_t i = 0; i < nt; ++i) s = crc_byte(L, lb, s, ldu8(t + i));
   }
   if (nextra) s = crc_byte(L, lb, s, extra);
   return ~s;
@@ -268,7 +268,7 @@ __device__ __forceinline__ CrcJob crc_job_setup(const BlockArgs& a, uint64_t i,
   } else if (MODE == kModeRaw) {
     j.init = a.init_crcs ? a.init_crcs[i] : 0u;
   } else {
-    j.last = a.last_bytes ? a.last_bytes[i] : p[size];
+    j.last = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
     j.extra = j.last;
     j.nextra = 1;
   }
@@ -294,8 +294,8 @@ __device__ __forceinline__ CrcJob crc_job_setup(const BlockArgs& a, uint64_t i,
   j.seg = p - static_cast<int64_t>(A - Wstart) + lane * 64;
   j.nt = static_cast<uint32_t>(E - Wend);
   const uint8_t* t = p + (Wend - A);
-  if (j.nt > 0) j.tail0 = ld4_a4(t);
-  if (j.nt > 4) j.tail1 = ld4_a4(t + 4);
+  if (j.nt > 0) j.tail0 = ld4v(t);
+  if (j.nt > 4) j.tail1 = ld4v(t + 4);
   return j;
 }
 
@@ -337,7 +337,7 @@ __device__ __forceinline__ void crc_job_finish(const BlockArgs& a, const CrcJob&
 __device__ __forceinline__ uint32_t crc_short(const uint32_t* __restrict__ L, uint32_t lb,
                                               const CrcJob& j) {
   uint32_t s = ~j.init;
-  for (uint32_t k = 0; k < j.len; ++k) s = crc_byte(L, lb, s, j.p[k]);
+  for (uint32_t k = 0; k < j.len; ++k) s = crc_byte(L, lb, s, ldu8(j.p + k));
   if (j.nextra) s = crc_byte(L, lb, s, j.extra);
   return ~s;
 }
@@ -505,7 +505,7 @@ __global__ void __launch_bounds__(kThreads)
       }
     } else {
       // format.cc:594-600 + builder.cc:1340-1345
-      const uint32_t last = a.last_bytes ? a.last_bytes[i] : p[size];
+      const uint32_t last = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
       const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
       const uint32_t c =
           crc_mask(wave_crc32c(L, lane, lb, p, size, 0, 1, last, lo)) + mod;
@@ -530,6 +530,16 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   uint32_t grid = static_cast<uint32_t>(
       std::min<uint64_t>((a.n + kWaves - 1) / kWaves, di.num_cus));
   if (grid == 0) grid = 1;
+#ifdef FORST_DEBUG_BOUNDS
+  {
+    DbgState st{};
+    st.lo = reinterpret_cast<uint64_t>(a.base);
+    st.hi = st.lo + a.base_len;
+    hipError_t e = hipMemcpyToSymbolAsync(HIP_SYMBOL(g_forst_dbg), &st, sizeof(st), 0,
+                                          hipMemcpyHostToDevice, stream);
+    if (e != hipSuccess) return e;
+  }
+#endif
   // FORST_CRC_VARIANT=simple selects the unpipelined kernel (A/B reference)
   const char* variant = std::getenv("FORST_CRC_VARIANT");
   const bool simple = variant && std::string(variant) == "simple";
@@ -691,3 +701,15 @@ hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,
 }
 
 }  // namespace forst
+
+#ifdef FORST_DEBUG_BOUNDS
+// diagnostics build only: first out-of-bounds access recorded by the CRC
+// kernels since the last launch (line, offset from base, width, count)
+extern "C" __attribute__((visibility("default"))) int forst_debug_fetch(unsigned long long* out) {
+  forst::DbgState st{};
+  if (hipMemcpyFromSymbol(&st, HIP_SYMBOL(forst::g_forst_dbg), sizeof(st)) != hipSuccess)
+    return -3;
+  for (int k = 0; k < 4; ++k) out[k] = st.rec[k];
+  return 0;
+}
+#endif

@@ -22,10 +22,53 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // start at any dword boundary are read with one instruction.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
 
+// Opaque per-lane zero.  Adding it to a wave-uniform data address forces a
+// VECTOR (global_load) access: hipcc otherwise turns uniform loads it proves
+// unclobbered into scalar s_load_dword, whose SBASE low bits are ignored --
+// wrong for the byte-granular, unaligned-start addresses of SST blocks --
+// and which read through the scalar cache.  Descriptor arrays may still use
+// SMEM; block bytes never do.
+__device__ __forceinline__ uint32_t vzero() {
+  uint32_t z;
+#ifndef FORST_HOST_EMULATION  // tests/emu compiles these sources as host C++
+  asm volatile("v_mov_b32 %0, 0" : "=v"(z));
+#else
+  z = 0;
+#endif
+  return z;
+}
+
+#ifdef FORST_DEBUG_BOUNDS
+// Diagnostics build only (make DEBUG_BOUNDS=1 -> lib/libforst_checksum_dbg.so):
+// every block-data load is checked against the launch's buffer bounds; the
+// first violation (source line, offset, width) is recorded and the access is
+// skipped instead of faulting the GPU.
+struct DbgState {
+  uint64_t lo, hi;
+  unsigned long long rec[4];  // line, offset from lo, width, count
+};
+static __device__ DbgState g_forst_dbg;
+__device__ __forceinline__ bool dbg_ok(const void* p, uint32_t n, uint32_t line) {
+  const uint64_t a = reinterpret_cast<uint64_t>(p);
+  if (a >= g_forst_dbg.lo && a + n <= g_forst_dbg.hi) return true;
+  if (atomicCAS(&g_forst_dbg.rec[0], 0ull, static_cast<unsigned long long>(line)) == 0ull) {
+    g_forst_dbg.rec[1] = a - g_forst_dbg.lo;
+    g_forst_dbg.rec[2] = n;
+  }
+  atomicAdd(&g_forst_dbg.rec[3], 1ull);
+  return false;
+}
+#define FORST_DBG_OK(p, n) ::forst::dbg_ok((p), (n), __LINE__)
+#else
+#define FORST_DBG_OK(p, n) true
+#endif
+
 __device__ __forceinline__ u32x4a4 ld16_a4(const uint8_t* p) {
+  if (!FORST_DBG_OK(p, 16)) return u32x4a4{0u, 0u, 0u, 0u};
   return *reinterpret_cast<const u32x4a4*>(p);
 }
 __device__ __forceinline__ uint32_t ld4_a4(const uint8_t* p) {
+  if (!FORST_DBG_OK(p, 4)) return 0u;
   return *reinterpret_cast<const uint32_t*>(p);
 }
 
@@ -37,7 +80,7 @@ __device__ __forceinline__ uint32_t ld4_a4(const uint8_t* p) {
 // the global address space and emits global_load, not flat_load.)
 __device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
   const uint32_t m = reinterpret_cast<uint64_t>(p) & 3;
-  const uint8_t* q = p - m;
+  const uint8_t* q = p - m + vzero();
   const uint32_t lo = ld4_a4(q);
   if (m == 0) return lo;
   const uint32_t hi = ld4_a4(q + 4);
@@ -45,7 +88,7 @@ __device__ __forceinline__ uint32_t ldu32(const uint8_t* p) {
 }
 __device__ __forceinline__ uint64_t ldu64(const uint8_t* p) {
   const uint32_t m = reinterpret_cast<uint64_t>(p) & 3;
-  const uint8_t* q = p - m;
+  const uint8_t* q = p - m + vzero();
   const uint32_t w0 = ld4_a4(q), w1 = ld4_a4(q + 4);
   if (m == 0) return (static_cast<uint64_t>(w1) << 32) | w0;
   const uint32_t w2 = ld4_a4(q + 8);
@@ -53,7 +96,12 @@ __device__ __forceinline__ uint64_t ldu64(const uint8_t* p) {
   const uint32_t hi = __builtin_amdgcn_alignbyte(w2, w1, m);
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
-__device__ __forceinline__ uint32_t ldu8(const uint8_t* p) { return *p; }
+__device__ __forceinline__ uint32_t ldu8(const uint8_t* p) {
+  if (!FORST_DBG_OK(p, 1)) return 0u;
+  return *(p + vzero());
+}
+// dword-aligned single dword, vector path
+__device__ __forceinline__ uint32_t ld4v(const uint8_t* p) { return ld4_a4(p + vzero()); }
 
 // util/crc32c.h:44-53
 __device__ __forceinline__ uint32_t crc_mask(uint32_t crc) {

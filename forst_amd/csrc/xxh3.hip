@@ -106,7 +106,7 @@ __device__ uint64_t xxh3_short(const uint8_t* in, uint32_t len) {
       return rrmxmx(in64 ^ (sec64(8) ^ sec64(16)), len);
     }
     if (len) {
-      const uint32_t c1 = in[0], c2 = in[len >> 1], c3 = in[len - 1];
+      const uint32_t c1 = ldu8(in), c2 = ldu8(in + (len >> 1)), c3 = ldu8(in + len - 1);
       const uint32_t combined = (c1 << 16) | (c2 << 24) | c3 | (len << 8);
       const uint32_t bf = static_cast<uint32_t>(sec64(0)) ^
                           static_cast<uint32_t>(sec64(4));
@@ -305,7 +305,7 @@ __global__ void __launch_bounds__(kThreads) xxh3_block_kernel(BlockArgs a) {
       if (lane == 0) a.out64[i] = h;
     } else if (MODE == kModeVerify) {
       // ComputeBuiltinChecksum(kXXH3, data, size+1), format.cc:577-586
-      const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), p[size]);
+      const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), ldu8(p + size));
       const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
       const uint32_t stored = ldu32(p + size + 1) - mod;
       const bool ok = stored == computed;
@@ -316,7 +316,7 @@ __global__ void __launch_bounds__(kThreads) xxh3_block_kernel(BlockArgs a) {
         if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
       }
     } else {
-      const uint32_t last = a.last_bytes ? a.last_bytes[i] : p[size];
+      const uint32_t last = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
       const uint32_t mod = a.modifiers ? a.modifiers[i] : 0u;
       const uint32_t c = modify_for_last_byte(static_cast<uint32_t>(h), last) + mod;
       if (lane == 0) {

@@ -1,0 +1,14 @@
+#!/bin/bash
+# tests/emu/build_emu.sh <out.so> -- TEST INFRASTRUCTURE ONLY.
+# Compiles the unmodified kernel sources as host C++ against the SIMT emulator
+# header (tests/emu/hip/hip_runtime.h) into a CPU-only library exposing the
+# same C ABI as forst_amd/lib/libforst_checksum.so.
+set -euo pipefail
+HERE=$(cd "$(dirname "$0")" && pwd)
+ROOT=$(cd "$HERE/../.." && pwd)
+OUT=${1:-/tmp/libforst_emu.so}
+CXX=${CXX_EMU:-/opt/rocm/llvm/bin/clang++}
+"$CXX" -std=c++20 -O1 -g -fPIC -shared -w -I"$HERE" -I"$ROOT/include" -include hip/hip_runtime.h -DFORST_HOST_EMULATION \
+  -x c++ "$ROOT/forst_amd/csrc/crc32c.hip" "$ROOT/forst_amd/csrc/xxh3.hip" \
+  "$ROOT/forst_amd/csrc/capi.hip" "$HERE/emu_globals.cc" -o "$OUT" -lpthread
+echo "$OUT"

@@ -1,0 +1,124 @@
+"""tests/emu/emu.py -- TEST INFRASTRUCTURE ONLY.
+
+Builds the kernel sources against the SIMT emulator (build_emu.sh) and calls
+the same C ABI on host (numpy) buffers, so kernel logic can be checked against
+the oracle on a CPU.  Never used by the product.
+"""
+import ctypes
+import os
+import subprocess
+import tempfile
+
+import numpy as np
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+_lib = None
+
+
+def lib():
+    global _lib
+    if _lib is None:
+        out = os.path.join(tempfile.gettempdir(), f"libforst_emu_{os.getpid()}.so")
+        subprocess.check_call([os.path.join(HERE, "build_emu.sh"), out],
+                              stdout=subprocess.DEVNULL)
+        L = ctypes.CDLL(out)
+        vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
+        sigs = {
+            "forst_last_error": (ctypes.c_char_p, []),
+            "forst_block_checksum_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
+            "forst_block_trailer_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
+            "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
+            "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
+            "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
+            "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
+            "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
+        }
+        for name, (res, args) in sigs.items():
+            f = getattr(L, name)
+            f.restype, f.argtypes = res, args
+        _lib = L
+    return _lib
+
+
+def _p(a):
+    return None if a is None else a.ctypes.data
+
+
+def _chk(rc):
+    if rc != 0:
+        raise RuntimeError(lib().forst_last_error().decode())
+
+
+def _aligned(base):
+    """copy into a 16-byte aligned buffer (the C ABI wants 4-byte alignment)"""
+    raw = np.zeros(base.nbytes + 64, dtype=np.uint8)
+    off = (-raw.ctypes.data) % 16
+    a = raw[off:off + base.nbytes]
+    a[:] = base
+    return a
+
+
+def block_checksum(ctype, base, offs, sizes, last=None, mods=None):
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    sizes = np.ascontiguousarray(sizes, np.uint32)
+    out = np.zeros(len(offs), np.uint32)
+    _chk(lib().forst_block_checksum_batch(int(ctype), _p(base), base.nbytes, _p(offs), _p(sizes),
+                                          _p(last), _p(mods), _p(out), len(offs), None))
+    return out
+
+
+def block_trailer(ctype, base, offs, sizes, last, mods=None):
+    b = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    sizes = np.ascontiguousarray(sizes, np.uint32)
+    out = np.zeros(len(offs), np.uint32)
+    _chk(lib().forst_block_trailer_batch(int(ctype), _p(b), b.nbytes, _p(offs), _p(sizes),
+                                         _p(last), _p(mods), _p(out), len(offs), None))
+    return b.copy(), out
+
+
+def block_verify(ctype, base, offs, sizes, mods=None):
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    sizes = np.ascontiguousarray(sizes, np.uint32)
+    n = len(offs)
+    comp = np.zeros(n, np.uint32)
+    st = np.zeros(n, np.uint32)
+    ok = np.zeros(n, np.uint8)
+    bad = np.zeros(1, np.uint64)
+    _chk(lib().forst_block_verify_batch(int(ctype), _p(base), base.nbytes, _p(offs), _p(sizes),
+                                        _p(mods), _p(comp), _p(st), _p(ok), _p(bad), n, None))
+    return comp, st, ok, int(bad[0])
+
+
+def crc32c(base, offs, lens, init=None):
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    out = np.zeros(len(offs), np.uint32)
+    _chk(lib().forst_crc32c_batch(_p(base), base.nbytes, _p(offs), _p(lens), _p(init), _p(out),
+                                  len(offs), None))
+    return out
+
+
+def xxh3(base, offs, lens):
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    out = np.zeros(len(offs), np.uint64)
+    _chk(lib().forst_xxh3_64_batch(_p(base), base.nbytes, _p(offs), _p(lens), _p(out),
+                                   len(offs), None))
+    return out
+
+
+def wal_verify(log, log_number=0):
+    log = _aligned(log)
+    nb = (log.nbytes + 32767) // 32768
+    st = np.zeros(nb, np.uint8)
+    nrec = np.zeros(nb, np.uint32)
+    fail = np.zeros(nb, np.uint32)
+    bad = np.zeros(1, np.uint64)
+    _chk(lib().forst_wal_verify_batch(_p(log), log.nbytes, 0, nb, log_number, _p(st), _p(nrec),
+                                      _p(fail), _p(bad), None))
+    return st, nrec, fail, int(bad[0])

@@ -1,0 +1,124 @@
+// tests/emu/hip/hip_runtime.h -- TEST INFRASTRUCTURE ONLY.
+//
+// A tiny SIMT emulator that lets the UNMODIFIED kernel sources in
+// forst_amd/csrc/*.hip compile as host C++ (clang) and run on the CPU: every
+// workgroup is run with one std::thread per work-item, waves of 64 threads
+// exchange values through a per-wave barrier (__shfl_xor, readfirstlane) and
+// __syncthreads is a workgroup barrier.  It shadows <hip/hip_runtime.h> only
+// when tests/emu is first on the include path (tests/emu/build_emu.sh); the
+// product build never sees it.  Used to debug kernel index math / lane logic
+// without a GPU and to run the oracle parity tests on the CPU.
+#pragma once
+
+#include <atomic>
+#include <barrier>
+#include <cstdint>
+#include <cstdio>
+#include <cstring>
+#include <functional>
+#include <memory>
+#include <thread>
+#include <vector>
+
+#define __global__
+#define __device__
+#define __host__
+#define __constant__
+#define __forceinline__ inline
+#define __launch_bounds__(...)
+#define __shared__ static
+
+struct dim3 {
+  uint32_t x, y, z;
+  constexpr dim3(uint32_t a = 1, uint32_t b = 1, uint32_t c = 1) : x(a), y(b), z(c) {}
+};
+
+typedef int hipError_t;
+typedef void* hipStream_t;
+constexpr hipError_t hipSuccess = 0;
+struct hipDeviceProp_t {
+  char gcnArchName[256];
+  int multiProcessorCount;
+};
+inline const char* hipGetErrorString(hipError_t) { return "emu"; }
+inline hipError_t hipGetLastError() { return hipSuccess; }
+inline hipError_t hipGetDevice(int* d) {
+  *d = 0;
+  return hipSuccess;
+}
+inline hipError_t hipGetDeviceProperties(hipDeviceProp_t* p, int) {
+  std::memset(p, 0, sizeof(*p));
+  std::strcpy(p->gcnArchName, "gfx950:sramecc+:xnack-");
+  const char* cus = std::getenv("FORST_EMU_CUS");
+  p->multiProcessorCount = cus ? std::atoi(cus) : 2;
+  return hipSuccess;
+}
+
+namespace emu {
+struct Wave {
+  uint32_t slot[64];
+  std::unique_ptr<std::barrier<>> bar;
+};
+struct Group {
+  std::unique_ptr<std::barrier<>> bar;
+  std::vector<Wave> waves;
+};
+extern thread_local dim3 tl_tid;
+extern thread_local dim3 tl_bid;
+extern thread_local Group* tl_group;
+extern dim3 g_grid, g_block;
+
+inline uint32_t exchange(uint32_t v, uint32_t src_lane) {
+  Wave& w = tl_group->waves[tl_tid.x >> 6];
+  const uint32_t lane = tl_tid.x & 63;
+  w.slot[lane] = v;
+  w.bar->arrive_and_wait();
+  const uint32_t r = w.slot[src_lane & 63];
+  w.bar->arrive_and_wait();
+  return r;
+}
+
+template <typename K, typename... Args>
+void launch(K kernel, dim3 grid, dim3 block, Args... args) {
+  g_grid = grid;
+  g_block = block;
+  const uint32_t nthreads = block.x;
+  for (uint32_t b = 0; b < grid.x; ++b) {
+    Group g;
+    g.bar = std::make_unique<std::barrier<>>(nthreads);
+    g.waves.resize((nthreads + 63) / 64);
+    for (uint32_t w = 0; w < g.waves.size(); ++w)
+      g.waves[w].bar = std::make_unique<std::barrier<>>(std::min<uint32_t>(64, nthreads - 64 * w));
+    std::vector<std::thread> th;
+    th.reserve(nthreads);
+    for (uint32_t t = 0; t < nthreads; ++t) {
+      th.emplace_back([&, t, b] {
+        tl_tid = dim3(t);
+        tl_bid = dim3(b);
+        tl_group = &g;
+        kernel(args...);
+      });
+    }
+    for (auto& x : th) x.join();
+  }
+}
+}  // namespace emu
+
+#define threadIdx (::emu::tl_tid)
+#define blockIdx (::emu::tl_bid)
+#define gridDim (::emu::g_grid)
+#define blockDim (::emu::g_block)
+
+inline void __syncthreads() { emu::tl_group->bar->arrive_and_wait(); }
+inline uint32_t __shfl_xor(uint32_t v, int mask) {
+  return emu::exchange(v, (emu::tl_tid.x & 63) ^ static_cast<uint32_t>(mask));
+}
+inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return emu::exchange(v, 0); }
+inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
+  return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8 * (s & 3)));
+}
+inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
+  return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
+
+#define hipLaunchKernelGGL(K, G, B, SH, ST, ...) ::emu::launch(K, G, B, __VA_ARGS__)

@@ -1,0 +1,76 @@
+"""The HIP kernel sources, compiled unmodified against the CPU SIMT emulator
+(tests/emu), vs the oracle on the golden vectors and edge layouts.  This checks
+kernel lane/index logic on the CPU; the real parity gate is
+tests/test_gpu_parity.py on the MI355X."""
+import os
+import shutil
+import struct
+import sys
+
+import numpy as np
+import pytest
+
+HERE = os.path.dirname(os.path.abspath(__file__))
+sys.path.insert(0, os.path.join(HERE, "emu"))
+
+if shutil.which("/opt/rocm/llvm/bin/clang++") is None:
+    pytest.skip("needs ROCm clang++ to build the emulator", allow_module_level=True)
+
+import emu  # noqa: E402
+
+from oracle import oracle as O  # noqa: E402
+
+
+@pytest.fixture(scope="module")
+def golden_arrays(ref_vectors):
+    v, blob = ref_vectors
+    arr = np.frombuffer(blob, dtype=np.uint8)
+    offs = np.array([r["off"] for r in v["vectors"]], dtype=np.uint64)
+    lens = np.array([r["n"] for r in v["vectors"]], dtype=np.uint32)
+    return v, arr, offs, lens
+
+
+def test_emu_crc32c_raw_and_verify(golden_arrays):
+    v, arr, offs, lens = golden_arrays
+    out = emu.crc32c(arr, offs, lens)
+    assert (out == np.array([r["crc32c"] for r in v["vectors"]], np.uint32)).all()
+    comp, st, ok, bad = emu.block_verify(1, arr, offs, lens)
+    assert (comp == np.array([r["builtin_plus1"][1] for r in v["vectors"]], np.uint32)).all()
+
+
+def test_emu_xxh3_and_blocks(golden_arrays):
+    v, arr, offs, lens = golden_arrays
+    out = emu.xxh3(arr, offs, lens)
+    assert (out == np.array([r["xxh3"] for r in v["vectors"]], np.uint64)).all()
+    for t in (1, 4):
+        got = emu.block_checksum(t, arr, offs, lens)
+        assert (got == np.array([r["with_last"][t] for r in v["vectors"]], np.uint32)).all()
+
+
+def test_emu_trailer_roundtrip_mixed():
+    rng = np.random.default_rng(8)
+    sizes = rng.integers(0, 9000, 400).astype(np.uint32)
+    offs = np.zeros(len(sizes), np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 5)
+    total = int(offs[-1]) + int(sizes[-1]) + 5
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
+    mods = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    for t in (1, 4):
+        b2, out = emu.block_trailer(t, base, offs, sizes, types, mods)
+        want = O.block_checksum_batch(t, base, offs, sizes, last_bytes=types, modifiers=mods)
+        assert (out == want).all()
+        o, n = int(offs[5]), int(sizes[5])
+        assert b2[o + n] == types[5]
+        assert struct.unpack("<I", b2[o + n + 1:o + n + 5].tobytes())[0] == int(want[5])
+        comp, st, ok, bad = emu.block_verify(t, b2, offs, sizes, mods)
+        assert bad == 0 and ok.all()
+
+
+def test_emu_wal():
+    rng = np.random.default_rng(1)
+    lens = rng.integers(0, 40000, 60).astype(np.uint32)
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens)
+    st, nrec, fail, bad = emu.wal_verify(buf)
+    assert bad == 0 and (st == 0).all() and int(nrec.sum()) == len(poffs)

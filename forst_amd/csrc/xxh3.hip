@@ -10,6 +10,9 @@
 // non-linear scramble (xxhash.h:4962-4977) is applied in order, per
 // accumulator, by the lanes that own it.  Short inputs (<= 240 B) run the
 // reference's length-class formulas redundantly on all lanes.
+#include <cstdlib>
+#include <string>
+
 #include "device_common.h"
 #include "engine.h"
 
@@ -165,12 +168,39 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-// sum over the 16 lanes that share L%4 (lane bits 2..5)
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
+  return (static_cast<uint64_t>(hi) << 32) | lo;
+}
+// DPP row rotate (within 16-lane rows), one VALU op, no LDS traffic
+template <int N>
+__device__ __forceinline__ uint64_t row_ror64(uint64_t v) {
+  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(v), 0x120 + N,
+                                                  0xf, 0xf, false);
+  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(v >> 32),
+                                                  0x120 + N, 0xf, 0xf, false);
+  return mk64(lo, hi);
+}
+
+// sum over the 16 lanes that share L%4 (lane bits 2..5): two DPP row
+// rotations, then the gfx950 cross-row swaps v_permlane16_swap /
+// v_permlane32_swap (own + partner) -- all VALU, every lane gets the sum.
 __device__ __forceinline__ uint64_t stripe_sum(uint64_t v) {
-  v += shfl_xor64(v, 4);
-  v += shfl_xor64(v, 8);
-  v += shfl_xor64(v, 16);
-  v += shfl_xor64(v, 32);
+  v += row_ror64<4>(v);
+  v += row_ror64<8>(v);
+  {
+    const auto lo = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(v),
+                                                     static_cast<uint32_t>(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane16_swap(static_cast<uint32_t>(v >> 32),
+                                                     static_cast<uint32_t>(v >> 32), false, false);
+    v = mk64(lo[0], hi[0]) + mk64(lo[1], hi[1]);
+  }
+  {
+    const auto lo = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(v),
+                                                     static_cast<uint32_t>(v), false, false);
+    const auto hi = __builtin_amdgcn_permlane32_swap(static_cast<uint32_t>(v >> 32),
+                                                     static_cast<uint32_t>(v >> 32), false, false);
+    v = mk64(lo[0], hi[0]) + mk64(lo[1], hi[1]);
+  }
   return v;
 }
 
@@ -273,8 +303,279 @@ __device__ uint64_t wave_xxh3_64(const uint8_t* p, uint32_t len, uint32_t lane,
   return xxh3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
 }
 
+// ---------------------------------------------------------------------------
+// Pipelined XXH3 block kernel: a wave walks its blocks as a stream of
+// (block, round) items, a round being up to 4 XXH3-blocks (4 KiB); the loads
+// of the next item are issued before the current round's reductions and
+// scramble chain run, so every wave keeps 4 KiB in flight while computing.
+// ---------------------------------------------------------------------------
+struct XxJob {
+  uint64_t i;
+  const uint8_t* p;
+  uint32_t len, nb, nbS, R, m, ml;
+  uint32_t stored, mod, last;
+  bool valid;
+};
+
+// Per-accumulator-pair constants used once per block (last-stripe keys,
+// merge keys, XXH3_INIT_ACC), evaluated at compile time from the secret and
+// read from constant memory at use so they do not occupy registers.
+constexpr uint8_t kSecC[192] = {
+    0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad,
+    0x1c, 0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3,
+    0x67, 0x1f, 0xcb, 0x79, 0xe6, 0x4e, 0xcc, 0xc0, 0xe5, 0x78, 0x82, 0x5a, 0xd0, 0x7d, 0xcc,
+    0xff, 0x72, 0x21, 0xb8, 0x08, 0x46, 0x74, 0xf7, 0x43, 0x24, 0x8e, 0xe0, 0x35, 0x90, 0xe6,
+    0x81, 0x3a, 0x26, 0x4c, 0x3c, 0x28, 0x52, 0xbb, 0x91, 0xc3, 0x00, 0xcb, 0x88, 0xd0, 0x65,
+    0x8b, 0x1b, 0x53, 0x2e, 0xa3, 0x71, 0x64, 0x48, 0x97, 0xa2, 0x0d, 0xf9, 0x4e, 0x38, 0x19,
+    0xef, 0x46, 0xa9, 0xde, 0xac, 0xd8, 0xa8, 0xfa, 0x76, 0x3f, 0xe3, 0x9c, 0x34, 0x3f, 0xf9,
+    0xdc, 0xbb, 0xc7, 0xc7, 0x0b, 0x4f, 0x1d, 0x8a, 0x51, 0xe0, 0x4b, 0xcd, 0xb4, 0x59, 0x31,
+    0xc8, 0x9f, 0x7e, 0xc9, 0xd9, 0x78, 0x73, 0x64, 0xea, 0xc5, 0xac, 0x83, 0x34, 0xd3, 0xeb,
+    0xc3, 0xc5, 0x81, 0xa0, 0xff, 0xfa, 0x13, 0x63, 0xeb, 0x17, 0x0d, 0xdd, 0x51, 0xb7, 0xf0,
+    0xda, 0x49, 0xd3, 0x16, 0x55, 0x26, 0x29, 0xd4, 0x68, 0x9e, 0x2b, 0x16, 0xbe, 0x58, 0x7d,
+    0x47, 0xa1, 0xfc, 0x8f, 0xf8, 0xb8, 0xd1, 0x7a, 0xd0, 0x31, 0xce, 0x45, 0xcb, 0x3a, 0x8f,
+    0x95, 0x16, 0x04, 0x28, 0xaf, 0xd7, 0xfb, 0xca, 0xbb, 0x4b, 0x40, 0x7e};
+constexpr uint64_t rd64c(uint32_t off) {
+  uint64_t v = 0;
+  for (int i = 7; i >= 0; --i) v = (v << 8) | kSecC[off + i];
+  return v;
+}
+enum { kColdL0 = 0, kColdL1, kColdM0, kColdM1, kColdI0, kColdI1, kColdN };
+#define FORST_XX_COLD(p, i0, i1)                                                           \
+  {rd64c(121 + 16 * (p)), rd64c(121 + 16 * (p) + 8), rd64c(11 + 16 * (p)),                 \
+   rd64c(11 + 16 * (p) + 8), (i0), (i1)}
+__device__ __constant__ const uint64_t kXxCold[4][kColdN] = {
+    FORST_XX_COLD(0, P32_3, P64_1), FORST_XX_COLD(1, P64_2, P64_3),
+    FORST_XX_COLD(2, P64_4, P32_2), FORST_XX_COLD(3, P64_5, P32_1)};
+#undef FORST_XX_COLD
+
+struct HotKeys {
+  uint64_t k0, k1;    // accumulate keys for (stripe L/4, pair L%4)
+  uint64_t ks0, ks1;  // scramble keys for accumulators 2p, 2p+1
+};
+__device__ __forceinline__ HotKeys hot_keys(uint32_t lane) {
+  const uint32_t s = lane >> 2, p = lane & 3;
+  return HotKeys{sec64(8 * s + 16 * p), sec64(8 * s + 16 * p + 8),
+                 sec64(192 - 64 + 16 * p), sec64(192 - 64 + 16 * p + 8)};
+}
+
+// XXH3-blocks per pipeline round (each lane holds 5 dwords per XXH3-block per
+// buffer; 2 keeps the double-buffered kernel under 128 VGPRs = 16 waves/CU)
+constexpr int kXxRound = 2;
+
+struct XxData {
+  uint32_t x[kXxRound][5];
+  uint32_t l[5];
+};
+
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) xxh3_block_kernel(BlockArgs a) {
+__device__ __forceinline__ XxJob xx_setup(const BlockArgs& a, uint64_t i, uint32_t lane) {
+  XxJob j;
+  j.i = i;
+  j.valid = false;
+  j.p = a.base;
+  j.len = j.nb = j.nbS = j.R = j.m = j.ml = 0;
+  j.stored = j.mod = j.last = 0;
+  if (i >= a.n) return j;
+  const uint64_t off = a.offsets[i];
+  const uint32_t size = a.sizes[i];
+  uint64_t need = size;
+  if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
+  if (MODE == kModeCompute && a.last_bytes == nullptr) need += 1;
+  j.valid = off <= a.base_len && need <= a.base_len - off;
+  if (!j.valid) return j;
+  const uint8_t* p = a.base + off;
+  j.p = p;
+  j.len = size;
+  j.mod = a.modifiers ? a.modifiers[i] : 0u;
+  if (MODE == kModeVerify) {
+    j.stored = ldu32(p + size + 1);
+    j.last = ldu8(p + size);
+  } else if (MODE != kModeRaw) {
+    j.last = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
+  }
+  if (size <= 240) return j;  // R = 0: length-class formulas
+  const uint64_t A = reinterpret_cast<uint64_t>(p);
+  j.nb = (size - 1) / 1024;
+  j.nbS = ((size - 1) - 1024 * j.nb) / 64;
+  j.R = (j.nb + kXxRound) / kXxRound;  // rounds over XXH3-blocks 0..nb
+  j.m = static_cast<uint32_t>(A & 3);
+  j.ml = static_cast<uint32_t>((A + size) & 3);
+  (void)lane;
+  return j;
+}
+
+__device__ __forceinline__ void xx_load(XxData& d, const XxJob& j, uint32_t r, uint32_t lane) {
+  if (j.R == 0) return;
+  const uint32_t s = lane >> 2;
+  // this lane's 16-byte slot of XXH3-block 0, dword aligned
+  const uint8_t* q = j.p - j.m + 16 * lane;
+#pragma unroll
+  for (int k = 0; k < kXxRound; ++k) {
+    const uint32_t g = kXxRound * r + k;
+    if (g > j.nb) break;
+    if (g < j.nb || s < j.nbS) {
+      const uint8_t* src = q + 1024ull * g;
+      const u32x4a4 v = ld16_a4(src);
+      d.x[k][0] = v.x;
+      d.x[k][1] = v.y;
+      d.x[k][2] = v.z;
+      d.x[k][3] = v.w;
+      if (j.m) d.x[k][4] = ld4_a4(src + 16);
+    }
+  }
+  if (r + 1 == j.R) {  // last stripe: this lane's pair of the 64 bytes at len-64
+    const uint8_t* lq = j.p + j.len - 64 + 16 * (lane & 3) - j.ml;
+    const u32x4a4 v = ld16_a4(lq);
+    d.l[0] = v.x;
+    d.l[1] = v.y;
+    d.l[2] = v.z;
+    d.l[3] = v.w;
+    if (j.ml) d.l[4] = ld4_a4(lq + 16);
+  }
+}
+
+__device__ __forceinline__ void xx_words(const uint32_t (&x)[5], uint32_t m, uint64_t& d0,
+                                         uint64_t& d1) {
+  uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
+  if (m) {
+    x0 = __builtin_amdgcn_alignbyte(x[1], x[0], m);
+    x1 = __builtin_amdgcn_alignbyte(x[2], x[1], m);
+    x2 = __builtin_amdgcn_alignbyte(x[3], x[2], m);
+    x3 = __builtin_amdgcn_alignbyte(x[4], x[3], m);
+  }
+  d0 = mk64(x0, x1);
+  d1 = mk64(x2, x3);
+}
+
+// round r of job j; returns true (and the hash in h) after the last round
+__device__ __forceinline__ bool xx_round(const XxJob& j, uint32_t r, uint32_t lane,
+                                         const HotKeys& K, const XxData& d, uint64_t& acc0,
+                                         uint64_t& acc1, uint64_t& h) {
+  const uint32_t s = lane >> 2;
+  const uint64_t* cold = kXxCold[lane & 3];
+  if (r == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
+    acc0 = cold[kColdI0];
+    acc1 = cold[kColdI1];
+  }
+  uint64_t c0[kXxRound], c1[kXxRound];
+#pragma unroll
+  for (int k = 0; k < kXxRound; ++k) {
+    const uint32_t g = kXxRound * r + k;
+    c0[k] = c1[k] = 0;
+    if (g > j.nb) break;
+    if (g < j.nb || s < j.nbS) {
+      uint64_t d0, d1;
+      xx_words(d.x[k], j.m, d0, d1);
+      c0[k] = mul32to64(d0 ^ K.k0) + d1;  // acc[2p]   (xxhash.h:4926-4927)
+      c1[k] = d0 + mul32to64(d1 ^ K.k1);  // acc[2p+1]
+    }
+  }
+#pragma unroll
+  for (int k = 0; k < kXxRound; ++k) {
+    const uint32_t g = kXxRound * r + k;
+    if (g > j.nb) break;
+    acc0 += stripe_sum(c0[k]);
+    acc1 += stripe_sum(c1[k]);
+    if (g < j.nb) {  // full XXH3-block: scramble (xxhash.h:5126-5128)
+      acc0 = scramble(acc0, K.ks0);
+      acc1 = scramble(acc1, K.ks1);
+    }
+  }
+  if (r + 1 != j.R) return false;
+  {  // last stripe at len-64 (xxhash.h:5146-5151)
+    uint64_t d0, d1;
+    xx_words(d.l, j.ml, d0, d1);
+    acc0 += mul32to64(d0 ^ cold[kColdL0]) + d1;
+    acc1 += d0 + mul32to64(d1 ^ cold[kColdL1]);
+  }
+  uint64_t t = mul128_fold64(acc0 ^ cold[kColdM0], acc1 ^ cold[kColdM1]);  // mergeAccs
+  t += shfl_xor64(t, 1);
+  t += shfl_xor64(t, 2);
+  h = xxh3_avalanche(static_cast<uint64_t>(j.len) * P64_1 + t);
+  return true;
+}
+
+template <int MODE>
+__device__ __forceinline__ void xx_finish(const BlockArgs& a, const XxJob& j, uint32_t lane,
+                                          uint64_t h) {
+  if (lane != 0) return;
+  if (!j.valid) {
+    if (a.out32) a.out32[j.i] = 0;
+    if (MODE == kModeRaw && a.out64) a.out64[j.i] = 0;
+    if (MODE == kModeVerify) {
+      if (a.ok_out) a.ok_out[j.i] = 0;
+      if (a.stored_out) a.stored_out[j.i] = 0;
+      if (a.mismatches) atomicAdd(a.mismatches, 1ull);
+    }
+    return;
+  }
+  if (MODE == kModeRaw) {
+    a.out64[j.i] = h;
+  } else if (MODE == kModeVerify) {
+    const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), j.last);
+    const uint32_t stored = j.stored - j.mod;
+    const bool ok = stored == computed;
+    if (a.out32) a.out32[j.i] = computed;
+    if (a.stored_out) a.stored_out[j.i] = stored;
+    if (a.ok_out) a.ok_out[j.i] = ok ? 1 : 0;
+    if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
+  } else {
+    const uint32_t c = modify_for_last_byte(static_cast<uint32_t>(h), j.last) + j.mod;
+    if (a.out32) a.out32[j.i] = c;
+    if (MODE == kModeTrailer) {
+      uint8_t* w = a.base_w + (j.p - a.base) + j.len;
+      w[0] = static_cast<uint8_t>(j.last);
+      stu32_bytes(w + 1, c);
+    }
+  }
+}
+
+template <int MODE>
+// (kThreads, 4): >= 4 waves per SIMD, i.e. <= 128 VGPRs -- 16 waves per CU
+// keep enough 4 KiB rounds in flight (measured: 152 VGPRs unconstrained).
+__global__ void __launch_bounds__(kThreads, 4) xxh3_block_kernel(BlockArgs a) {
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const HotKeys K = hot_keys(lane);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  XxJob cur = xx_setup<MODE>(a, static_cast<uint64_t>(blockIdx.x) * kWaves + wave, lane);
+  XxData dA, dB;
+  xx_load(dA, cur, 0, lane);
+  uint32_t r = 0;
+  uint64_t acc0 = 0, acc1 = 0;
+  auto step = [&](XxData& dc, XxData& dn) {
+    const bool same = cur.valid && cur.R > 0 && r + 1 < cur.R;
+    XxJob nxt = cur;
+    if (same) {
+      xx_load(dn, cur, r + 1, lane);
+    } else {
+      nxt = xx_setup<MODE>(a, cur.i + nw, lane);
+      xx_load(dn, nxt, 0, lane);
+    }
+    if (!cur.valid) {
+      xx_finish<MODE>(a, cur, lane, 0);
+    } else if (cur.R == 0) {
+      xx_finish<MODE>(a, cur, lane, xxh3_short(cur.p, cur.len));
+    } else {
+      uint64_t h = 0;
+      if (xx_round(cur, r, lane, K, dc, acc0, acc1, h)) xx_finish<MODE>(a, cur, lane, h);
+    }
+    if (same) {
+      ++r;
+    } else {
+      cur = nxt;
+      r = 0;
+    }
+  };
+  while (cur.i < a.n) {
+    step(dA, dB);
+    if (cur.i >= a.n) break;
+    step(dB, dA);
+  }
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) xxh3_block_kernel_simple(BlockArgs a) {
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const LaneKeys K = lane_keys(lane);
@@ -371,24 +672,35 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   const uint64_t want = (a.n + kWaves - 1) / kWaves;
   const uint32_t grid = static_cast<uint32_t>(
       std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
+  // FORST_XXH3_VARIANT=simple selects the unpipelined kernel (A/B reference)
+  const char* variant = std::getenv("FORST_XXH3_VARIANT");
+  const bool simple = variant && std::string(variant) == "simple";
+#define FORST_LAUNCH_XXH3(M, TAG)                                                          \
+  do {                                                                                     \
+    if (simple) {                                                                          \
+      *name = "xxh3_block_kernel_simple<" TAG ">";                                         \
+      hipLaunchKernelGGL(xxh3_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,       \
+                         stream, a);                                                       \
+    } else {                                                                               \
+      *name = "xxh3_block_kernel<" TAG ">";                                                \
+      hipLaunchKernelGGL(xxh3_block_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, a);  \
+    }                                                                                      \
+  } while (0)
   switch (mode) {
     case kModeCompute:
-      *name = "xxh3_block_kernel<compute>";
-      hipLaunchKernelGGL(xxh3_block_kernel<kModeCompute>, dim3(grid), dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_XXH3(kModeCompute, "compute");
       break;
     case kModeTrailer:
-      *name = "xxh3_block_kernel<trailer>";
-      hipLaunchKernelGGL(xxh3_block_kernel<kModeTrailer>, dim3(grid), dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_XXH3(kModeTrailer, "trailer");
       break;
     case kModeVerify:
-      *name = "xxh3_block_kernel<verify>";
-      hipLaunchKernelGGL(xxh3_block_kernel<kModeVerify>, dim3(grid), dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_XXH3(kModeVerify, "verify");
       break;
     default:
-      *name = "xxh3_block_kernel<raw>";
-      hipLaunchKernelGGL(xxh3_block_kernel<kModeRaw>, dim3(grid), dim3(kThreads), 0, stream, a);
+      FORST_LAUNCH_XXH3(kModeRaw, "raw");
       break;
   }
+#undef FORST_LAUNCH_XXH3
   return hipGetLastError();
 }
 

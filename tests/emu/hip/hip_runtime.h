@@ -117,6 +117,35 @@ inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return emu::exchang
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8 * (s & 3)));
 }
+// DPP: only the row_ror:n controls (0x121..0x12f) are used by the kernels
+inline uint32_t __builtin_amdgcn_update_dpp(uint32_t, uint32_t src, int ctrl, int, int, bool) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  const uint32_t n = static_cast<uint32_t>(ctrl - 0x120) & 15;
+  return emu::exchange(src, (lane & ~15u) | ((lane - n) & 15u));
+}
+typedef uint32_t emu_u32x2 __attribute__((ext_vector_type(2)));
+// v_permlane16_swap / v_permlane32_swap: swap odd 16-lane rows (upper 32-lane
+// half) of `old` with even rows (lower half) of `src`; returns {old', src'}
+inline emu_u32x2 __builtin_amdgcn_permlane16_swap(uint32_t old, uint32_t src, bool, bool) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  const uint32_t o_partner = emu::exchange(old, lane ^ 16);
+  const uint32_t s_partner = emu::exchange(src, lane ^ 16);
+  const bool odd = (lane >> 4) & 1;
+  emu_u32x2 r;
+  r[0] = odd ? s_partner : old;  // odd rows of old <- even rows of src
+  r[1] = odd ? src : o_partner;  // even rows of src <- odd rows of old
+  return r;
+}
+inline emu_u32x2 __builtin_amdgcn_permlane32_swap(uint32_t old, uint32_t src, bool, bool) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  const uint32_t o_partner = emu::exchange(old, lane ^ 32);
+  const uint32_t s_partner = emu::exchange(src, lane ^ 32);
+  const bool hi = (lane >> 5) & 1;
+  emu_u32x2 r;
+  r[0] = hi ? s_partner : old;
+  r[1] = hi ? src : o_partner;
+  return r;
+}
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }

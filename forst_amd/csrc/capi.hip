@@ -95,8 +95,8 @@ int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
       break;
     case FORST_kxxHash:
     case FORST_kxxHash64:
-      return set_error(FORST_EUNSUPPORTED,
-                       "kxxHash/kxxHash64 are not implemented by the GPU engine yet");
+      e = launch_xxhash_legacy_blocks(type == FORST_kxxHash64, mode, a, s, &g_last_kernel);
+      break;
     default:
       // options_helper.h:34 IsSupportedChecksumType rejects > kXXH3
       return set_error(FORST_EINVAL, "unknown ChecksumType " + std::to_string(type));

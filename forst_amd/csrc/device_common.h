@@ -38,6 +38,20 @@ __device__ __forceinline__ uint32_t vzero() {
   return z;
 }
 
+// Copy through an opaque v_mov: the load that produced `v` is waited for HERE
+// and the result is no longer a load destination.  Used on rarely taken
+// branches whose loaded values merge into a hot path, where hipcc would
+// otherwise place a draining s_waitcnt vmcnt(0) after the join.
+__device__ __forceinline__ uint32_t retire(uint32_t v) {
+  uint32_t r;
+#ifndef FORST_HOST_EMULATION
+  asm volatile("v_mov_b32 %0, %1" : "=v"(r) : "v"(v));
+#else
+  r = v;
+#endif
+  return r;
+}
+
 #ifdef FORST_DEBUG_BOUNDS
 // Diagnostics build only (make DEBUG_BOUNDS=1 -> lib/libforst_checksum_dbg.so):
 // every block-data load is checked against the launch's buffer bounds; the

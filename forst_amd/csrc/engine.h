@@ -64,6 +64,9 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
 hipError_t launch_noop_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
+// kxxHash (x64 = false, XXH32) / kxxHash64 (x64 = true, Lower32 of XXH64)
+hipError_t launch_xxhash_legacy_blocks(bool x64, int mode, const BlockArgs& a,
+                                       hipStream_t stream, const char** kernel_name);
 hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
                              const char** kernel_name);
 hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,

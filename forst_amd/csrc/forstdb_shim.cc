@@ -26,7 +26,7 @@ std::string Status::ToString() const {
 }
 
 bool GpuSupportsChecksumType(ChecksumType t) {
-  return t == kNoChecksum || t == kCRC32c || t == kXXH3;
+  return t == kNoChecksum || t == kCRC32c || t == kxxHash || t == kxxHash64 || t == kXXH3;
 }
 
 // table/block_based/reader_common.cc:55-60

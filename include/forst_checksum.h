@@ -70,7 +70,7 @@ enum forst_checksum_type {
 /* return codes */
 #define FORST_OK 0
 #define FORST_EINVAL (-1)        /* bad pointer / size / alignment */
-#define FORST_EUNSUPPORTED (-2)  /* ChecksumType not handled by the GPU engine */
+#define FORST_EUNSUPPORTED (-2)  /* reserved: ChecksumType not handled (all 5 are) */
 #define FORST_EHIP (-3)          /* HIP runtime error (see forst_last_error) */
 #define FORST_ENODEV (-4)        /* no gfx950 device / code object not loadable */
 

@@ -44,7 +44,9 @@ static void pure() {
   CHECK(ChecksumModifierForContext(7, 0x100000001ull) == (7u ^ 2u));
   CHECK(IsSupportedChecksumType(kXXH3));
   CHECK(!IsSupportedChecksumType(static_cast<ChecksumType>(5)));
-  CHECK(GpuSupportsChecksumType(kCRC32c) && !GpuSupportsChecksumType(kxxHash));
+  CHECK(GpuSupportsChecksumType(kCRC32c) && GpuSupportsChecksumType(kxxHash) &&
+        GpuSupportsChecksumType(kxxHash64) &&
+        !GpuSupportsChecksumType(static_cast<ChecksumType>(5)));
   // reader_common.cc:55-60 exact format
   Status s = Status::Corruption(
       BlockChecksumMismatchMessage(kCRC32c, 1, 2, false, "f.sst", 7, 4096));

@@ -113,13 +113,34 @@ inline void __syncthreads() { emu::tl_group->bar->arrive_and_wait(); }
 inline uint32_t __shfl_xor(uint32_t v, int mask) {
   return emu::exchange(v, (emu::tl_tid.x & 63) ^ static_cast<uint32_t>(mask));
 }
+inline uint32_t __shfl(uint32_t v, int src) {
+  return emu::exchange(v, static_cast<uint32_t>(src));
+}
 inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return emu::exchange(v, 0); }
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8 * (s & 3)));
 }
-// DPP: only the row_ror:n controls (0x121..0x12f) are used by the kernels
-inline uint32_t __builtin_amdgcn_update_dpp(uint32_t, uint32_t src, int ctrl, int, int, bool) {
+inline uint32_t __builtin_amdgcn_readlane(uint32_t v, uint32_t l) { return emu::exchange(v, l); }
+inline unsigned long long __ballot(int pred) {
+  emu::Wave& w = emu::tl_group->waves[emu::tl_tid.x >> 6];
   const uint32_t lane = emu::tl_tid.x & 63;
+  w.slot[lane] = pred ? 1u : 0u;
+  w.bar->arrive_and_wait();
+  unsigned long long m = 0;
+  for (uint32_t l = 0; l < 64; ++l) m |= static_cast<unsigned long long>(w.slot[l] & 1u) << l;
+  w.bar->arrive_and_wait();
+  return m;
+}
+inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+// DPP: row_shr:n (0x111..0x11f; lane i <- lane i-n in its row, else `old`)
+// and row_ror:n (0x121..0x12f; lane i <- lane (i-n) mod 16 of its row)
+inline uint32_t __builtin_amdgcn_update_dpp(uint32_t old, uint32_t src, int ctrl, int, int, bool) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  if (ctrl > 0x110 && ctrl < 0x120) {
+    const uint32_t n = static_cast<uint32_t>(ctrl - 0x110);
+    const uint32_t v = emu::exchange(src, (lane & 15u) >= n ? lane - n : lane);
+    return (lane & 15u) >= n ? v : old;
+  }
   const uint32_t n = static_cast<uint32_t>(ctrl - 0x120) & 15;
   return emu::exchange(src, (lane & ~15u) | ((lane - n) & 15u));
 }

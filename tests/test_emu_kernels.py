@@ -47,6 +47,20 @@ def test_emu_xxh3_and_blocks(golden_arrays):
         assert (got == np.array([r["with_last"][t] for r in v["vectors"]], np.uint32)).all()
 
 
+def test_emu_xxhash_legacy_blocks(golden_arrays):
+    # kxxHash / kxxHash64 (format.cc:573-576, :603-622) against the reference
+    v, arr, offs, lens = golden_arrays
+    for t in (2, 3):
+        got = emu.block_checksum(t, arr, offs, lens)
+        assert (got == np.array([r["with_last"][t] for r in v["vectors"]], np.uint32)).all()
+        # virtual last byte (last_bytes[] given, type byte not in memory)
+        last = np.array([arr[int(o) + int(n)] for o, n in zip(offs, lens)], np.uint8)
+        got = emu.block_checksum(t, arr, offs, lens, last=last)
+        assert (got == np.array([r["with_last"][t] for r in v["vectors"]], np.uint32)).all()
+        comp, st, ok, bad = emu.block_verify(t, arr, offs, lens)
+        assert (comp == np.array([r["builtin_plus1"][t] for r in v["vectors"]], np.uint32)).all()
+
+
 def test_emu_trailer_roundtrip_mixed():
     rng = np.random.default_rng(8)
     sizes = rng.integers(0, 9000, 400).astype(np.uint32)
@@ -56,7 +70,7 @@ def test_emu_trailer_roundtrip_mixed():
     base = rng.integers(0, 256, total, dtype=np.uint8)
     types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
     mods = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
-    for t in (1, 4):
+    for t in (1, 2, 3, 4):
         b2, out = emu.block_trailer(t, base, offs, sizes, types, mods)
         want = O.block_checksum_batch(t, base, offs, sizes, last_bytes=types, modifiers=mods)
         assert (out == want).all()
@@ -74,3 +88,44 @@ def test_emu_wal():
     buf, poffs, plens = O.wal_frame(payload, lens)
     st, nrec, fail, bad = emu.wal_verify(buf)
     assert bad == 0 and (st == 0).all() and int(nrec.sum()) == len(poffs)
+
+
+def test_emu_crc_stream_batches_and_edges():
+    """> 64 blocks per wave (descriptor/result batch switches), the 64-byte
+    fast-path threshold, every start alignment, a block at the buffer start
+    (head lane would underflow -> wave_crc32c path), all CRC modes."""
+    rng = np.random.default_rng(21)
+    n = 2600
+    sizes = rng.integers(0, 700, n).astype(np.uint32)
+    sizes[:40] = np.arange(40) + 40          # 40..79 around the threshold
+    sizes[40:48] = [4091, 4092, 4093, 4094, 4095, 4096, 8191, 12000]
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 5 + rng.integers(0, 4, n - 1))
+    total = int(offs[-1]) + int(sizes[-1]) + 5 + 4096
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    types = rng.integers(0, 8, n, dtype=np.uint8)
+    mods = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    # compute, type byte from memory and from last_bytes[]
+    want = O.block_checksum_batch(1, base, offs, sizes, modifiers=mods)
+    assert (emu.block_checksum(1, base, offs, sizes, mods=mods) == want).all()
+    want = O.block_checksum_batch(1, base, offs, sizes, last_bytes=types, modifiers=mods)
+    assert (emu.block_checksum(1, base, offs, sizes, last=types, mods=mods) == want).all()
+    # trailer then verify (with a corruption)
+    b2, out = emu.block_trailer(1, base, offs, sizes, types, mods)
+    assert (out == want).all()
+    b2[int(offs[7]) + 3] ^= 0x10
+    comp, st, ok, bad = emu.block_verify(1, b2, offs, sizes, mods)
+    assert bad == 1 and not ok[7] and ok.sum() == n - 1
+    # raw crc32c::Extend with per-message init
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = emu.crc32c(base, offs, sizes, init=init)
+    for k in range(0, n, 37):
+        o, s = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.crc32c_extend(int(init[k]), base[o:o + s]), (k, s, o & 3)
+    # messages at the very start of the buffer (round-0 head would underflow)
+    offs2 = np.array([0, 1, 2, 3, 70, 4100], np.uint64)
+    sizes2 = np.array([5000, 4999, 64, 4093, 100, 9000], np.uint32)
+    got = emu.crc32c(base, offs2, sizes2)
+    for k in range(len(offs2)):
+        o, s = int(offs2[k]), int(sizes2[k])
+        assert int(got[k]) == O.crc32c_extend(0, base[o:o + s]), k

@@ -23,6 +23,7 @@ CONFIGS = {
     "C3": (1 << 20, (4096, 16384, 65536), 4), "C3CRC": (1 << 20, (4096, 16384, 65536), 1),
     "X4": (1 << 20, 4096, 4), "DEV4": (1 << 20, ("dev", 4096), 1),
     "C64": (1 << 18, 65536, 1), "X64": (1 << 18, 65536, 4),
+    "H32": (1 << 20, 16384, 2), "H64": (1 << 20, 16384, 3), "H64S": (1 << 20, 4096, 3),
 }
 
 

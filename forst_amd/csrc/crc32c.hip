@@ -27,6 +27,7 @@
 #include "crc32c_tables.h"
 #include "device_common.h"
 #include "engine.h"
+#include "stream_common.h"
 
 namespace forst {
 namespace {
@@ -232,7 +233,6 @@ __device__ __forceinline__ void fill_tables(uint32_t* L) {
 // Blocks shorter than 64 bytes, blocks whose round-0 head lane would read in
 // front of the buffer, and out-of-range descriptors take the wave_crc32c path.
 // ---------------------------------------------------------------------------
-constexpr uint32_t kBatch = 64;
 constexpr uint32_t kOffTinv = kLdsDwords;  // 256-byte inverse of T3's top byte
 constexpr uint32_t kLdsDwordsStream = kLdsDwords + 64;
 static_assert(kLdsDwordsStream * 4 <= 160 * 1024, "stream kernel LDS");
@@ -254,33 +254,6 @@ __device__ __forceinline__ uint32_t crc_unstep(const uint32_t* __restrict__ L, u
   return ((sp ^ t) << 8) | b;
 }
 
-// per-lane descriptor batch (lane j <-> block kb + j)
-struct DescBatch {
-  uint32_t off_lo, off_hi, size, mod, extra;
-};
-
-template <int MODE>
-__device__ __forceinline__ void load_batch(const BlockArgs& a, uint64_t kb, uint64_t kend,
-                                           uint32_t lane, DescBatch& d) {
-  uint64_t i = kb + lane;
-  i = i < kend ? i : kend - 1;  // clamped: loads are unconditional
-  const uint64_t off = a.offsets[i];
-  d.off_lo = static_cast<uint32_t>(off);
-  d.off_hi = static_cast<uint32_t>(off >> 32);
-  d.size = a.sizes[i];
-  const uint32_t* mp = a.modifiers ? a.modifiers : a.sizes;
-  const uint32_t mv = mp[i];
-  d.mod = a.modifiers ? mv : 0u;
-  if (MODE == kModeRaw) {
-    const uint32_t* ip = a.init_crcs ? a.init_crcs : a.sizes;
-    const uint32_t iv = ip[i];
-    d.extra = a.init_crcs ? iv : 0u;
-  } else {
-    const uint8_t* lp = a.last_bytes ? a.last_bytes : reinterpret_cast<const uint8_t*>(a.sizes);
-    d.extra = lp[i];
-  }
-}
-
 // wave-uniform description of one block (lives in SGPRs)
 struct Blk {
   uint64_t off;     // message start (offset from base)
@@ -292,40 +265,22 @@ struct Blk {
   bool valid, slow;
 };
 
-__device__ __forceinline__ uint64_t readlane64(uint32_t lo, uint32_t hi, uint32_t l) {
-  return (static_cast<uint64_t>(__builtin_amdgcn_readlane(hi, l)) << 32) |
-         __builtin_amdgcn_readlane(lo, l);
-}
-
 template <int MODE>
 __device__ __forceinline__ Blk blk_setup(const BlockArgs& a, const uint32_t* __restrict__ L,
                                          uint32_t lb, uint64_t k, uint64_t kend, uint64_t kb,
                                          const DescBatch& cb, const DescBatch& nb,
                                          const uint32_t (&kS0)[4]) {
   Blk b;
-  const uint32_t kk = static_cast<uint32_t>(k - kb);  // 0..127 (k may be >= kend)
-  const uint32_t sl = kk & 63u;
-  const bool in_n = kk >= 64;
-  const uint64_t off_c = readlane64(cb.off_lo, cb.off_hi, sl);
-  const uint64_t off_n = readlane64(nb.off_lo, nb.off_hi, sl);
-  b.off = in_n ? off_n : off_c;
-  const uint32_t size_c = __builtin_amdgcn_readlane(cb.size, sl);
-  const uint32_t size_n = __builtin_amdgcn_readlane(nb.size, sl);
-  b.size = in_n ? size_n : size_c;
-  const uint32_t mod_c = __builtin_amdgcn_readlane(cb.mod, sl);
-  const uint32_t mod_n = __builtin_amdgcn_readlane(nb.mod, sl);
-  b.mod = in_n ? mod_n : mod_c;
-  const uint32_t ex_c = __builtin_amdgcn_readlane(cb.extra, sl);
-  const uint32_t ex_n = __builtin_amdgcn_readlane(nb.extra, sl);
-  b.extra = in_n ? ex_n : ex_c;
+  const Desc d = batch_desc(k, kb, cb, nb);  // k may be >= kend (then invalid)
+  b.off = d.off;
+  b.size = d.size;
+  b.mod = d.mod;
+  b.extra = d.extra;
 
   const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
   const bool mem_last = MODE == kModeVerify || ((MODE == kModeCompute || MODE == kModeTrailer) &&
                                                 !a.last_bytes);
-  uint64_t need = b.size;
-  if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
-  if (MODE == kModeCompute && !a.last_bytes) need += 1;
-  b.valid = k < kend && b.off <= a.base_len && need <= a.base_len - b.off;
+  b.valid = k < kend && desc_in_range<MODE>(a, d);
   (void)has_extra;
   b.len = b.size + (mem_last ? 1u : 0u);
 
@@ -430,10 +385,10 @@ __device__ __forceinline__ uint32_t stream_finish(const uint32_t* __restrict__ L
   s = tree_level<2>(L, lane, s);
   s = tree_level<3>(L, lane, s);
   // levels 4..5 on the row results (wave-uniform: broadcast LDS reads)
-  const uint32_t g0 = __builtin_amdgcn_readlane(s, 15);
-  const uint32_t g1 = __builtin_amdgcn_readlane(s, 31);
-  const uint32_t g2 = __builtin_amdgcn_readlane(s, 47);
-  const uint32_t g3 = __builtin_amdgcn_readlane(s, 63);
+  const uint32_t g0 = readlane32(s, 15);
+  const uint32_t g1 = readlane32(s, 31);
+  const uint32_t g2 = readlane32(s, 47);
+  const uint32_t g3 = readlane32(s, 63);
   const uint32_t t01 = crc_shift(L, kOffTree + 1024u * 4, g0) ^ g1;
   const uint32_t t23 = crc_shift(L, kOffTree + 1024u * 4, g2) ^ g3;
   uint32_t st = crc_shift(L, kOffTree + 1024u * 5, t01) ^ t23;
@@ -456,9 +411,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(BlockArgs a) {
   const uint32_t lb = (lane & 31) << 2;
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-  const uint64_t q = a.n / nw, rem = a.n % nw;
-  const uint64_t kbeg = gw * q + (gw < rem ? gw : rem);
-  const uint64_t kend = kbeg + q + (gw < rem ? 1 : 0);
+  uint64_t kbeg, kend;
+  wave_share(a.n, nw, gw, kbeg, kend);
   if (kbeg >= kend) return;
   const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
 

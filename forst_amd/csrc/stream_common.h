@@ -1,0 +1,94 @@
+// forst_amd/csrc/stream_common.h -- pieces shared by the streaming block
+// kernels (crc32c.hip, xxh3.hip): per-wave contiguous shares, 64-entry
+// descriptor batches held one block per lane, and v_readlane helpers.
+//
+// A streaming kernel keeps one step of global loads in flight while it
+// computes the previous one.  That only works if no other VMEM load is
+// waited for in between (s_waitcnt vmcnt counts in issue order), so block
+// descriptors are fetched 64 at a time into VGPRs (lane j <-> block kb+j) and
+// read back into SGPRs with v_readlane; results are collected the same way
+// and stored once per batch.
+#pragma once
+#include "device_common.h"
+#include "engine.h"
+
+namespace forst {
+
+constexpr uint32_t kBatch = 64;
+
+// [kbeg, kend): wave gw's contiguous share of n blocks over nw waves
+__device__ __forceinline__ void wave_share(uint64_t n, uint64_t nw, uint64_t gw, uint64_t& kbeg,
+                                           uint64_t& kend) {
+  const uint64_t q = n / nw, rem = n % nw;
+  kbeg = gw * q + (gw < rem ? gw : rem);
+  kend = kbeg + q + (gw < rem ? 1 : 0);
+}
+
+// per-lane descriptor batch (lane j <-> block kb + j)
+struct DescBatch {
+  uint32_t off_lo, off_hi, size, mod, extra;  // extra: last byte, or init (raw CRC)
+};
+
+template <int MODE>
+__device__ __forceinline__ void load_batch(const BlockArgs& a, uint64_t kb, uint64_t kend,
+                                           uint32_t lane, DescBatch& d) {
+  uint64_t i = kb + lane;
+  i = i < kend ? i : kend - 1;  // clamped: the loads are unconditional
+  const uint64_t off = a.offsets[i];
+  d.off_lo = static_cast<uint32_t>(off);
+  d.off_hi = static_cast<uint32_t>(off >> 32);
+  d.size = a.sizes[i];
+  const uint32_t* mp = a.modifiers ? a.modifiers : a.sizes;
+  const uint32_t mv = mp[i];
+  d.mod = a.modifiers ? mv : 0u;
+  if (MODE == kModeRaw) {
+    const uint32_t* ip = a.init_crcs ? a.init_crcs : a.sizes;
+    const uint32_t iv = ip[i];
+    d.extra = a.init_crcs ? iv : 0u;
+  } else {
+    const uint8_t* lp = a.last_bytes ? a.last_bytes : reinterpret_cast<const uint8_t*>(a.sizes);
+    d.extra = lp[i];
+  }
+}
+
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
+  // (the builtin returns int: cast before any widening, or it sign-extends)
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(l)));
+}
+__device__ __forceinline__ uint64_t readlane64(uint32_t lo, uint32_t hi, uint32_t l) {
+  return (static_cast<uint64_t>(readlane32(hi, l)) << 32) | readlane32(lo, l);
+}
+
+// descriptor k (kb <= k < kb + 128) from the current / next batch, uniform
+struct Desc {
+  uint64_t off;
+  uint32_t size, mod, extra;
+};
+__device__ __forceinline__ Desc batch_desc(uint64_t k, uint64_t kb, const DescBatch& cb,
+                                           const DescBatch& nb) {
+  const uint32_t kk = static_cast<uint32_t>(k - kb);
+  const uint32_t sl = kk & 63u;
+  const bool in_n = kk >= 64;
+  Desc d;
+  const uint64_t off_c = readlane64(cb.off_lo, cb.off_hi, sl);
+  const uint64_t off_n = readlane64(nb.off_lo, nb.off_hi, sl);
+  d.off = in_n ? off_n : off_c;
+  const uint32_t size_c = readlane32(cb.size, sl), size_n = readlane32(nb.size, sl);
+  d.size = in_n ? size_n : size_c;
+  const uint32_t mod_c = readlane32(cb.mod, sl), mod_n = readlane32(nb.mod, sl);
+  d.mod = in_n ? mod_n : mod_c;
+  const uint32_t ex_c = readlane32(cb.extra, sl), ex_n = readlane32(nb.extra, sl);
+  d.extra = in_n ? ex_n : ex_c;
+  return d;
+}
+
+// bytes a block of this mode must have inside the buffer (reader / builder)
+template <int MODE>
+__device__ __forceinline__ bool desc_in_range(const BlockArgs& a, const Desc& d) {
+  uint64_t need = d.size;
+  if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
+  if (MODE == kModeCompute && !a.last_bytes) need += 1;
+  return d.off <= a.base_len && need <= a.base_len - d.off;
+}
+
+}  // namespace forst

@@ -15,6 +15,7 @@
 
 #include "device_common.h"
 #include "engine.h"
+#include "stream_common.h"
 
 namespace forst {
 namespace {
@@ -304,22 +305,18 @@ __device__ uint64_t wave_xxh3_64(const uint8_t* p, uint32_t len, uint32_t lane,
 }
 
 // ---------------------------------------------------------------------------
-// Pipelined XXH3 block kernel: a wave walks its blocks as a stream of
-// (block, round) items, a round being up to 4 XXH3-blocks (4 KiB); the loads
-// of the next item are issued before the current round's reductions and
-// scramble chain run, so every wave keeps 4 KiB in flight while computing.
+// Streaming XXH3 block kernel (same shape as crc32c_stream_kernel): a wave
+// walks its contiguous share of blocks as (block, round) steps, a round being
+// 4 XXH3-blocks (4 KiB: per lane 4 x (dwordx4 + the dword after it, for
+// unaligned starts)).  The loads of the next step -- plus the block's last
+// stripe and trailer dwords -- are issued unconditionally (clamped to a safe
+// address when not needed) before the current step's stripe sums and
+// scrambles run, so the compiler's wait for the current step leaves the next
+// one in flight.  Descriptors come in 64-block batches (stream_common.h);
+// per-lane cold constants live in LDS so no VMEM load sits in the loop.
 // ---------------------------------------------------------------------------
-struct XxJob {
-  uint64_t i;
-  const uint8_t* p;
-  uint32_t len, nb, nbS, R, m, ml;
-  uint32_t stored, mod, last;
-  bool valid;
-};
-
 // Per-accumulator-pair constants used once per block (last-stripe keys,
-// merge keys, XXH3_INIT_ACC), evaluated at compile time from the secret and
-// read from constant memory at use so they do not occupy registers.
+// merge keys, XXH3_INIT_ACC), evaluated at compile time from the secret.
 constexpr uint8_t kSecC[192] = {
     0xb8, 0xfe, 0x6c, 0x39, 0x23, 0xa4, 0x4b, 0xbe, 0x7c, 0x01, 0x81, 0x2c, 0xf7, 0x21, 0xad,
     0x1c, 0xde, 0xd4, 0x6d, 0xe9, 0x83, 0x90, 0x97, 0xdb, 0x72, 0x40, 0xa4, 0xa4, 0xb7, 0xb3,
@@ -358,80 +355,83 @@ __device__ __forceinline__ HotKeys hot_keys(uint32_t lane) {
                  sec64(192 - 64 + 16 * p), sec64(192 - 64 + 16 * p + 8)};
 }
 
-// XXH3-blocks per pipeline round (each lane holds 5 dwords per XXH3-block per
-// buffer; 2 keeps the double-buffered kernel under 128 VGPRs = 16 waves/CU)
-constexpr int kXxRound = 2;
+constexpr int kXxRound = 4;  // XXH3-blocks per step
 
-struct XxData {
-  uint32_t x[kXxRound][5];
-  uint32_t l[5];
+struct XBlk {
+  uint64_t off;
+  uint64_t q0;      // offset of lane 0's 16-byte slot of XXH3-block 0 (dword aligned)
+  uint64_t lq;      // offset of pair 0's slot of the last stripe (dword aligned)
+  uint64_t t0, t1;  // trailer dword offsets
+  uint32_t size, mod, extra;
+  uint32_t nb, nbS, R, m, ml, tb;  // tb: byte index of the type byte in t0
+  bool valid, slow;
 };
 
 template <int MODE>
-__device__ __forceinline__ XxJob xx_setup(const BlockArgs& a, uint64_t i, uint32_t lane) {
-  XxJob j;
-  j.i = i;
-  j.valid = false;
-  j.p = a.base;
-  j.len = j.nb = j.nbS = j.R = j.m = j.ml = 0;
-  j.stored = j.mod = j.last = 0;
-  if (i >= a.n) return j;
-  const uint64_t off = a.offsets[i];
-  const uint32_t size = a.sizes[i];
-  uint64_t need = size;
-  if (MODE == kModeVerify || MODE == kModeTrailer) need += 5;
-  if (MODE == kModeCompute && a.last_bytes == nullptr) need += 1;
-  j.valid = off <= a.base_len && need <= a.base_len - off;
-  if (!j.valid) return j;
-  const uint8_t* p = a.base + off;
-  j.p = p;
-  j.len = size;
-  j.mod = a.modifiers ? a.modifiers[i] : 0u;
-  if (MODE == kModeVerify) {
-    j.stored = ldu32(p + size + 1);
-    j.last = ldu8(p + size);
-  } else if (MODE != kModeRaw) {
-    j.last = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
+__device__ __forceinline__ XBlk xblk_setup(const BlockArgs& a, uint64_t k, uint64_t kend,
+                                           uint64_t kb, const DescBatch& cb,
+                                           const DescBatch& nb) {
+  XBlk b;
+  const Desc d = batch_desc(k, kb, cb, nb);
+  b.off = d.off;
+  b.size = d.size;
+  b.mod = d.mod;
+  b.extra = d.extra;
+  b.valid = k < kend && desc_in_range<MODE>(a, d);
+  b.slow = !b.valid || b.size <= 240;
+  b.nb = (b.size - 1) / 1024;
+  b.nbS = ((b.size - 1) - 1024 * b.nb) / 64;
+  b.R = (b.nb + kXxRound) / kXxRound;  // XXH3-blocks 0..nb
+  b.m = static_cast<uint32_t>(b.off & 3);
+  const uint64_t E = b.off + b.size;
+  b.ml = static_cast<uint32_t>(E & 3);
+  b.q0 = b.off - b.m;
+  b.lq = E - 64 - b.ml;
+  // type byte at E, stored LE32 at E+1 (verify); type byte only (compute /
+  // trailer without last_bytes[]); nothing otherwise (point at the block)
+  const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
+  b.tb = b.ml;
+  b.t0 = mem_last ? (E & ~3ull) : b.q0;
+  b.t1 = MODE == kModeVerify ? (E & ~3ull) + 4 : b.t0;
+  if (b.slow) {  // dummy loads at the buffer start
+    b.q0 = b.lq = b.t0 = b.t1 = 0;
+    b.nb = b.nbS = 0;
   }
-  if (size <= 240) return j;  // R = 0: length-class formulas
-  const uint64_t A = reinterpret_cast<uint64_t>(p);
-  j.nb = (size - 1) / 1024;
-  j.nbS = ((size - 1) - 1024 * j.nb) / 64;
-  j.R = (j.nb + kXxRound) / kXxRound;  // rounds over XXH3-blocks 0..nb
-  j.m = static_cast<uint32_t>(A & 3);
-  j.ml = static_cast<uint32_t>((A + size) & 3);
-  (void)lane;
-  return j;
+  return b;
 }
 
-__device__ __forceinline__ void xx_load(XxData& d, const XxJob& j, uint32_t r, uint32_t lane) {
-  if (j.R == 0) return;
+struct XStep {
+  uint32_t x[kXxRound][5];
+  uint32_t l[5];
+  uint32_t t0, t1;
+};
+
+__device__ __forceinline__ void xx_issue(const uint8_t* __restrict__ base, uint32_t lane,
+                                         const XBlk& b, uint32_t r, XStep& d) {
   const uint32_t s = lane >> 2;
-  // this lane's 16-byte slot of XXH3-block 0, dword aligned
-  const uint8_t* q = j.p - j.m + 16 * lane;
 #pragma unroll
   for (int k = 0; k < kXxRound; ++k) {
     const uint32_t g = kXxRound * r + k;
-    if (g > j.nb) break;
-    if (g < j.nb || s < j.nbS) {
-      const uint8_t* src = q + 1024ull * g;
-      const u32x4a4 v = ld16_a4(src);
-      d.x[k][0] = v.x;
-      d.x[k][1] = v.y;
-      d.x[k][2] = v.z;
-      d.x[k][3] = v.w;
-      if (j.m) d.x[k][4] = ld4_a4(src + 16);
-    }
+    const bool need = g < b.nb || (g == b.nb && s < b.nbS);
+    const uint64_t o = need ? b.q0 + 1024ull * g + 16 * lane : b.q0;
+    const u32x4a4 v = ld16_a4(base + o);
+    d.x[k][0] = v.x;
+    d.x[k][1] = v.y;
+    d.x[k][2] = v.z;
+    d.x[k][3] = v.w;
+    // the dword after the slot (unaligned starts); it always holds a message
+    // byte when the slot is needed, so it never crosses into an unmapped page
+    d.x[k][4] = ld4_a4(base + o + 16);
   }
-  if (r + 1 == j.R) {  // last stripe: this lane's pair of the 64 bytes at len-64
-    const uint8_t* lq = j.p + j.len - 64 + 16 * (lane & 3) - j.ml;
-    const u32x4a4 v = ld16_a4(lq);
-    d.l[0] = v.x;
-    d.l[1] = v.y;
-    d.l[2] = v.z;
-    d.l[3] = v.w;
-    if (j.ml) d.l[4] = ld4_a4(lq + 16);
-  }
+  const uint8_t* lp = base + b.lq + 16 * (lane & 3);
+  const u32x4a4 v = ld16_a4(lp);
+  d.l[0] = v.x;
+  d.l[1] = v.y;
+  d.l[2] = v.z;
+  d.l[3] = v.w;
+  d.l[4] = ld4_a4(lp + 16);
+  d.t0 = ld4v(base + b.t0);
+  d.t1 = ld4v(base + b.t1);
 }
 
 __device__ __forceinline__ void xx_words(const uint32_t (&x)[5], uint32_t m, uint64_t& d0,
@@ -447,130 +447,156 @@ __device__ __forceinline__ void xx_words(const uint32_t (&x)[5], uint32_t m, uin
   d1 = mk64(x2, x3);
 }
 
-// round r of job j; returns true (and the hash in h) after the last round
-__device__ __forceinline__ bool xx_round(const XxJob& j, uint32_t r, uint32_t lane,
-                                         const HotKeys& K, const XxData& d, uint64_t& acc0,
-                                         uint64_t& acc1, uint64_t& h) {
+// round r of block b (accumulate + scramble per XXH3-block, xxhash.h:5123-5140)
+__device__ __forceinline__ void xx_step_round(const XBlk& b, uint32_t r, uint32_t lane,
+                                              const HotKeys& K, const XStep& d, uint64_t& acc0,
+                                              uint64_t& acc1) {
   const uint32_t s = lane >> 2;
-  const uint64_t* cold = kXxCold[lane & 3];
-  if (r == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
-    acc0 = cold[kColdI0];
-    acc1 = cold[kColdI1];
-  }
-  uint64_t c0[kXxRound], c1[kXxRound];
 #pragma unroll
   for (int k = 0; k < kXxRound; ++k) {
     const uint32_t g = kXxRound * r + k;
-    c0[k] = c1[k] = 0;
-    if (g > j.nb) break;
-    if (g < j.nb || s < j.nbS) {
-      uint64_t d0, d1;
-      xx_words(d.x[k], j.m, d0, d1);
-      c0[k] = mul32to64(d0 ^ K.k0) + d1;  // acc[2p]   (xxhash.h:4926-4927)
-      c1[k] = d0 + mul32to64(d1 ^ K.k1);  // acc[2p+1]
-    }
-  }
-#pragma unroll
-  for (int k = 0; k < kXxRound; ++k) {
-    const uint32_t g = kXxRound * r + k;
-    if (g > j.nb) break;
-    acc0 += stripe_sum(c0[k]);
-    acc1 += stripe_sum(c1[k]);
-    if (g < j.nb) {  // full XXH3-block: scramble (xxhash.h:5126-5128)
+    if (g > b.nb) break;
+    uint64_t d0, d1;
+    xx_words(d.x[k], b.m, d0, d1);
+    uint64_t c0 = mul32to64(d0 ^ K.k0) + d1;  // acc[2p]   (xxhash.h:4926-4927)
+    uint64_t c1 = d0 + mul32to64(d1 ^ K.k1);  // acc[2p+1]
+    if (g == b.nb && s >= b.nbS) c0 = c1 = 0;
+    acc0 += stripe_sum(c0);
+    acc1 += stripe_sum(c1);
+    if (g < b.nb) {  // full XXH3-block: scramble (xxhash.h:5126-5128)
       acc0 = scramble(acc0, K.ks0);
       acc1 = scramble(acc1, K.ks1);
     }
   }
-  if (r + 1 != j.R) return false;
-  {  // last stripe at len-64 (xxhash.h:5146-5151)
-    uint64_t d0, d1;
-    xx_words(d.l, j.ml, d0, d1);
-    acc0 += mul32to64(d0 ^ cold[kColdL0]) + d1;
-    acc1 += d0 + mul32to64(d1 ^ cold[kColdL1]);
-  }
-  uint64_t t = mul128_fold64(acc0 ^ cold[kColdM0], acc1 ^ cold[kColdM1]);  // mergeAccs
-  t += shfl_xor64(t, 1);
-  t += shfl_xor64(t, 2);
-  h = xxh3_avalanche(static_cast<uint64_t>(j.len) * P64_1 + t);
-  return true;
 }
 
 template <int MODE>
-__device__ __forceinline__ void xx_finish(const BlockArgs& a, const XxJob& j, uint32_t lane,
-                                          uint64_t h) {
-  if (lane != 0) return;
-  if (!j.valid) {
-    if (a.out32) a.out32[j.i] = 0;
-    if (MODE == kModeRaw && a.out64) a.out64[j.i] = 0;
-    if (MODE == kModeVerify) {
-      if (a.ok_out) a.ok_out[j.i] = 0;
-      if (a.stored_out) a.stored_out[j.i] = 0;
-      if (a.mismatches) atomicAdd(a.mismatches, 1ull);
-    }
-    return;
-  }
-  if (MODE == kModeRaw) {
-    a.out64[j.i] = h;
-  } else if (MODE == kModeVerify) {
-    const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), j.last);
-    const uint32_t stored = j.stored - j.mod;
-    const bool ok = stored == computed;
-    if (a.out32) a.out32[j.i] = computed;
-    if (a.stored_out) a.stored_out[j.i] = stored;
-    if (a.ok_out) a.ok_out[j.i] = ok ? 1 : 0;
-    if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
-  } else {
-    const uint32_t c = modify_for_last_byte(static_cast<uint32_t>(h), j.last) + j.mod;
-    if (a.out32) a.out32[j.i] = c;
-    if (MODE == kModeTrailer) {
-      uint8_t* w = a.base_w + (j.p - a.base) + j.len;
-      w[0] = static_cast<uint8_t>(j.last);
-      stu32_bytes(w + 1, c);
-    }
-  }
-}
-
-template <int MODE>
-// (kThreads, 4): >= 4 waves per SIMD, i.e. <= 128 VGPRs -- 16 waves per CU
-// keep enough 4 KiB rounds in flight (measured: 152 VGPRs unconstrained).
-__global__ void __launch_bounds__(kThreads, 4) xxh3_block_kernel(BlockArgs a) {
+__global__ void __launch_bounds__(kThreads) xxh3_stream_kernel(BlockArgs a) {
+  __shared__ uint64_t cold[4 * kColdN];
+  if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
+  __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const HotKeys K = hot_keys(lane);
+  const uint64_t* ck = cold + kColdN * (lane & 3);
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  XxJob cur = xx_setup<MODE>(a, static_cast<uint64_t>(blockIdx.x) * kWaves + wave, lane);
-  XxData dA, dB;
-  xx_load(dA, cur, 0, lane);
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  uint64_t kbeg, kend;
+  wave_share(a.n, nw, gw, kbeg, kend);
+  if (kbeg >= kend) return;
+
+  DescBatch cb, nb;
+  uint64_t kb = kbeg;
+  load_batch<MODE>(a, kb, kend, lane, cb);
+  load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
+  uint64_t k = kbeg;
+  XBlk C = xblk_setup<MODE>(a, k, kend, kb, cb, nb);
+  XBlk N = xblk_setup<MODE>(a, k + 1, kend, kb, cb, nb);
+  uint32_t rOut = 0, rHi = 0, rSt = 0, rOk = 0;
+  XStep X, Y;
+  xx_issue(a.base, lane, C, 0, X);
   uint32_t r = 0;
   uint64_t acc0 = 0, acc1 = 0;
-  auto step = [&](XxData& dc, XxData& dn) {
-    const bool same = cur.valid && cur.R > 0 && r + 1 < cur.R;
-    XxJob nxt = cur;
-    if (same) {
-      xx_load(dn, cur, r + 1, lane);
-    } else {
-      nxt = xx_setup<MODE>(a, cur.i + nw, lane);
-      xx_load(dn, nxt, 0, lane);
+
+  auto flush = [&](uint32_t cnt) {
+    const uint64_t i = kb + lane;
+    const bool mine = lane < cnt;
+    if (MODE == kModeRaw) {
+      if (mine && a.out64) a.out64[i] = mk64(rOut, rHi);
+    } else if (mine && a.out32) {
+      a.out32[i] = rOut;
     }
-    if (!cur.valid) {
-      xx_finish<MODE>(a, cur, lane, 0);
-    } else if (cur.R == 0) {
-      xx_finish<MODE>(a, cur, lane, xxh3_short(cur.p, cur.len));
-    } else {
-      uint64_t h = 0;
-      if (xx_round(cur, r, lane, K, dc, acc0, acc1, h)) xx_finish<MODE>(a, cur, lane, h);
+    if (MODE == kModeVerify) {
+      if (mine && a.stored_out) a.stored_out[i] = rSt;
+      if (mine && a.ok_out) a.ok_out[i] = static_cast<uint8_t>(rOk);
+      const uint64_t badm = __ballot(mine && rOk == 0);
+      if (a.mismatches && badm && lane == 0)
+        atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
     }
-    if (same) {
-      ++r;
-    } else {
-      cur = nxt;
-      r = 0;
+    if (MODE == kModeTrailer) {
+      if (mine && rOk) {
+        const uint64_t off = (static_cast<uint64_t>(cb.off_hi) << 32) | cb.off_lo;
+        uint8_t* p = a.base_w + off + cb.size;
+        if (a.last_bytes) p[0] = static_cast<uint8_t>(cb.extra);
+        stu32_bytes(p + 1, rOut);
+      }
     }
   };
-  while (cur.i < a.n) {
-    step(dA, dB);
-    if (cur.i >= a.n) break;
-    step(dB, dA);
+
+  auto step = [&](XStep& cu, XStep& nx) -> bool {
+    const bool last = C.slow || r + 1 >= C.R;
+    if (last)
+      xx_issue(a.base, lane, N, 0, nx);
+    else
+      xx_issue(a.base, lane, C, r + 1, nx);
+    uint64_t h = 0;
+    if (!C.slow) {
+      if (r == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
+        acc0 = ck[kColdI0];
+        acc1 = ck[kColdI1];
+      }
+      xx_step_round(C, r, lane, K, cu, acc0, acc1);
+      if (!last) {
+        ++r;
+        return true;
+      }
+      uint64_t d0, d1;  // last stripe at len-64 (xxhash.h:5146-5151)
+      xx_words(cu.l, C.ml, d0, d1);
+      acc0 += mul32to64(d0 ^ ck[kColdL0]) + d1;
+      acc1 += d0 + mul32to64(d1 ^ ck[kColdL1]);
+      uint64_t t = mul128_fold64(acc0 ^ ck[kColdM0], acc1 ^ ck[kColdM1]);  // mergeAccs
+      t += shfl_xor64(t, 1);
+      t += shfl_xor64(t, 2);
+      h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + t);
+    }
+    uint32_t lastb = 0, stored = 0;
+    if (!C.slow) {
+      lastb = (cu.t0 >> (8 * C.tb)) & 0xffu;
+      if (MODE == kModeVerify)
+        stored = C.tb == 3 ? cu.t1 : __builtin_amdgcn_alignbyte(cu.t1, cu.t0, C.tb + 1);
+    } else if (C.valid) {
+      // short input: the length-class formulas, with their own loads; retire()
+      // keeps those loads from merging into the hot path (see crc32c.hip)
+      const uint8_t* p = a.base + C.off;
+      const uint64_t hs = xxh3_short(p, C.size);
+      h = mk64(retire(static_cast<uint32_t>(hs)), retire(static_cast<uint32_t>(hs >> 32)));
+      if (MODE != kModeRaw) lastb = retire(ldu8(p + C.size));
+      if (MODE == kModeVerify) stored = retire(ldu32(p + C.size + 1));
+    }
+    if ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) lastb = C.extra;
+    uint32_t out, hi = 0, st = 0, ok = C.valid ? 1u : 0u;
+    if (MODE == kModeRaw) {
+      out = static_cast<uint32_t>(h);
+      hi = static_cast<uint32_t>(h >> 32);
+    } else if (MODE == kModeVerify) {
+      // ComputeBuiltinChecksum(kXXH3, data, size+1), format.cc:577-586
+      const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), lastb);
+      st = stored - C.mod;
+      ok = (C.valid && st == computed) ? 1u : 0u;
+      out = computed;
+    } else {
+      out = modify_for_last_byte(static_cast<uint32_t>(h), lastb) + C.mod;
+    }
+    if (!C.valid) out = hi = st = 0;
+    const uint32_t kk = static_cast<uint32_t>(k - kb);
+    rOut = lane == kk ? out : rOut;
+    rHi = lane == kk ? hi : rHi;
+    rSt = lane == kk ? st : rSt;
+    rOk = lane == kk ? ok : rOk;
+    ++k;
+    if (k - kb == kBatch || k == kend) {
+      flush(static_cast<uint32_t>(k - kb));
+      if (k == kend) return false;
+      kb = k;
+      cb = nb;
+      load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
+    }
+    C = N;
+    N = xblk_setup<MODE>(a, k + 1, kend, kb, cb, nb);
+    r = 0;
+    return true;
+  };
+  while (step(X, Y) && step(Y, X)) {
   }
 }
 
@@ -663,6 +689,22 @@ __global__ void __launch_bounds__(kThreads) noop_block_kernel(BlockArgs a) {
   }
 }
 
+// resident workgroups per CU of the stream kernel: its grid is exactly what
+// fits at once, so every wave's contiguous share runs concurrently (no tail
+// of late workgroups)
+template <int MODE>
+uint32_t stream_occupancy() {
+  static const uint32_t occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_stream_kernel<MODE>, kThreads,
+                                                     0) != hipSuccess ||
+        o < 1)
+      o = 1;
+    return static_cast<uint32_t>(o);
+  }();
+  return occ;
+}
+
 }  // namespace
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
@@ -672,9 +714,10 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   const uint64_t want = (a.n + kWaves - 1) / kWaves;
   const uint32_t grid = static_cast<uint32_t>(
       std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
-  // FORST_XXH3_VARIANT=simple selects the unpipelined kernel (A/B reference)
+  // FORST_XXH3_VARIANT=simple selects the per-block kernel (A/B reference);
+  // it also serves buffers too small for the stream kernel's dummy loads.
   const char* variant = std::getenv("FORST_XXH3_VARIANT");
-  const bool simple = variant && std::string(variant) == "simple";
+  const bool simple = (variant && std::string(variant) == "simple") || a.base_len < 4096;
 #define FORST_LAUNCH_XXH3(M, TAG)                                                          \
   do {                                                                                     \
     if (simple) {                                                                          \
@@ -682,8 +725,10 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
       hipLaunchKernelGGL(xxh3_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,       \
                          stream, a);                                                       \
     } else {                                                                               \
-      *name = "xxh3_block_kernel<" TAG ">";                                                \
-      hipLaunchKernelGGL(xxh3_block_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, a);  \
+      *name = "xxh3_stream_kernel<" TAG ">";                                               \
+      const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
+          1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));     \
+      hipLaunchKernelGGL(xxh3_stream_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, a);   \
     }                                                                                      \
   } while (0)
   switch (mode) {

@@ -116,11 +116,16 @@ inline uint32_t __shfl_xor(uint32_t v, int mask) {
 inline uint32_t __shfl(uint32_t v, int src) {
   return emu::exchange(v, static_cast<uint32_t>(src));
 }
-inline uint32_t __builtin_amdgcn_readfirstlane(uint32_t v) { return emu::exchange(v, 0); }
+// the real builtins return int (sign-extends when widened): mirror that
+inline int __builtin_amdgcn_readfirstlane(int v) {
+  return static_cast<int>(emu::exchange(static_cast<uint32_t>(v), 0));
+}
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8 * (s & 3)));
 }
-inline uint32_t __builtin_amdgcn_readlane(uint32_t v, uint32_t l) { return emu::exchange(v, l); }
+inline int __builtin_amdgcn_readlane(int v, int l) {
+  return static_cast<int>(emu::exchange(static_cast<uint32_t>(v), static_cast<uint32_t>(l)));
+}
 inline unsigned long long __ballot(int pred) {
   emu::Wave& w = emu::tl_group->waves[emu::tl_tid.x >> 6];
   const uint32_t lane = emu::tl_tid.x & 63;
@@ -172,3 +177,8 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 }
 
 #define hipLaunchKernelGGL(K, G, B, SH, ST, ...) ::emu::launch(K, G, B, __VA_ARGS__)
+template <typename K>
+inline hipError_t hipOccupancyMaxActiveBlocksPerMultiprocessor(int* n, K, int, size_t) {
+  *n = 2;
+  return hipSuccess;
+}

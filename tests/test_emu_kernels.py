@@ -122,10 +122,41 @@ def test_emu_crc_stream_batches_and_edges():
     for k in range(0, n, 37):
         o, s = int(offs[k]), int(sizes[k])
         assert int(got[k]) == O.crc32c_extend(int(init[k]), base[o:o + s]), (k, s, o & 3)
+    # the XXH3 stream kernel on the same layout (short and long inputs)
+    want = O.block_checksum_batch(4, base, offs, sizes, last_bytes=types, modifiers=mods)
+    assert (emu.block_checksum(4, base, offs, sizes, last=types, mods=mods) == want).all()
+    want = O.block_checksum_batch(4, base, offs, sizes, modifiers=mods)
+    assert (emu.block_checksum(4, base, offs, sizes, mods=mods) == want).all()
+    b2, out = emu.block_trailer(4, base, offs, sizes, types, mods)
+    b2[int(offs[41]) + 1000] ^= 0x01
+    comp, st, ok, bad = emu.block_verify(4, b2, offs, sizes, mods)
+    assert bad == 1 and not ok[41] and ok.sum() == n - 1
+    got = emu.xxh3(base, offs, sizes)
+    for k in range(0, n, 41):
+        o, s = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.xxh3_64(base[o:o + s]), (k, s)
     # messages at the very start of the buffer (round-0 head would underflow)
     offs2 = np.array([0, 1, 2, 3, 70, 4100], np.uint64)
     sizes2 = np.array([5000, 4999, 64, 4093, 100, 9000], np.uint32)
     got = emu.crc32c(base, offs2, sizes2)
     for k in range(len(offs2)):
         o, s = int(offs2[k]), int(sizes2[k])
+        assert int(got[k]) == O.crc32c_extend(0, base[o:o + s]), k
+
+
+def test_emu_offsets_above_2gib():
+    """64-bit descriptor offsets (bit 31 set): readlane results must not be
+    sign-extended when the offset is rebuilt (a GPU-only failure mode at the
+    full C2 size, 1 M x 4 KiB = 4.3 GB)."""
+    big = (1 << 31) + 3 * 65536
+    base = np.zeros(big, dtype=np.uint8)  # lazily zero pages
+    rng = np.random.default_rng(5)
+    tail0 = (1 << 31) - 65536
+    base[tail0:] = rng.integers(0, 256, big - tail0, dtype=np.uint8)
+    offs = np.array([tail0 + 3, (1 << 31) + 1, (1 << 31) + 70001, (1 << 31) - 9000],
+                    np.uint64)
+    sizes = np.array([60000, 4096, 5000, 8999], np.uint32)
+    got = emu.crc32c(base, offs, sizes)
+    for k in range(len(offs)):
+        o, s = int(offs[k]), int(sizes[k])
         assert int(got[k]) == O.crc32c_extend(0, base[o:o + s]), k

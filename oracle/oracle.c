@@ -579,6 +579,166 @@ uint64_t oracle_xxh64(const void* p, size_t len, uint64_t seed) {
 }
 
 /* ======================================================================== */
+/* XXPH3 (xxHash 0.7.2 preview, util/xxph3.h) -- Hash64 / NPHash64          */
+/* (util/hash.cc:81-88, util/hash.h:45-62), the per-KV protection hash of    */
+/* db/kv_checksum.h.  Same default secret as XXH3 0.8.1 (xxph3.h:920).       */
+/* ======================================================================== */
+
+/* xxph3.h:1069 XXPH3_avalanche (PRIME64_3, unlike 0.8.1's PRIME_MX1) */
+static inline uint64_t xxph3_avalanche(uint64_t h) {
+  h ^= h >> 37;
+  h *= P64_3;
+  h ^= h >> 32;
+  return h;
+}
+
+/* xxph3.h:1082-1140 XXPH3_len_{1to3,4to8,9to16}_64b + RocksDB's empty rule */
+static uint64_t xxph3_len_0to16(const uint8_t* in, size_t len, uint64_t seed) {
+  const uint8_t* s = kSecret;
+  if (len > 8) {
+    const uint64_t lo = ld64(in) ^ (ld64(s) + seed);
+    const uint64_t hi = ld64(in + len - 8) ^ (ld64(s + 8) - seed);
+    return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+  }
+  if (len >= 4) {
+    const uint64_t in64 = (uint64_t)ld32(in) | ((uint64_t)ld32(in + len - 4) << 32);
+    const uint64_t keyed = in64 ^ (ld64(s) + seed);
+    const uint64_t mix64 = len + ((keyed ^ (keyed >> 51)) * P32_1);
+    return xxph3_avalanche((mix64 ^ (mix64 >> 47)) * P64_2);
+  }
+  if (len) {
+    const uint32_t combined = (uint32_t)in[0] | ((uint32_t)in[len >> 1] << 8) |
+                              ((uint32_t)in[len - 1] << 16) | ((uint32_t)len << 24);
+    const uint64_t keyed = (uint64_t)combined ^ ((uint64_t)ld32(s) + seed);
+    return xxph3_avalanche(keyed * P64_1);
+  }
+  return mul128_fold64(seed + ld64(s), P64_2); /* xxph3.h:1133-1138 */
+}
+
+/* xxph3.h:1640 XXPH3_mix16B */
+static inline uint64_t xxph3_mix16B(const uint8_t* in, const uint8_t* s, uint64_t seed) {
+  return mul128_fold64(ld64(in) ^ (ld64(s) + seed), ld64(in + 8) ^ (ld64(s + 8) - seed));
+}
+
+/* xxph3.h:1651 XXPH3_len_17to128_64b */
+static uint64_t xxph3_len_17to128(const uint8_t* in, size_t len, uint64_t seed) {
+  const uint8_t* s = kSecret;
+  uint64_t acc = len * P64_1;
+  if (len > 32) {
+    if (len > 64) {
+      if (len > 96) {
+        acc += xxph3_mix16B(in + 48, s + 96, seed);
+        acc += xxph3_mix16B(in + len - 64, s + 112, seed);
+      }
+      acc += xxph3_mix16B(in + 32, s + 64, seed);
+      acc += xxph3_mix16B(in + len - 48, s + 80, seed);
+    }
+    acc += xxph3_mix16B(in + 16, s + 32, seed);
+    acc += xxph3_mix16B(in + len - 32, s + 48, seed);
+  }
+  acc += xxph3_mix16B(in, s, seed);
+  acc += xxph3_mix16B(in + len - 16, s + 16, seed);
+  return xxph3_avalanche(acc);
+}
+
+/* xxph3.h:1681 XXPH3_len_129to240_64b */
+static uint64_t xxph3_len_129to240(const uint8_t* in, size_t len, uint64_t seed) {
+  const uint8_t* s = kSecret;
+  uint64_t acc = len * P64_1;
+  const int nb_rounds = (int)len / 16;
+  for (int i = 0; i < 8; i++) acc += xxph3_mix16B(in + 16 * i, s + 16 * i, seed);
+  acc = xxph3_avalanche(acc);
+  for (int i = 8; i < nb_rounds; i++) acc += xxph3_mix16B(in + 16 * i, s + 16 * (i - 8) + 3, seed);
+  acc += xxph3_mix16B(in + len - 16, s + 136 - 17, seed);
+  return xxph3_avalanche(acc);
+}
+
+/* xxph3.h:1322-1339 XXPH3_accumulate_512, XXPH3_acc_64bits (no lane swap) */
+static inline void xxph3_acc512(uint64_t* acc, const uint8_t* in, const uint8_t* s) {
+  for (int i = 0; i < 8; i++) {
+    const uint64_t d = ld64(in + 8 * i);
+    const uint64_t dk = d ^ ld64(s + 8 * i);
+    acc[i] += d;
+    acc[i] += (dk & 0xFFFFFFFFull) * (dk >> 32);
+  }
+}
+
+/* xxph3.h:1514-1583 hashLong: 16 stripes per 1 KiB block (nb_blocks =
+ * len / 1024, NOT (len-1)/1024), scramble after each full block, last stripe
+ * only if len % 64 != 0, merge from secret+11 with start len*PRIME64_1.
+ * The seeded secret is kSecret with +seed / -seed on alternating 8-byte words
+ * (xxph3.h:1609-1620). */
+static uint64_t xxph3_hashlong(const uint8_t* in, size_t len, uint64_t seed) {
+  uint8_t sec[192];
+  for (int i = 0; i < 12; i++) {
+    const uint64_t a = ld64(kSecret + 16 * i) + seed;
+    const uint64_t b = ld64(kSecret + 16 * i + 8) - seed;
+    memcpy(sec + 16 * i, &a, 8);
+    memcpy(sec + 16 * i + 8, &b, 8);
+  }
+  uint64_t acc[8] = {P32_3, P64_1, P64_2, P64_3, P64_4, P32_2, P64_5, P32_1};
+  const size_t nb_blocks = len / 1024;
+  for (size_t n = 0; n < nb_blocks; n++) {
+    for (int st = 0; st < 16; st++) xxph3_acc512(acc, in + 1024 * n + 64 * st, sec + 8 * st);
+    for (int i = 0; i < 8; i++) { /* xxph3.h:1464-1477 scramble */
+      uint64_t a = acc[i];
+      a ^= a >> 47;
+      a ^= ld64(sec + 128 + 8 * i);
+      acc[i] = a * P32_1;
+    }
+  }
+  const size_t nb_stripes = (len - 1024 * nb_blocks) / 64;
+  for (size_t st = 0; st < nb_stripes; st++)
+    xxph3_acc512(acc, in + 1024 * nb_blocks + 64 * st, sec + 8 * st);
+  if (len & 63) xxph3_acc512(acc, in + len - 64, sec + 192 - 64 - 7);
+  uint64_t r = len * P64_1;
+  for (int i = 0; i < 4; i++)
+    r += mul128_fold64(acc[2 * i] ^ ld64(sec + 11 + 16 * i),
+                       acc[2 * i + 1] ^ ld64(sec + 11 + 16 * i + 8));
+  return xxph3_avalanche(r);
+}
+
+/* xxph3.h:1733 XXPH3_64bits_withSeed == util/hash.cc:81 Hash64(data, n, seed) */
+uint64_t oracle_hash64(const void* p, size_t n, uint64_t seed) {
+  const uint8_t* in = (const uint8_t*)p;
+  if (n <= 16) return xxph3_len_0to16(in, n, seed);
+  if (n <= 128) return xxph3_len_17to128(in, n, seed);
+  if (n <= 240) return xxph3_len_129to240(in, n, seed);
+  return xxph3_hashlong(in, n, seed);
+}
+
+/* db/kv_checksum.h:84-88 field seeds */
+#define KV_SEED_K 0ull
+#define KV_SEED_V 0xD28AAD72F49BD50Bull
+#define KV_SEED_O 0xA5155AE5E937AA16ull
+#define KV_SEED_S 0x77A00858DDD37F21ull
+#define KV_SEED_C 0x4A2AB5CBD26F542Cull
+
+/* ProtectionInfo64().ProtectKV / ProtectKVO [.ProtectS] [.ProtectC]
+ * (db/kv_checksum.h:296-332, :420-460): XOR of NPHash64 of each field with its
+ * seed; op/seq/cf are hashed as their native (little-endian) bytes. */
+uint64_t oracle_kv_protect(const void* key, size_t klen, const void* value, size_t vlen,
+                           int op_type, int has_seq, uint64_t seq, int has_cf, uint32_t cf) {
+  uint64_t v = oracle_hash64(key, klen, KV_SEED_K) ^ oracle_hash64(value, vlen, KV_SEED_V);
+  if (op_type >= 0) {
+    const uint8_t op = (uint8_t)op_type;
+    v ^= oracle_hash64(&op, 1, KV_SEED_O);
+  }
+  if (has_seq) v ^= oracle_hash64(&seq, 8, KV_SEED_S);
+  if (has_cf) v ^= oracle_hash64(&cf, 4, KV_SEED_C);
+  return v;
+}
+
+/* ProtectionInfo<T>::Verify (kv_checksum.h:117-133): the low `len` bytes of
+ * the protection value against the LE bytes at `stored`. */
+int oracle_kv_verify(uint64_t prot, uint32_t len, const void* stored) {
+  uint64_t s = 0;
+  memcpy(&s, stored, len);
+  const uint64_t mask = len >= 8 ? ~0ull : ((1ull << (8 * len)) - 1);
+  return ((s ^ prot) & mask) == 0;
+}
+
+/* ======================================================================== */
 /* Block checksum dispatcher (table/format.cc, table/format.h)               */
 /* ======================================================================== */
 

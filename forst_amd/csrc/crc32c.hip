@@ -517,6 +517,484 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(BlockArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Streaming block kernel v2: two independent CRC chains per lane.
+//
+// The latency of the v1 kernel is a serial chain of 17 dependent LDS table
+// steps per 4 KiB round (16 dwords + the hop) plus a 6-step combine tree per
+// block.  v2 halves the chain: in every 4 KiB round, chain c (0, 1) of lane l
+// owns the 32-byte segment [2048c + 32l, +32) -- 8 dwords -- so a lane runs
+// two independent 8-step chains whose LDS latencies overlap.  The hop to the
+// next round is fused with the first dword step (s' = J2(s) ^ G(w0), J2 = shift
+// by 4096 - 32 + 4 bytes).  The finish is three table steps deep instead of a
+// tree: every lane moves each chain state to the end of its 16-lane row with
+// A[lo] (lo = 15 - (l & 15)), the rows are XOR-reduced with DPP (no tables),
+// and the 8 row values (2 chains x 4 rows) are moved to the end of the round
+// with B[hi] and XORed.  The <= 3 tail bytes and the block's type byte are
+// folded in ONE slicing step of k <= 4 bytes.
+//
+// LDS (byte addresses; the only __shared__ object, at 0):
+//   [0, 64K)       G and J2, replicated 8x and interleaved: row e (256 B) holds
+//                  G_t[e] copy c at dword 8t + c and J2_t[e] copy c at dword
+//                  32 + 8t + c (t = 0..3 table, c = 0..7 copy).  Lane l
+//                  (c = l & 7, g = (l >> 3) & 3) does the i-th lookup of a
+//                  step on table i ^ g with byte i ^ g, so the 32 lanes of a
+//                  ds_read_b32 bank group hit dwords 8{0,1,2,3} + c: 32
+//                  distinct banks, conflict free.  The address
+//                  256 * byte + 4 (8 t + c) [+ 128 for J2] is ONE v_perm_b32 of
+//                  the data word and a per-lane constant.
+//   [64K, 124K)    A[1..15]: shift by 32 lo bytes (unreplicated, 4 KiB each)
+//   [124K, 152K)   B[1..7]: shift by 512 hi bytes
+// ---------------------------------------------------------------------------
+constexpr uint32_t kOffA2 = 65536;
+constexpr uint32_t kOffB2 = kOffA2 + 15 * 4096;
+constexpr uint32_t kLds2Bytes = kOffB2 + 7 * 4096;
+static_assert(kLds2Bytes <= 160 * 1024, "v2 tables must fit in LDS");
+constexpr uint32_t kRB2 = FORST_CRC_ROUND_BYTES;
+constexpr uint32_t kSeg2 = FORST_CRC2_SEG_BYTES;       // 32
+constexpr uint32_t kChain2 = FORST_CRC2_CHAIN_BYTES;   // 2048
+static_assert(kSeg2 * 16 * 8 == 2 * kChain2, "A/B tables assume 32-byte segments, 2 chains");
+
+__device__ __forceinline__ uint32_t lds32(const uint8_t* __restrict__ Lb, uint32_t addr) {
+  return *reinterpret_cast<const uint32_t*>(Lb + addr);
+}
+
+struct Lanes2 {
+  uint32_t lreg[4];   // 4 (8 (i^g) + c)  (G; J2 is +128, folded into the ds_read offset)
+  uint32_t sel[4];    // v_perm selector: addr = {0, 0, x.b(i^g), S1.b0}
+};
+
+__device__ __forceinline__ Lanes2 lanes2(uint32_t lane) {
+  Lanes2 k;
+  const uint32_t c = lane & 7, g = (lane >> 3) & 3;
+#pragma unroll
+  for (uint32_t i = 0; i < 4; ++i) {
+    const uint32_t tt = i ^ g;
+    k.lreg[i] = 4 * (8 * tt + c);
+    k.sel[i] = 0x0c0c0000u | ((4 + tt) << 8);
+  }
+  return k;
+}
+__device__ __forceinline__ uint32_t lane_c4(uint32_t lane) { return (lane & 7) << 2; }
+
+// replicated 4-table linear map: G (J = false) or J2 (J = true)
+template <bool J>
+__device__ __forceinline__ uint32_t rep_map(const uint8_t* __restrict__ Lb, const Lanes2& k,
+                                            uint32_t x) {
+  uint32_t r = 0;
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    r ^= lds32(Lb, __builtin_amdgcn_perm(x, k.lreg[i], k.sel[i]) + (J ? 128u : 0u));
+  return r;
+}
+
+// k-byte slicing step (k <= 4, wave-uniform): the state after bytes y_0..y_k-1
+// (little-endian in y):  (s >> 8k) ^ XOR_j G[4-k+j][(s ^ y)_j]
+__device__ __forceinline__ uint32_t step_k(const uint8_t* __restrict__ Lb, const Lanes2& kk,
+                                           uint32_t s, uint32_t y, uint32_t k) {
+  if (k == 0) return s;
+  const uint32_t x = s ^ y;
+  const uint32_t c4 = lane_c4(threadIdx.x);
+  uint32_t r = k == 4 ? 0u : (s >> (8 * k));
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j) {
+    if (j < k) {
+      const uint32_t t = 4 - k + j;
+      r ^= lds32(Lb, __builtin_amdgcn_perm(x, c4, 0x0c0c0000u | ((4 + j) << 8)) + 32 * t);
+    }
+  }
+  return r;
+}
+
+// linear shift through an unreplicated 4 x 256 table at byte offset b
+__device__ __forceinline__ uint32_t shift_at(const uint8_t* __restrict__ Lb, uint32_t b,
+                                             uint32_t v) {
+  return lds32(Lb, b + ((v & 0xffu) << 2)) ^ lds32(Lb, b + 1024 + (((v >> 8) & 0xffu) << 2)) ^
+         lds32(Lb, b + 2048 + (((v >> 16) & 0xffu) << 2)) ^ lds32(Lb, b + 3072 + ((v >> 24) << 2));
+}
+
+__device__ __forceinline__ void fill_tables2(uint32_t* L) {
+  const uint32_t tid = threadIdx.x;
+  // row e, dword d: d < 32 -> G_{d>>3}[e], else J2_{(d-32)>>3}[e]
+  for (uint32_t i = tid; i < 16384; i += kThreads) {
+    const uint32_t e = i >> 6, d = i & 63, t = (d >> 3) & 3;
+    L[i] = d < 32 ? kCrcG[t * 256 + e] : kCrcJ2[t * 256 + e];
+  }
+  for (uint32_t i = tid; i < 15 * 1024; i += kThreads) L[kOffA2 / 4 + i] = kCrcA[i];
+  for (uint32_t i = tid; i < 7 * 1024; i += kThreads) L[kOffB2 / 4 + i] = kCrcB[i];
+  __syncthreads();
+}
+
+// raw mode with a per-message init: S0 = ~init moved back over m bytes
+__device__ __forceinline__ uint32_t unstep_m(uint32_t v, uint32_t m) {
+  if (m == 0) return v;
+  const uint32_t* col = kCrcUnstep + 32 * (m - 1);
+  uint32_t r = 0;
+  for (uint32_t i = 0; i < 32; ++i) r ^= ((v >> i) & 1u) ? col[i] : 0u;
+  return r;
+}
+
+// wave-uniform description of one block, kept compact (three live copies
+// sit in SGPRs): derived quantities are recomputed where they are used
+struct Blk2 {
+  uint64_t off;
+  uint64_t we;  // window end: last dword boundary <= message end
+  uint32_t size, mod, extra, R, S0;
+  uint32_t pk;  // cA:1 | lA:6 | jA:3 | q:3 | nt:2 | valid:1 | slow:1 | m:2
+  __device__ __forceinline__ uint32_t cA() const { return pk & 1u; }
+  __device__ __forceinline__ uint32_t lA() const { return (pk >> 1) & 63u; }
+  __device__ __forceinline__ uint32_t jA() const { return (pk >> 7) & 7u; }
+  __device__ __forceinline__ uint32_t q() const { return (pk >> 10) & 7u; }
+  __device__ __forceinline__ uint32_t nt() const { return (pk >> 13) & 3u; }
+  __device__ __forceinline__ bool valid() const { return (pk >> 15) & 1u; }
+  __device__ __forceinline__ bool slow() const { return (pk >> 16) & 1u; }
+  __device__ __forceinline__ uint32_t bm() const { return 0xffffffffu << (8 * (pk >> 17)); }
+  // round-0 window start (may be < 0)
+  __device__ __forceinline__ int64_t w0() const {
+    return static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRB2;
+  }
+};
+
+template <int MODE>
+__device__ __forceinline__ bool mem_last_byte(const BlockArgs& a) {
+  return MODE == kModeVerify || ((MODE == kModeCompute || MODE == kModeTrailer) && !a.last_bytes);
+}
+
+template <int MODE>
+__device__ __forceinline__ Blk2 blk2_setup(const BlockArgs& a, uint64_t k, uint64_t kend,
+                                           uint64_t kb, const DescBatch& cb,
+                                           const DescBatch& nb) {
+  Blk2 b;
+  const Desc d = batch_desc(k, kb, cb, nb);
+  b.off = d.off;
+  b.size = d.size;
+  b.mod = d.mod;
+  b.extra = d.extra;
+  const bool valid = k < kend && desc_in_range<MODE>(a, d);
+  const uint64_t E = b.off + b.size + (mem_last_byte<MODE>(a) ? 1u : 0u);
+  const uint64_t ws = b.off & ~3ull;
+  b.we = E & ~3ull;
+  const uint64_t d4 = b.we - ws;
+  b.R = static_cast<uint32_t>((d4 + kRB2 - 1) / kRB2);
+  const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - b.w0());
+  const uint32_t cA = hA >> 11, lA = (hA >> 5) & 63u, jA = (hA >> 2) & 7u;
+  // head segment starting in front of the buffer (only blocks at offset < 28):
+  // it is loaded from offset 0 and shifted up by q dwords in registers
+  const int64_t seg_head = static_cast<int64_t>(ws) - 4 * static_cast<int64_t>(jA);
+  const uint32_t q = seg_head < 0 ? static_cast<uint32_t>(-seg_head) >> 2 : 0u;
+  const uint32_t nt = static_cast<uint32_t>(E - b.we);
+  const uint32_t m = static_cast<uint32_t>(b.off & 3);
+  const bool slow = !valid || d4 < 64;
+  b.S0 = MODE == kModeRaw ? unstep_m(~b.extra, m) : kCrcS0[m];
+  if (slow) {  // the slow path loads on its own; dummy step loads at [0, 4 KiB)
+    b.we = kRB2;
+    b.R = 1;
+    b.pk = (nt << 13) | (valid ? 1u << 15 : 0u) | (1u << 16) | (m << 17);
+  } else {
+    b.pk = cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
+           (m << 17);
+  }
+  return b;
+}
+
+struct StepBuf2 {
+  uint32_t w[2][8];
+  uint32_t t0, t1;
+};
+
+template <int MODE>
+__device__ __forceinline__ void issue_step2(const uint8_t* __restrict__ base, uint32_t lane,
+                                            const Blk2& b, uint32_t r, StepBuf2& buf) {
+  const int64_t w0 = b.w0();
+  const uint32_t cA = b.cA(), lA = b.lA();
+#pragma unroll
+  for (uint32_t c = 0; c < 2; ++c) {
+    int64_t so = w0 + static_cast<int64_t>(r) * kRB2 + kChain2 * c + kSeg2 * lane;
+    if (r == 0) {
+      // segments wholly in front of the head: any safe in-message address
+      const bool pre = c < cA || (c == cA && lane < lA);
+      so = pre ? static_cast<int64_t>(b.we) - kSeg2 : so;
+      so = so < 0 ? 0 : so;
+    }
+    const uint8_t* sp = base + so;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const u32x4a4 v = ld16_a4(sp + 16 * q);
+      buf.w[c][4 * q + 0] = v.x;
+      buf.w[c][4 * q + 1] = v.y;
+      buf.w[c][4 * q + 2] = v.z;
+      buf.w[c][4 * q + 3] = v.w;
+    }
+  }
+  // tail dword at we (holds the <= 3 tail bytes; in verify mode the stored
+  // checksum starts inside it or is the next dword); slow blocks: offset 0
+  const uint32_t nt = b.nt();
+  const uint64_t t0 = b.slow() ? 0 : (nt > 0 || MODE == kModeVerify) ? b.we : b.we - 4;
+  buf.t0 = ld4v(base + t0);
+  buf.t1 = MODE == kModeVerify ? ld4v(base + (b.slow() || nt == 0 ? t0 : t0 + 4)) : 0u;
+}
+
+// one round of both chains
+__device__ __forceinline__ void stream_round2(const uint8_t* __restrict__ Lb, const Lanes2& K,
+                                              uint32_t lane, const Blk2& b, uint32_t r,
+                                              uint32_t (&s)[2], const uint32_t (&w)[2][8]) {
+  if (r == 0) {
+    const uint32_t cA = b.cA(), lA = b.lA(), jA = b.jA(), q = b.q();
+    const uint32_t bm = b.bm();
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c) {
+      uint32_t wc[8];
+#pragma unroll
+      for (int j = 0; j < 8; ++j) wc[j] = w[c][j];
+      if (q != 0 && c == cA) {  // head segment loaded from offset 0: shift up q dwords
+        uint32_t sh[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) {
+          uint32_t v = 0;
+#pragma unroll
+          for (int qq = 1; qq < 8; ++qq)
+            if (qq <= j) v = (q == static_cast<uint32_t>(qq)) ? wc[j - qq] : v;
+          sh[j] = v;
+        }
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wc[j] = lane == lA ? sh[j] : wc[j];
+      }
+      uint32_t sc = 0;
+#pragma unroll
+      for (uint32_t j = 0; j < 8; ++j) {
+        uint32_t x = sc ^ wc[j];
+        if (c == cA && j == jA) {
+          const uint32_t head = (wc[j] & bm) ^ b.S0;
+          x = lane == lA ? head : x;
+        }
+        sc = rep_map<false>(Lb, K, x);
+      }
+      const bool pre = c < cA || (c == cA && lane < lA);
+      s[c] = pre ? 0u : sc;
+    }
+  } else {
+    uint32_t s0 = rep_map<true>(Lb, K, s[0]) ^ rep_map<false>(Lb, K, w[0][0]);
+    uint32_t s1 = rep_map<true>(Lb, K, s[1]) ^ rep_map<false>(Lb, K, w[1][0]);
+#pragma unroll
+    for (int j = 1; j < 8; ++j) {
+      s0 = rep_map<false>(Lb, K, s0 ^ w[0][j]);
+      s1 = rep_map<false>(Lb, K, s1 ^ w[1][j]);
+    }
+    s[0] = s0;
+    s[1] = s1;
+  }
+}
+
+// XOR of the 16 lanes of each row, valid in the row's last lane (DPP row_shr)
+template <int N>
+__device__ __forceinline__ uint32_t row_shr_xor(uint32_t v) {
+  return v ^ static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x110 + N,
+                                                               0xf, 0xf, false));
+}
+
+// join the 2 x 64 chain states, fold in the tail bytes and the extra byte;
+// returns ~state (the crc32c::Extend value), wave-uniform
+__device__ __forceinline__ uint32_t stream_finish2(const uint8_t* __restrict__ Lb,
+                                                   const Lanes2& K, uint32_t lane, const Blk2& b,
+                                                   const uint32_t (&s)[2], uint32_t t0,
+                                                   bool has_extra) {
+  // chain c of lane l ends 2048 (1 - c) + 32 (63 - l) bytes before the round end
+  const bool lo0 = (lane & 15) == 15;
+  const uint32_t abase = kOffA2 + 4096 * (14 - (lane & 15));  // A[lo], lo = 15 - (lane & 15)
+  uint32_t a0 = lo0 ? s[0] : shift_at(Lb, abase, s[0]);
+  uint32_t a1 = lo0 ? s[1] : shift_at(Lb, abase, s[1]);
+  a0 = row_shr_xor<1>(a0);
+  a1 = row_shr_xor<1>(a1);
+  a0 = row_shr_xor<2>(a0);
+  a1 = row_shr_xor<2>(a1);
+  a0 = row_shr_xor<4>(a0);
+  a1 = row_shr_xor<4>(a1);
+  a0 = row_shr_xor<8>(a0);
+  a1 = row_shr_xor<8>(a1);
+  // lane 16 rho + 15: chain 0 row value needs B[7 - rho], chain 1 B[3 - rho]
+  uint32_t v = 0;
+  if (lo0) {
+    const uint32_t rho = lane >> 4;
+    const uint32_t v0 = shift_at(Lb, kOffB2 + 4096 * (6 - rho), a0);
+    const uint32_t v1 = rho == 3 ? a1 : shift_at(Lb, kOffB2 + 4096 * (2 - rho), a1);
+    v = v0 ^ v1;
+  }
+  const uint32_t st = readlane32(v, 15) ^ readlane32(v, 31) ^ readlane32(v, 47) ^
+                      readlane32(v, 63);
+  const uint32_t nt = b.nt();
+  uint32_t y = nt ? (t0 & (0xffffffffu >> (32 - 8 * nt))) : 0u;
+  uint32_t k = nt;
+  if (has_extra) {
+    y |= (b.extra & 0xffu) << (8 * k);
+    ++k;
+  }
+  return ~step_k(Lb, K, st, y, k);
+}
+
+// short messages (< 64 bytes past the head dword): dword-serial, wave-uniform
+__device__ __forceinline__ uint32_t small_crc2(const uint8_t* __restrict__ Lb, const Lanes2& K,
+                                               const uint8_t* p, uint32_t len, uint32_t init,
+                                               uint32_t nextra, uint32_t extra) {
+  uint32_t s = ~init;
+  const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3);
+  uint32_t nh = (4 - m) & 3;
+  nh = nh < len ? nh : len;
+  uint32_t y = 0;
+  for (uint32_t i = 0; i < nh; ++i) y |= ldu8(p + i) << (8 * i);
+  s = step_k(Lb, K, s, y, nh);
+  uint32_t i = nh;
+  for (; i + 4 <= len; i += 4) s = rep_map<false>(Lb, K, s ^ ld4v(p + i));
+  y = 0;
+  const uint32_t nt = len - i;
+  for (uint32_t j = 0; j < nt; ++j) y |= ldu8(p + i + j) << (8 * j);
+  s = step_k(Lb, K, s, y, nt);
+  if (nextra) s = step_k(Lb, K, s, extra & 0xffu, 1);
+  return ~s;
+}
+
+// PROBE = 1 (diagnostics only, FORST_CRC_VARIANT=probe_load): the same loads
+// and control flow, but every data word is only XOR-folded (no table lookups)
+// and every block reports ok -- the memory-side ceiling of this access pattern.
+template <int MODE, int PROBE = 0>
+__global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
+  __shared__ uint32_t L[kLds2Bytes / 4];
+  fill_tables2(L);
+  const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const Lanes2 K = lanes2(lane);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  uint64_t kbeg, kend;
+  wave_share(a.n, nw, gw, kbeg, kend);
+  if (kbeg >= kend) return;
+  const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
+
+  DescBatch cb, nb;
+  uint64_t kb = kbeg;
+  load_batch<MODE>(a, kb, kend, lane, cb);
+  load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
+  // Three cursors over the (block, round) step sequence: C is computed from
+  // the buffer filled two steps ago, P1's loads are in flight, P2's are issued
+  // now -- two 4 KiB steps (8 KiB) per wave stay in flight while C computes.
+  uint64_t k = kbeg, k1 = 0, k2 = 0;  // blocks of C, P1, P2
+  uint32_t r = 0, r1 = 0, r2 = 0;     // their rounds
+  Blk2 C = blk2_setup<MODE>(a, k, kend, kb, cb, nb);
+  Blk2 P1, P2;
+  auto advance = [&](const Blk2& b, uint64_t kk, uint32_t rr, Blk2& nbk, uint64_t& nk,
+                     uint32_t& nr) {
+    if (!b.slow() && rr + 1 < b.R) {
+      nbk = b;
+      nk = kk;
+      nr = rr + 1;
+    } else {
+      nk = kk + 1;
+      nr = 0;
+      nbk = blk2_setup<MODE>(a, nk, kend, kb, cb, nb);
+    }
+  };
+  advance(C, k, 0, P1, k1, r1);
+  advance(P1, k1, r1, P2, k2, r2);
+  uint32_t rOut = 0, rSt = 0, rOk = 0;
+  StepBuf2 X, Y, Z;
+  issue_step2<MODE>(a.base, lane, C, 0, X);
+  issue_step2<MODE>(a.base, lane, P1, r1, Y);
+  uint32_t s[2] = {0, 0};
+
+  auto flush = [&](uint32_t cnt) {
+    const uint64_t i = kb + lane;
+    const bool mine = lane < cnt;
+    if (mine && a.out32) a.out32[i] = rOut;
+    if (MODE == kModeVerify) {
+      if (mine && a.stored_out) a.stored_out[i] = rSt;
+      if (mine && a.ok_out) a.ok_out[i] = static_cast<uint8_t>(rOk);
+      const uint64_t badm = __ballot(mine && rOk == 0);
+      if (a.mismatches && badm && lane == 0)
+        atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
+    }
+    if (MODE == kModeTrailer) {
+      if (mine && rOk) {
+        const uint64_t off = (static_cast<uint64_t>(cb.off_hi) << 32) | cb.off_lo;
+        uint8_t* p = a.base_w + off + cb.size;
+        if (a.last_bytes) p[0] = static_cast<uint8_t>(cb.extra);
+        stu32_bytes(p + 1, rOut);
+      }
+    }
+  };
+
+  // one step: issue P2 into nx, compute C from cu; false when done
+  auto step = [&](StepBuf2& cu, StepBuf2& nx) -> bool {
+    issue_step2<MODE>(a.base, lane, P2, r2, nx);
+    const bool last = C.slow() || r + 1 >= C.R;
+    if (PROBE) {
+#pragma unroll
+      for (int j = 0; j < 8; ++j) {
+        s[0] ^= cu.w[0][j];
+        s[1] ^= cu.w[1][j];
+      }
+    } else if (!C.slow()) {
+      stream_round2(Lb, K, lane, C, r, s, cu.w);
+    }
+    if (last) {
+      uint32_t crc = 0, stored = 0;
+      if (PROBE) {
+        const uint32_t f = s[0] ^ s[1] ^ cu.t0 ^ cu.t1;
+        stored = crc_mask(0) + C.mod;
+        crc = __ballot(f == 0x9e3779b9u) ? 1u : 0u;
+        s[0] = s[1] = 0;
+      } else if (!C.slow()) {
+        crc = stream_finish2(Lb, K, lane, C, s, cu.t0, has_extra);
+        if (MODE == kModeVerify)
+          stored = C.nt() ? __builtin_amdgcn_alignbyte(cu.t1, cu.t0, C.nt()) : cu.t0;
+      } else if (C.valid()) {
+        const uint8_t* p = a.base + C.off;
+        const uint32_t init = MODE == kModeRaw ? C.extra : 0u;
+        crc = small_crc2(Lb, K, p, C.size + (mem_last_byte<MODE>(a) ? 1u : 0u), init, has_extra ? 1u : 0u, C.extra);
+        // retire(): keep the slow path's loads from merging into the hot path
+        if (MODE == kModeVerify) stored = retire(ldu32(p + C.size + 1));
+        crc = retire(crc);
+      }
+      uint32_t out, st = 0, ok = C.valid() ? 1u : 0u;
+      if (MODE == kModeRaw) {
+        out = crc;
+      } else if (MODE == kModeVerify) {
+        const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
+        st = stored - C.mod;
+        ok = (C.valid() && st == computed) ? 1u : 0u;
+        out = computed;
+      } else {
+        out = crc_mask(crc) + C.mod;  // format.cc:594-600 + builder.cc:1340-1345
+      }
+      if (!C.valid()) {
+        out = 0;
+        st = 0;
+      }
+      const uint32_t kk = static_cast<uint32_t>(k - kb);
+      rOut = lane == kk ? out : rOut;
+      rSt = lane == kk ? st : rSt;
+      rOk = lane == kk ? ok : rOk;
+      if (k + 1 - kb == kBatch || k + 1 == kend) {
+        flush(static_cast<uint32_t>(k + 1 - kb));
+        if (k + 1 == kend) return false;
+        kb = k + 1;
+        cb = nb;
+        load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
+      }
+    }
+    // rotate the cursors: C <- P1 <- P2 <- the step after P2
+    C = P1;
+    k = k1;
+    r = r1;
+    P1 = P2;
+    k1 = k2;
+    r1 = r2;
+    advance(P1, k1, r1, P2, k2, r2);
+    return true;
+  };
+  while (step(X, Z) && step(Y, X) && step(Z, Y)) {
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kThreads)
     crc32c_block_kernel_simple(BlockArgs a) {
@@ -603,19 +1081,30 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
 #endif
   // FORST_CRC_VARIANT=simple selects the per-block kernel (A/B reference); it
   // also serves buffers too small for the stream kernel's dummy loads.
+  // FORST_CRC_VARIANT=v1 selects the one-chain stream kernel (A/B reference).
   const char* variant = std::getenv("FORST_CRC_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < kRB;
-#define FORST_LAUNCH_CRC(M, TAG)                                                         \
-  do {                                                                                   \
-    if (simple) {                                                                        \
-      *name = "crc32c_block_kernel_simple<" TAG ">";                                     \
-      hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,   \
-                         stream, a);                                                     \
-    } else {                                                                             \
-      *name = "crc32c_stream_kernel<" TAG ">";                                           \
-      hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, \
-                         a);                                                             \
-    }                                                                                    \
+  const bool v1 = variant && std::string(variant) == "v1";
+  const bool probe = variant && std::string(variant) == "probe_load";
+#define FORST_LAUNCH_CRC(M, TAG)                                                          \
+  do {                                                                                    \
+    if (simple) {                                                                         \
+      *name = "crc32c_block_kernel_simple<" TAG ">";                                      \
+      hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,    \
+                         stream, a);                                                      \
+    } else if (v1) {                                                                      \
+      *name = "crc32c_stream_kernel<" TAG ">";                                            \
+      hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \
+                         a);                                                              \
+    } else if (probe && M == kModeVerify) {                                               \
+      *name = "crc32c_stream2_kernel<probe_load>";                                        \
+      hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 1>), dim3(grid), dim3(kThreads), \
+                         0, stream, a);                                                   \
+    } else {                                                                              \
+      *name = "crc32c_stream2_kernel<" TAG ">";                                           \
+      hipLaunchKernelGGL(crc32c_stream2_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, \
+                         a);                                                              \
+    }                                                                                     \
   } while (0)
   switch (mode) {
     case kModeCompute:

@@ -123,6 +123,18 @@ inline int __builtin_amdgcn_readfirstlane(int v) {
 inline uint32_t __builtin_amdgcn_alignbyte(uint32_t hi, uint32_t lo, uint32_t s) {
   return static_cast<uint32_t>(((static_cast<uint64_t>(hi) << 32) | lo) >> (8 * (s & 3)));
 }
+// v_perm_b32: byte n of the result = byte sel_n of {S0:S1} (0-3 -> S1, 4-7 -> S0),
+// 12 -> 0x00, >= 13 -> 0xff (8-11, sign replication, unused here)
+inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
+  const uint64_t v = (static_cast<uint64_t>(s0) << 32) | s1;
+  uint32_t r = 0;
+  for (int n = 0; n < 4; ++n) {
+    const uint32_t b = (sel >> (8 * n)) & 0xffu;
+    const uint32_t byte = b < 8 ? static_cast<uint32_t>(v >> (8 * b)) & 0xffu : b == 12 ? 0u : 0xffu;
+    r |= byte << (8 * n);
+  }
+  return r;
+}
 inline int __builtin_amdgcn_readlane(int v, int l) {
   return static_cast<int>(emu::exchange(static_cast<uint32_t>(v), static_cast<uint32_t>(l)));
 }

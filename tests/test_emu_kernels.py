@@ -144,6 +144,31 @@ def test_emu_crc_stream_batches_and_edges():
         assert int(got[k]) == O.crc32c_extend(0, base[o:o + s]), k
 
 
+def test_emu_blocks_at_buffer_start():
+    """Blocks whose first 32-byte lane segment would start in front of the
+    buffer (offset < 28, head dword index > offset/4): the v2 CRC kernel loads
+    that segment from offset 0 and re-aligns it in registers."""
+    rng = np.random.default_rng(33)
+    base = rng.integers(0, 256, 200000, dtype=np.uint8)
+    offs, sizes = [], []
+    for o in range(28):
+        for d in (0, 4, 8, 12, 20, 28, 100, 2047, 2048, 2049, 4095):
+            offs.append(o)
+            sizes.append(4096 + d + (o * 7) % 5)
+    offs = np.array(offs, np.uint64)
+    sizes = np.array(sizes, np.uint32)
+    init = rng.integers(0, 2**32, len(offs), dtype=np.uint64).astype(np.uint32)
+    got = emu.crc32c(base, offs, sizes, init=init)
+    for k in range(len(offs)):
+        o, s = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.crc32c_extend(int(init[k]), base[o:o + s]), (o, s)
+    want = O.block_checksum_batch(1, base, offs, sizes)
+    assert (emu.block_checksum(1, base, offs, sizes) == want).all()
+    comp, st, ok, bad = emu.block_verify(1, base, offs, sizes)
+    ocomp, ook, obad = O.block_verify_batch(1, base, offs, sizes)
+    assert (comp == ocomp).all() and bad == obad
+
+
 def test_emu_offsets_above_2gib():
     """64-bit descriptor offsets (bit 31 set): readlane results must not be
     sign-extended when the offset is rebuilt (a GPU-only failure mode at the

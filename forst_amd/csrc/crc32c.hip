@@ -660,10 +660,12 @@ __device__ __forceinline__ bool mem_last_byte(const BlockArgs& a) {
   return MODE == kModeVerify || ((MODE == kModeCompute || MODE == kModeTrailer) && !a.last_bytes);
 }
 
+// scalar setup (blocks of the NEXT descriptor batch: at most two per batch,
+// reached by the look-ahead cursors before the batch becomes current)
 template <int MODE>
-__device__ __forceinline__ Blk2 blk2_setup(const BlockArgs& a, uint64_t k, uint64_t kend,
-                                           uint64_t kb, const DescBatch& cb,
-                                           const DescBatch& nb) {
+__device__ __forceinline__ Blk2 blk2_setup_scalar(const BlockArgs& a, uint64_t k, uint64_t kend,
+                                                  uint64_t kb, const DescBatch& cb,
+                                                  const DescBatch& nb) {
   Blk2 b;
   const Desc d = batch_desc(k, kb, cb, nb);
   b.off = d.off;
@@ -694,6 +696,59 @@ __device__ __forceinline__ Blk2 blk2_setup(const BlockArgs& a, uint64_t k, uint6
     b.pk = cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
            (m << 17);
   }
+  return b;
+}
+
+// Per-lane derived block fields of the CURRENT descriptor batch (lane j <->
+// block kb + j), computed once per 64 blocks in vector code so that a block's
+// setup is a few v_readlane instead of ~100 scalar instructions.
+struct Derived2 {
+  uint32_t pk, R, S0;  // S0 only in raw mode (per-message init)
+};
+
+template <int MODE>
+__device__ __forceinline__ Derived2 derive2(const BlockArgs& a, const DescBatch& cb, uint64_t kb,
+                                            uint64_t kend, uint32_t lane) {
+  Derived2 d;
+  const uint64_t off = (static_cast<uint64_t>(cb.off_hi) << 32) | cb.off_lo;
+  const Desc ds{off, cb.size, cb.mod, cb.extra};
+  const bool valid = kb + lane < kend && desc_in_range<MODE>(a, ds);
+  const uint64_t E = off + cb.size + (mem_last_byte<MODE>(a) ? 1u : 0u);
+  const uint64_t ws = off & ~3ull;
+  const uint64_t we = E & ~3ull;
+  const uint64_t d4 = we - ws;
+  const uint32_t R = static_cast<uint32_t>((d4 + kRB2 - 1) / kRB2);
+  const int64_t w0 = static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRB2;
+  const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - w0);
+  const uint32_t cA = hA >> 11, lA = (hA >> 5) & 63u, jA = (hA >> 2) & 7u;
+  const int64_t seg_head = static_cast<int64_t>(ws) - 4 * static_cast<int64_t>(jA);
+  const uint32_t q = seg_head < 0 ? static_cast<uint32_t>(-seg_head) >> 2 : 0u;
+  const uint32_t nt = static_cast<uint32_t>(E - we);
+  const uint32_t m = static_cast<uint32_t>(off & 3);
+  const bool slow = !valid || d4 < 64;
+  d.R = slow ? 1u : R;
+  d.pk = slow ? ((nt << 13) | (valid ? 1u << 15 : 0u) | (1u << 16) | (m << 17))
+              : (cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
+                 (m << 17));
+  d.S0 = MODE == kModeRaw ? unstep_m(~cb.extra, m) : 0u;
+  return d;
+}
+
+template <int MODE>
+__device__ __forceinline__ Blk2 blk2_setup(const BlockArgs& a, uint64_t k, uint64_t kend,
+                                           uint64_t kb, const DescBatch& cb, const DescBatch& nb,
+                                           const Derived2& cd) {
+  if (k - kb >= kBatch) return blk2_setup_scalar<MODE>(a, k, kend, kb, cb, nb);
+  const uint32_t sl = static_cast<uint32_t>(k - kb);
+  Blk2 b;
+  b.off = readlane64(cb.off_lo, cb.off_hi, sl);
+  b.size = readlane32(cb.size, sl);
+  b.mod = readlane32(cb.mod, sl);
+  b.extra = readlane32(cb.extra, sl);
+  b.pk = readlane32(cd.pk, sl);
+  b.R = readlane32(cd.R, sl);
+  b.S0 = MODE == kModeRaw ? readlane32(cd.S0, sl) : kCrcS0[b.pk >> 17];
+  b.we = b.slow() ? kRB2 : ((b.off + b.size + (mem_last_byte<MODE>(a) ? 1u : 0u)) & ~3ull);
   return b;
 }
 
@@ -874,12 +929,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
   uint64_t kb = kbeg;
   load_batch<MODE>(a, kb, kend, lane, cb);
   load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
+  Derived2 cd = derive2<MODE>(a, cb, kb, kend, lane);
   // Three cursors over the (block, round) step sequence: C is computed from
   // the buffer filled two steps ago, P1's loads are in flight, P2's are issued
   // now -- two 4 KiB steps (8 KiB) per wave stay in flight while C computes.
   uint64_t k = kbeg, k1 = 0, k2 = 0;  // blocks of C, P1, P2
   uint32_t r = 0, r1 = 0, r2 = 0;     // their rounds
-  Blk2 C = blk2_setup<MODE>(a, k, kend, kb, cb, nb);
+  Blk2 C = blk2_setup<MODE>(a, k, kend, kb, cb, nb, cd);
   Blk2 P1, P2;
   auto advance = [&](const Blk2& b, uint64_t kk, uint32_t rr, Blk2& nbk, uint64_t& nk,
                      uint32_t& nr) {
@@ -890,7 +946,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
     } else {
       nk = kk + 1;
       nr = 0;
-      nbk = blk2_setup<MODE>(a, nk, kend, kb, cb, nb);
+      nbk = blk2_setup<MODE>(a, nk, kend, kb, cb, nb, cd);
     }
   };
   advance(C, k, 0, P1, k1, r1);
@@ -978,6 +1034,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
         if (k + 1 == kend) return false;
         kb = k + 1;
         cb = nb;
+        cd = derive2<MODE>(a, cb, kb, kend, lane);
         load_batch<MODE>(a, kb + kBatch, kend, lane, nb);
       }
     }

@@ -789,7 +789,29 @@ __device__ __forceinline__ void issue_step2(const uint8_t* __restrict__ base, ui
   buf.t1 = MODE == kModeVerify ? ld4v(base + (b.slow() || nt == 0 ? t0 : t0 + 4)) : 0u;
 }
 
-// one round of both chains
+__device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
+  return __builtin_amdgcn_bitop3_b32(a, b, c, 0x96);  // v_bitop3_b32: a ^ b ^ c
+}
+
+// the four table reads of G(x) (J = false) or J2(x) (J = true)
+template <bool J>
+__device__ __forceinline__ void rep_look(const uint8_t* __restrict__ Lb, const Lanes2& k,
+                                         uint32_t x, uint32_t (&l)[4]) {
+#pragma unroll
+  for (int i = 0; i < 4; ++i)
+    l[i] = lds32(Lb, __builtin_amdgcn_perm(x, k.lreg[i], k.sel[i]) + (J ? 128u : 0u));
+}
+
+// G(x) ^ e: the next chain input when e is the next data word
+__device__ __forceinline__ uint32_t g_then(const uint8_t* __restrict__ Lb, const Lanes2& k,
+                                           uint32_t x, uint32_t e) {
+  uint32_t l[4];
+  rep_look<false>(Lb, k, x, l);
+  return xor3(l[0], l[1], xor3(l[2], l[3], e));
+}
+
+// one round of both chains.  Chain inputs are carried as x = state ^ next word,
+// so every step is 4 v_perm + 4 ds_read + 2 v_bitop3.
 __device__ __forceinline__ void stream_round2(const uint8_t* __restrict__ Lb, const Lanes2& K,
                                               uint32_t lane, const Blk2& b, uint32_t r,
                                               uint32_t (&s)[2], const uint32_t (&w)[2][8]) {
@@ -814,29 +836,41 @@ __device__ __forceinline__ void stream_round2(const uint8_t* __restrict__ Lb, co
 #pragma unroll
         for (int j = 0; j < 8; ++j) wc[j] = lane == lA ? sh[j] : wc[j];
       }
-      uint32_t sc = 0;
+      // words in front of the message's first dword are zeroed (G(0) = 0, so
+      // the chain state stays 0 until the head word) ...
+      const uint32_t js = (c < cA || (c == cA && lane < lA)) ? 8u
+                          : (c == cA && lane == lA)          ? jA
+                                                             : 0u;
 #pragma unroll
-      for (uint32_t j = 0; j < 8; ++j) {
-        uint32_t x = sc ^ wc[j];
-        if (c == cA && j == jA) {
-          const uint32_t head = (wc[j] & bm) ^ b.S0;
-          x = lane == lA ? head : x;
-        }
-        sc = rep_map<false>(Lb, K, x);
+      for (uint32_t j = 0; j < 8; ++j) wc[j] = j < js ? 0u : wc[j];
+      // ... and the head word of the head lane loses the bytes in front of
+      // the message and gains S0 (uniform dynamic index jA)
+      if (c == cA) {
+        const uint32_t hv = wc[jA];
+        wc[jA] = lane == lA ? ((hv & bm) ^ b.S0) : hv;
       }
-      const bool pre = c < cA || (c == cA && lane < lA);
-      s[c] = pre ? 0u : sc;
+      uint32_t x = wc[0];
+#pragma unroll
+      for (int j = 1; j < 8; ++j) x = g_then(Lb, K, x, wc[j]);
+      s[c] = g_then(Lb, K, x, 0u);
     }
   } else {
-    uint32_t s0 = rep_map<true>(Lb, K, s[0]) ^ rep_map<false>(Lb, K, w[0][0]);
-    uint32_t s1 = rep_map<true>(Lb, K, s[1]) ^ rep_map<false>(Lb, K, w[1][0]);
+    // first word of each chain: J2(s) ^ G(w0) ^ w1 (hop fused with the step)
+    uint32_t x[2];
 #pragma unroll
-    for (int j = 1; j < 8; ++j) {
-      s0 = rep_map<false>(Lb, K, s0 ^ w[0][j]);
-      s1 = rep_map<false>(Lb, K, s1 ^ w[1][j]);
+    for (int c = 0; c < 2; ++c) {
+      uint32_t lj[4], lg[4];
+      rep_look<true>(Lb, K, s[c], lj);
+      rep_look<false>(Lb, K, w[c][0], lg);
+      x[c] = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]), xor3(lg[2], lg[3], w[c][1]));
     }
-    s[0] = s0;
-    s[1] = s1;
+#pragma unroll
+    for (int j = 2; j < 8; ++j) {
+      x[0] = g_then(Lb, K, x[0], w[0][j]);
+      x[1] = g_then(Lb, K, x[1], w[1][j]);
+    }
+    s[0] = g_then(Lb, K, x[0], 0u);
+    s[1] = g_then(Lb, K, x[1], 0u);
   }
 }
 
@@ -982,18 +1016,26 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
   auto step = [&](StepBuf2& cu, StepBuf2& nx) -> bool {
     issue_step2<MODE>(a.base, lane, P2, r2, nx);
     const bool last = C.slow() || r + 1 >= C.R;
-    if (PROBE) {
+    if (PROBE == 1) {
 #pragma unroll
       for (int j = 0; j < 8; ++j) {
         s[0] ^= cu.w[0][j];
         s[1] ^= cu.w[1][j];
       }
+    } else if (PROBE == 3 && !C.slow()) {
+      stream_round2(Lb, K, lane, C, 1, s, cu.w);  // no head handling
     } else if (!C.slow()) {
       stream_round2(Lb, K, lane, C, r, s, cu.w);
     }
     if (last) {
       uint32_t crc = 0, stored = 0;
-      if (PROBE) {
+      if (PROBE == 2 || PROBE == 3) {  // rounds only / no head: finish cost still in 3
+        const uint32_t f = PROBE == 3 ? stream_finish2(Lb, K, lane, C, s, cu.t0, has_extra)
+                                      : s[0] ^ s[1];
+        stored = crc_mask(0) + C.mod;
+        crc = __ballot(f == 0x9e3779b9u) ? 1u : 0u;
+        s[0] = s[1] = 0;
+      } else if (PROBE) {
         const uint32_t f = s[0] ^ s[1] ^ cu.t0 ^ cu.t1;
         stored = crc_mask(0) + C.mod;
         crc = __ballot(f == 0x9e3779b9u) ? 1u : 0u;
@@ -1142,7 +1184,13 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   const char* variant = std::getenv("FORST_CRC_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < kRB;
   const bool v1 = variant && std::string(variant) == "v1";
-  const bool probe = variant && std::string(variant) == "probe_load";
+  // diagnostics: probe_load (loads only), probe_rounds (no finish),
+  // probe_nohead (no round-0 head handling); results are not checksums
+  const int probe = !variant ? 0
+                    : std::string(variant) == "probe_load"   ? 1
+                    : std::string(variant) == "probe_rounds" ? 2
+                    : std::string(variant) == "probe_nohead" ? 3
+                                                             : 0;
 #define FORST_LAUNCH_CRC(M, TAG)                                                          \
   do {                                                                                    \
     if (simple) {                                                                         \
@@ -1154,9 +1202,16 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
       hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \
                          a);                                                              \
     } else if (probe && M == kModeVerify) {                                               \
-      *name = "crc32c_stream2_kernel<probe_load>";                                        \
-      hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 1>), dim3(grid), dim3(kThreads), \
-                         0, stream, a);                                                   \
+      *name = "crc32c_stream2_kernel<probe>";                                             \
+      if (probe == 1)                                                                     \
+        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 1>), dim3(grid),           \
+                           dim3(kThreads), 0, stream, a);                                 \
+      else if (probe == 2)                                                                \
+        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 2>), dim3(grid),           \
+                           dim3(kThreads), 0, stream, a);                                 \
+      else                                                                                \
+        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 3>), dim3(grid),           \
+                           dim3(kThreads), 0, stream, a);                                 \
     } else {                                                                              \
       *name = "crc32c_stream2_kernel<" TAG ">";                                           \
       hipLaunchKernelGGL(crc32c_stream2_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, \

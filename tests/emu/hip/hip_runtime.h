@@ -135,6 +135,15 @@ inline uint32_t __builtin_amdgcn_perm(uint32_t s0, uint32_t s1, uint32_t sel) {
   }
   return r;
 }
+// v_bitop3_b32: bit i of the result = bit ((a_i << 2) | (b_i << 1) | c_i) of imm
+inline uint32_t __builtin_amdgcn_bitop3_b32(uint32_t a, uint32_t b, uint32_t c, uint32_t imm) {
+  uint32_t r = 0;
+  for (int i = 0; i < 32; ++i) {
+    const uint32_t idx = (((a >> i) & 1u) << 2) | (((b >> i) & 1u) << 1) | ((c >> i) & 1u);
+    r |= ((imm >> idx) & 1u) << i;
+  }
+  return r;
+}
 inline int __builtin_amdgcn_readlane(int v, int l) {
   return static_cast<int>(emu::exchange(static_cast<uint32_t>(v), static_cast<uint32_t>(l)));
 }

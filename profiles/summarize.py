@@ -22,11 +22,16 @@ from collections import defaultdict
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 
 
+MODES = {"0": "compute", "1": "trailer", "2": "verify", "3": "raw"}
+
+
 def short(name):
+    """rocprof's demangled name -> the engine's kernel name (forst_last_kernel)"""
+    import re
     n = name.replace("forst::(anonymous namespace)::", "").replace("void ", "")
     n = n.split("(forst::")[0].split("(unsigned")[0]
-    return n.replace("<0>", "<compute>").replace("<1>", "<trailer>").replace(
-        "<2>", "<verify>").replace("<3>", "<raw>")
+    # <MODE> or <MODE, 0> -> <mode>; probe instantiations keep their numbers
+    return re.sub(r"<(\d)(?:, 0)?>", lambda m: "<" + MODES[m.group(1)] + ">", n)
 
 
 def load_counter(path):

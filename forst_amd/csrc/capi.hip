@@ -257,6 +257,92 @@ FORST_API int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                     "wal_record_crc launch");
 }
 
+namespace forst {
+namespace {
+int dispatch_kv(int mode, const KvArgs& a, void* stream) {
+  if (a.n == 0) return FORST_OK;
+  if (!a.base || !a.key_off || !a.key_len)
+    return set_error(FORST_EINVAL, "base/offsets/lengths must be non-null");
+  int rc = check_device();
+  if (rc) return rc;
+  return hip_status(launch_kv(mode, a, static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "kv launch");
+}
+}  // namespace
+}  // namespace forst
+
+FORST_API int forst_hash64_batch(const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
+                                 const uint32_t* lengths, const uint64_t* seeds, uint64_t seed,
+                                 uint64_t* out, uint64_t n, void* stream) {
+  if (n && !out) return set_error(FORST_EINVAL, "out must be non-null");
+  KvArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.key_off = offsets;
+  a.key_len = lengths;
+  a.seeds = seeds;
+  a.seed = seed;
+  a.out = out;
+  a.n = n;
+  return dispatch_kv(kKvHash, a, stream);
+}
+
+FORST_API int forst_kv_protect_batch(const uint8_t* base, uint64_t base_len,
+                                     const uint64_t* key_offsets, const uint32_t* key_sizes,
+                                     const uint64_t* value_offsets, const uint32_t* value_sizes,
+                                     const uint8_t* op_types, const uint64_t* seqnos,
+                                     const uint32_t* cf_ids, uint64_t* out, uint64_t n,
+                                     void* stream) {
+  if (n && (!out || !value_offsets || !value_sizes))
+    return set_error(FORST_EINVAL, "out/value_offsets/value_sizes must be non-null");
+  KvArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.key_off = key_offsets;
+  a.key_len = key_sizes;
+  a.val_off = value_offsets;
+  a.val_len = value_sizes;
+  a.ops = op_types;
+  a.seqs = seqnos;
+  a.cfs = cf_ids;
+  a.out = out;
+  a.n = n;
+  return dispatch_kv(kKvProtect, a, stream);
+}
+
+FORST_API int forst_kv_verify_batch(const uint8_t* base, uint64_t base_len,
+                                    const uint64_t* key_offsets, const uint32_t* key_sizes,
+                                    const uint64_t* value_offsets, const uint32_t* value_sizes,
+                                    const uint8_t* op_types, const uint64_t* seqnos,
+                                    const uint32_t* cf_ids, uint32_t protection_bytes,
+                                    const uint64_t* checksum_offsets, uint64_t* computed,
+                                    uint8_t* ok, unsigned long long* mismatches, uint64_t n,
+                                    void* stream) {
+  if (n && (!value_offsets || !value_sizes || !checksum_offsets))
+    return set_error(FORST_EINVAL, "value/checksum arrays must be non-null");
+  // kv_checksum.h:97-133 supports 1, 2, 4, 8 (advanced_options.h:1227)
+  if (protection_bytes != 1 && protection_bytes != 2 && protection_bytes != 4 &&
+      protection_bytes != 8)
+    return set_error(FORST_EINVAL, "protection_bytes must be 1, 2, 4 or 8");
+  KvArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.key_off = key_offsets;
+  a.key_len = key_sizes;
+  a.val_off = value_offsets;
+  a.val_len = value_sizes;
+  a.ops = op_types;
+  a.seqs = seqnos;
+  a.cfs = cf_ids;
+  a.prot_bytes = protection_bytes;
+  a.chk_off = checksum_offsets;
+  a.out = computed;
+  a.ok = ok;
+  a.mismatches = mismatches;
+  a.n = n;
+  return dispatch_kv(kKvVerify, a, stream);
+}
+
 FORST_API int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
                                 void* stream) {
   if (n == 0) return FORST_OK;

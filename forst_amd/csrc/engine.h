@@ -50,6 +50,33 @@ struct WalArgs {
   uint32_t* crc_out;
 };
 
+// Per-KV protection / Hash64 batches (kv_protect.hip).
+enum KvMode : int {
+  kKvHash = 0,     // out[i] = Hash64(key_i, seeds ? seeds[i] : seed)
+  kKvProtect = 1,  // out[i] = ProtectionInfo64 of (key, value[, op][, seq][, cf])
+  kKvVerify = 2,   // ... compared with prot_bytes LE bytes at chk_off[i]
+};
+
+struct KvArgs {
+  const uint8_t* base;
+  uint64_t base_len;
+  const uint64_t* key_off;  // (buffers in Hash64 mode)
+  const uint32_t* key_len;
+  const uint64_t* val_off;
+  const uint32_t* val_len;
+  const uint8_t* ops;        // nullable: ProtectKV instead of ProtectKVO
+  const uint64_t* seqs;      // nullable: no ProtectS
+  const uint32_t* cfs;       // nullable: no ProtectC
+  const uint64_t* seeds;     // Hash64 mode, nullable
+  uint64_t seed;
+  const uint64_t* chk_off;   // verify
+  uint32_t prot_bytes;       // verify: 1, 2, 4 or 8
+  uint64_t* out;             // nullable in verify mode
+  uint8_t* ok;               // verify, nullable
+  unsigned long long* mismatches;  // verify, nullable
+  uint64_t n;
+};
+
 struct DeviceInfo {
   int device;
   int num_cus;
@@ -71,6 +98,7 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
                              const char** kernel_name);
 hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,
                                  const char** kernel_name);
+hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n,
                               uint64_t seed, hipStream_t stream);
 

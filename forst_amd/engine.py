@@ -175,6 +175,53 @@ def wal_record_crc_batch(log, header_offsets, write_in_place=True, out=None, str
     return out
 
 
+def hash64_batch(base, offsets, lengths, seeds=None, seed=0, out=None, stream=None):
+    """Hash64 / NPHash64 per buffer (util/hash.cc:81, XXPH3 0.7.2 preview)."""
+    n = _desc(offsets, lengths)
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint64, device=base.device)
+    check(lib().forst_hash64_batch(base.data_ptr(), base.numel(), offsets.data_ptr(),
+                                   lengths.data_ptr(), _p(seeds), seed & (2**64 - 1),
+                                   out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def kv_protect_batch(base, key_offsets, key_sizes, value_offsets, value_sizes, op_types=None,
+                     seqnos=None, cf_ids=None, out=None, stream=None):
+    """ProtectionInfo64 ProtectKV / ProtectKVO [+S] [+C] per entry (db/kv_checksum.h)."""
+    n = _desc(key_offsets, key_sizes)
+    assert _desc(value_offsets, value_sizes) == n
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint64, device=base.device)
+    check(lib().forst_kv_protect_batch(base.data_ptr(), base.numel(), key_offsets.data_ptr(),
+                                       key_sizes.data_ptr(), value_offsets.data_ptr(),
+                                       value_sizes.data_ptr(), _p(op_types), _p(seqnos),
+                                       _p(cf_ids), out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def kv_verify_batch(base, key_offsets, key_sizes, value_offsets, value_sizes, protection_bytes,
+                    checksum_offsets, op_types=None, seqnos=None, cf_ids=None, computed=True,
+                    ok=True, mismatches=None, stream=None):
+    """ProtectionInfo<T>::Verify per entry (db/kv_checksum.h:117-133), e.g.
+    MemTable::VerifyEntryChecksum.  Returns (computed, ok, mismatches)."""
+    n = _desc(key_offsets, key_sizes)
+    _dev_u8(base)
+    dev = base.device
+    c = torch.empty(n, dtype=torch.uint64, device=dev) if computed is True else computed
+    o = torch.empty(n, dtype=torch.uint8, device=dev) if ok is True else ok
+    if mismatches is None:
+        mismatches = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(lib().forst_kv_verify_batch(base.data_ptr(), base.numel(), key_offsets.data_ptr(),
+                                      key_sizes.data_ptr(), value_offsets.data_ptr(),
+                                      value_sizes.data_ptr(), _p(op_types), _p(seqnos),
+                                      _p(cf_ids), protection_bytes, checksum_offsets.data_ptr(),
+                                      _p(c), _p(o), _p(mismatches), n, _stream(stream)))
+    return c, o, mismatches
+
+
 def fill_stream(dev_u8, start, seed, stream=None):
     """Synthetic splitmix64 byte stream written on the device."""
     _dev_u8(dev_u8)

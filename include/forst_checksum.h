@@ -30,6 +30,11 @@
  *                                  block per wave
  *   forst_wal_record_crc_batch  <- log::Writer::EmitPhysicalRecord CRC
  *                                  (db/log_writer.cc:228-263)
+ *   forst_hash64_batch          <- Hash64 / NPHash64 (util/hash.cc:81-88)
+ *   forst_kv_protect_batch      <- ProtectionInfo64 ProtectKV[O][S|C]
+ *                                  (db/kv_checksum.h:296-460)
+ *   forst_kv_verify_batch       <- ProtectionInfo<T>::Verify
+ *                                  (db/kv_checksum.h:117-133)
  *
  * Conventions
  *  - All array/buffer pointers are DEVICE pointers (hipMalloc'd, or host
@@ -155,6 +160,44 @@ int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                                const uint64_t* header_offsets,
                                uint64_t n_records, int write_in_place,
                                uint32_t* crc_out, void* stream);
+
+/* NPHash64 / Hash64 (util/hash.h:45-62, util/hash.cc:81 ->
+ * XXPH3_64bits_withSeed, util/xxph3.h:1733; xxHash 0.7.2 preview):
+ * out[i] = Hash64(base + offsets[i], lengths[i], seeds ? seeds[i] : seed).
+ * Out-of-range buffers give 0. */
+int forst_hash64_batch(const uint8_t* base, uint64_t base_len, const uint64_t* offsets,
+                       const uint32_t* lengths, const uint64_t* seeds, uint64_t seed,
+                       uint64_t* out, uint64_t n, void* stream);
+
+/* Per-KV protection info (a15, db/kv_checksum.h): out[i] =
+ *   ProtectionInfo64().ProtectKV(key_i, value_i)               (op_types == NULL)
+ *   ProtectionInfo64().ProtectKVO(key_i, value_i, op_types[i])  (kv_checksum.h:296)
+ *   [.ProtectS(seqnos[i])]  if seqnos != NULL                   (kv_checksum.h:453)
+ *   [.ProtectC(cf_ids[i])]  if cf_ids != NULL                   (kv_checksum.h:420)
+ * i.e. the XOR of NPHash64 of each field with its seed (kv_checksum.h:84-88).
+ * key_i = base[key_offsets[i] .. + key_sizes[i]), value_i likewise.  The
+ * WriteBatch / memtable / block callers (write_batch.cc:824+,
+ * memtable.cc:273-307, block.h:271) Encode() the low 1/2/4/8 bytes. */
+int forst_kv_protect_batch(const uint8_t* base, uint64_t base_len,
+                           const uint64_t* key_offsets, const uint32_t* key_sizes,
+                           const uint64_t* value_offsets, const uint32_t* value_sizes,
+                           const uint8_t* op_types, const uint64_t* seqnos,
+                           const uint32_t* cf_ids, uint64_t* out, uint64_t n, void* stream);
+
+/* ProtectionInfo<T>::Verify(protection_bytes, checksum_ptr)
+ * (kv_checksum.h:117-133) per entry, as MemTable::VerifyEntryChecksum
+ * (memtable.cc:273-307) and the block kv checksums do it: the low
+ * protection_bytes (1, 2, 4, 8) bytes of the protection value against the LE
+ * bytes at base + checksum_offsets[i].  computed / ok may be NULL;
+ * *mismatches (device counter, may be NULL) += failing entries (entries whose
+ * fields reach past base_len fail). */
+int forst_kv_verify_batch(const uint8_t* base, uint64_t base_len,
+                          const uint64_t* key_offsets, const uint32_t* key_sizes,
+                          const uint64_t* value_offsets, const uint32_t* value_sizes,
+                          const uint8_t* op_types, const uint64_t* seqnos,
+                          const uint32_t* cf_ids, uint32_t protection_bytes,
+                          const uint64_t* checksum_offsets, uint64_t* computed, uint8_t* ok,
+                          unsigned long long* mismatches, uint64_t n, void* stream);
 
 /* Bench/test utility: fill dev[0 .. n) with bytes [start, start+n) of the
  * splitmix64 stream `seed` (SURVEY.md §8d synthetic inputs). */

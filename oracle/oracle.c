@@ -729,6 +729,23 @@ uint64_t oracle_kv_protect(const void* key, size_t klen, const void* value, size
   return v;
 }
 
+void oracle_hash64_batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint64_t* seeds, uint64_t seed, uint64_t* out, size_t n) {
+  for (size_t i = 0; i < n; i++)
+    out[i] = oracle_hash64(base + offsets[i], lengths[i], seeds ? seeds[i] : seed);
+}
+
+void oracle_kv_protect_batch(const uint8_t* base, const uint64_t* key_offsets,
+                             const uint32_t* key_sizes, const uint64_t* value_offsets,
+                             const uint32_t* value_sizes, const uint8_t* op_types,
+                             const uint64_t* seqnos, const uint32_t* cf_ids, uint64_t* out,
+                             size_t n) {
+  for (size_t i = 0; i < n; i++)
+    out[i] = oracle_kv_protect(base + key_offsets[i], key_sizes[i], base + value_offsets[i],
+                               value_sizes[i], op_types ? op_types[i] : -1, seqnos != NULL,
+                               seqnos ? seqnos[i] : 0, cf_ids != NULL, cf_ids ? cf_ids[i] : 0);
+}
+
 /* ProtectionInfo<T>::Verify (kv_checksum.h:117-133): the low `len` bytes of
  * the protection value against the LE bytes at `stored`. */
 int oracle_kv_verify(uint64_t prot, uint32_t len, const void* stored) {

@@ -37,6 +37,23 @@ uint64_t oracle_xxh3_64(const void* p, size_t n);
 uint32_t oracle_xxh32(const void* p, size_t n, uint32_t seed);
 uint64_t oracle_xxh64(const void* p, size_t n, uint64_t seed);
 
+/* ---- XXPH3 (xxHash 0.7.2 preview, util/xxph3.h): Hash64 / NPHash64 ---- */
+uint64_t oracle_hash64(const void* p, size_t n, uint64_t seed); /* util/hash.cc:81 */
+/* db/kv_checksum.h ProtectionInfo64: ProtectKV (op_type < 0) / ProtectKVO,
+ * then ProtectS if has_seq, ProtectC if has_cf */
+uint64_t oracle_kv_protect(const void* key, size_t klen, const void* value, size_t vlen,
+                           int op_type, int has_seq, uint64_t seq, int has_cf, uint32_t cf);
+/* ProtectionInfo<T>::Verify (kv_checksum.h:117-133); 1 if the low len bytes match */
+int oracle_kv_verify(uint64_t prot, uint32_t len, const void* stored);
+/* batch forms matching forst_hash64_batch / forst_kv_{protect,verify}_batch */
+void oracle_hash64_batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
+                         const uint64_t* seeds, uint64_t seed, uint64_t* out, size_t n);
+void oracle_kv_protect_batch(const uint8_t* base, const uint64_t* key_offsets,
+                             const uint32_t* key_sizes, const uint64_t* value_offsets,
+                             const uint32_t* value_sizes, const uint8_t* op_types,
+                             const uint64_t* seqnos, const uint32_t* cf_ids, uint64_t* out,
+                             size_t n);
+
 /* ---- block checksum dispatcher (table/format.cc, table/format.h) ---- */
 uint32_t oracle_compute_builtin_checksum(int type, const void* p, size_t n);
 uint32_t oracle_compute_builtin_checksum_with_last_byte(int type, const void* p,

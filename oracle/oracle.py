@@ -54,6 +54,11 @@ def lib():
             "oracle_wal_framed_size": (u64, [vp, sz, i]),
             "oracle_wal_frame": (u64, [vp, vp, sz, i, u32, vp, vp, vp, vp]),
             "oracle_wal_verify": (u64, [vp, u64, vp, u64, vp, i]),
+            "oracle_hash64": (u64, [vp, sz, u64]),
+            "oracle_kv_protect": (u64, [vp, sz, vp, sz, i, i, u64, i, u32]),
+            "oracle_kv_verify": (i, [u64, u32, vp]),
+            "oracle_hash64_batch": (None, [vp, vp, vp, vp, u64, vp, sz]),
+            "oracle_kv_protect_batch": (None, [vp, vp, vp, vp, vp, vp, vp, vp, vp, sz]),
             "oracle_splitmix64": (u64, [u64]),
             "oracle_fill_stream": (None, [vp, u64, u64, u64]),
         }
@@ -206,6 +211,49 @@ def wal_verify(buf, nthreads=1):
     bad = ctypes.c_uint64()
     n = lib().oracle_wal_verify(_ptr(buf), buf.nbytes, None, 0, ctypes.byref(bad), nthreads)
     return n, bad.value
+
+
+KV_SEED_K, KV_SEED_V = 0, 0xD28AAD72F49BD50B  # db/kv_checksum.h:84-88
+KV_SEED_O, KV_SEED_S, KV_SEED_C = 0xA5155AE5E937AA16, 0x77A00858DDD37F21, 0x4A2AB5CBD26F542C
+
+
+def hash64(data, seed=0):
+    """util/hash.cc:81 Hash64 = XXPH3_64bits_withSeed (util/xxph3.h:1733)"""
+    p, n, _k = _buf(data)
+    return lib().oracle_hash64(p, n, seed & (2**64 - 1))
+
+
+def kv_protect(key, value, op_type=None, seq=None, cf=None):
+    """ProtectionInfo64().ProtectKV[O](...)[.ProtectS(seq)][.ProtectC(cf)]"""
+    kp, kn, _k1 = _buf(key)
+    vp, vn, _k2 = _buf(value)
+    return lib().oracle_kv_protect(kp, kn, vp, vn, -1 if op_type is None else op_type,
+                                   seq is not None, seq or 0, cf is not None, cf or 0)
+
+
+def hash64_batch(base, offsets, lengths, seeds=None, seed=0):
+    out = np.zeros(len(offsets), dtype=np.uint64)
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    lengths = np.ascontiguousarray(lengths, np.uint32)
+    lib().oracle_hash64_batch(_ptr(base), _ptr(offsets), _ptr(lengths),
+                              _ptr(None if seeds is None else np.ascontiguousarray(seeds, np.uint64)),
+                              seed, _ptr(out), len(offsets))
+    return out
+
+
+def kv_protect_batch(base, key_offsets, key_sizes, value_offsets, value_sizes, op_types=None,
+                     seqnos=None, cf_ids=None):
+    n = len(key_offsets)
+    out = np.zeros(n, dtype=np.uint64)
+    arrs = [np.ascontiguousarray(key_offsets, np.uint64), np.ascontiguousarray(key_sizes, np.uint32),
+            np.ascontiguousarray(value_offsets, np.uint64),
+            np.ascontiguousarray(value_sizes, np.uint32)]
+    opt = [None if op_types is None else np.ascontiguousarray(op_types, np.uint8),
+           None if seqnos is None else np.ascontiguousarray(seqnos, np.uint64),
+           None if cf_ids is None else np.ascontiguousarray(cf_ids, np.uint32)]
+    lib().oracle_kv_protect_batch(_ptr(base), *[_ptr(a) for a in arrs], *[_ptr(a) for a in opt],
+                                  _ptr(out), n)
+    return out
 
 
 def splitmix64(x):

@@ -32,6 +32,10 @@ def lib():
             "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
             "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
             "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
+            "forst_hash64_batch": (i, [vp, u64, vp, vp, vp, u64, vp, u64, vp]),
+            "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
+            "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp,
+                                          vp, u64, vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -122,3 +126,45 @@ def wal_verify(log, log_number=0):
     _chk(lib().forst_wal_verify_batch(_p(log), log.nbytes, 0, nb, log_number, _p(st), _p(nrec),
                                       _p(fail), _p(bad), None))
     return st, nrec, fail, int(bad[0])
+
+
+def hash64(base, offs, lens, seeds=None, seed=0):
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    sd = None if seeds is None else np.ascontiguousarray(seeds, np.uint64)
+    out = np.zeros(len(offs), np.uint64)
+    _chk(lib().forst_hash64_batch(_p(base), base.nbytes, _p(offs), _p(lens), _p(sd), seed,
+                                  _p(out), len(offs), None))
+    return out
+
+
+def _kv_arrays(ko, ks, vo, vs, ops, seqs, cfs):
+    return ([np.ascontiguousarray(ko, np.uint64), np.ascontiguousarray(ks, np.uint32),
+             np.ascontiguousarray(vo, np.uint64), np.ascontiguousarray(vs, np.uint32)],
+            [None if ops is None else np.ascontiguousarray(ops, np.uint8),
+             None if seqs is None else np.ascontiguousarray(seqs, np.uint64),
+             None if cfs is None else np.ascontiguousarray(cfs, np.uint32)])
+
+
+def kv_protect(base, ko, ks, vo, vs, ops=None, seqs=None, cfs=None):
+    base = _aligned(base)
+    arrs, opt = _kv_arrays(ko, ks, vo, vs, ops, seqs, cfs)
+    out = np.zeros(len(arrs[0]), np.uint64)
+    _chk(lib().forst_kv_protect_batch(_p(base), base.nbytes, *[_p(a) for a in arrs],
+                                      *[_p(a) for a in opt], _p(out), len(out), None))
+    return out
+
+
+def kv_verify(base, ko, ks, vo, vs, prot_bytes, chk, ops=None, seqs=None, cfs=None):
+    base = _aligned(base)
+    arrs, opt = _kv_arrays(ko, ks, vo, vs, ops, seqs, cfs)
+    n = len(arrs[0])
+    chk = np.ascontiguousarray(chk, np.uint64)
+    comp = np.zeros(n, np.uint64)
+    ok = np.zeros(n, np.uint8)
+    bad = np.zeros(1, np.uint64)
+    _chk(lib().forst_kv_verify_batch(_p(base), base.nbytes, *[_p(a) for a in arrs],
+                                     *[_p(a) for a in opt], prot_bytes, _p(chk), _p(comp),
+                                     _p(ok), _p(bad), n, None))
+    return comp, ok, int(bad[0])

@@ -242,9 +242,23 @@ def make_ref_vectors(L):
             crc = L.ref_crc32c_mask(L.ref_crc32c_value(ctypes.c_char_p(buf), len(buf)))
             wal.append({"type": rtype, "log_number": lognum, "payload_hex": payload.hex(),
                         "masked_crc": crc})
+    # per-KV protection fields (db/kv_checksum.h:84-88, :296-460): NPHash64 of
+    # the op type (1 byte), sequence number (8 bytes LE) and column family id
+    # (4 bytes LE) with their seeds, by the reference's Hash64 (util/hash.cc:81)
+    kv = {"op": [], "seq": [], "cf": []}
+    for op in range(0, 32):
+        b = bytes([op])
+        kv["op"].append([op, L.ref_hash64(ctypes.c_char_p(b), 1, 0xA5155AE5E937AA16)])
+    for seq in [0, 1, 2, 255, 256, 0x123456789A, (1 << 56) - 1, (1 << 64) - 1] + \
+            [int(x) for x in rng.integers(0, 2**63, 24)]:
+        b = seq.to_bytes(8, "little")
+        kv["seq"].append([seq, L.ref_hash64(ctypes.c_char_p(b), 8, 0x77A00858DDD37F21)])
+    for cf in [0, 1, 2, 7, 0xFFFFFFFF] + [int(x) for x in rng.integers(0, 2**32, 11)]:
+        b = cf.to_bytes(4, "little")
+        kv["cf"].append([cf, L.ref_hash64(ctypes.c_char_p(b), 4, 0x4A2AB5CBD26F542C)])
     return raw, {"blob_bytes": total,
                  "lengths_note": "vectors[i] covers stream.golden_blob(blob_bytes)[off:off+n]",
-                 "vectors": vecs, "modifiers": mods, "wal": wal}
+                 "vectors": vecs, "modifiers": mods, "wal": wal, "kv_fields": kv}
 
 
 def main():

@@ -185,3 +185,33 @@ def test_emu_offsets_above_2gib():
     for k in range(len(offs)):
         o, s = int(offs[k]), int(sizes[k])
         assert int(got[k]) == O.crc32c_extend(0, base[o:o + s]), k
+
+
+def test_emu_hash64_golden(golden_arrays):
+    # Hash64 (XXPH3) kernel vs the reference's values, per-buffer seeds
+    v, arr, offs, lens = golden_arrays
+    got0 = emu.hash64(arr, offs, lens)
+    assert (got0 == np.array([r["hash64_s0"] for r in v["vectors"]], np.uint64)).all()
+    seeds = np.full(len(offs), O.KV_SEED_V, np.uint64)
+    got1 = emu.hash64(arr, offs, lens, seeds=seeds)
+    assert (got1 == np.array([r["hash64_s1"] for r in v["vectors"]], np.uint64)).all()
+
+
+@pytest.mark.parametrize("prot_bytes,flags", [(8, (True, True, False)), (1, (False, False, False)),
+                                              (4, (True, True, True)), (2, (True, False, True))])
+def test_emu_kv_protect_verify(prot_bytes, flags):
+    import kvdata
+    d = kvdata.make_kv(150, 3 + prot_bytes, prot_bytes, *flags)
+    got = emu.kv_protect(d["base"], d["ko"], d["ks"], d["vo"], d["vs"], d["ops"], d["seqs"],
+                         d["cfs"])
+    assert (got == d["prot"]).all()
+    comp, ok, bad = emu.kv_verify(d["base"], d["ko"], d["ks"], d["vo"], d["vs"], prot_bytes,
+                                  d["co"], d["ops"], d["seqs"], d["cfs"])
+    assert bad == 0 and ok.all() and (comp == d["prot"]).all()
+    b2 = d["base"].copy()
+    b2[int(d["vo"][40]) + max(0, int(d["vs"][40]) - 1)] ^= 0x04  # value byte (or separator)
+    b2[int(d["co"][77])] ^= 0x80                                  # stored checksum
+    comp, ok, bad = emu.kv_verify(b2, d["ko"], d["ks"], d["vo"], d["vs"], prot_bytes, d["co"],
+                                  d["ops"], d["seqs"], d["cfs"])
+    want_bad = {77} | ({40} if int(d["vs"][40]) > 0 else set())
+    assert set(np.nonzero(ok == 0)[0].tolist()) == want_bad and bad == len(want_bad)

@@ -21,6 +21,7 @@ if not torch.cuda.is_available():
 from forst_amd import engine, workload  # noqa: E402
 from forst_amd.engine import ChecksumType as CT  # noqa: E402
 from oracle import oracle as O  # noqa: E402
+import stream  # noqa: E402,F401  (tests/golden on sys.path via conftest)
 
 DEV = "cuda"
 
@@ -336,3 +337,111 @@ def test_full_size_c2_properties():
     okh = host(ok)
     assert int(host(bad)[0]) == 64
     assert set(np.nonzero(okh == 0)[0].tolist()) == set(victims.tolist())
+
+
+# ---- a15: Hash64 (XXPH3) and per-KV protection (db/kv_checksum.h) ---------
+
+def test_hash64_golden(golden):
+    v, arr, base, offs, lens = golden
+    got0 = host(engine.hash64_batch(base, offs, lens)).view(np.uint64)
+    assert (got0 == np.array([r["hash64_s0"] for r in v["vectors"]], np.uint64)).all()
+    seeds = d(np.full(len(v["vectors"]), O.KV_SEED_V, np.uint64).view(np.int64))
+    got1 = host(engine.hash64_batch(base, offs, lens, seeds=seeds)).view(np.uint64)
+    assert (got1 == np.array([r["hash64_s1"] for r in v["vectors"]], np.uint64)).all()
+    got2 = host(engine.hash64_batch(base, offs, lens, seed=O.KV_SEED_V)).view(np.uint64)
+    assert (got2 == got1).all()
+
+
+def _kv_dev(kd):
+    def opt(a, dt):
+        return None if a is None else d(a.view(dt))
+    return dict(base=d(kd["base"]), ko=d(kd["ko"].view(np.int64)), ks=d(kd["ks"].view(np.int32)),
+                vo=d(kd["vo"].view(np.int64)), vs=d(kd["vs"].view(np.int32)),
+                co=d(kd["co"].view(np.int64)), ops=opt(kd["ops"], np.uint8),
+                seqs=opt(kd["seqs"], np.int64), cfs=opt(kd["cfs"], np.int32))
+
+
+@pytest.mark.parametrize("prot_bytes,flags", [(8, (True, True, False)), (1, (False, False, False)),
+                                              (4, (True, True, True)), (2, (True, False, True))])
+def test_kv_protect_and_verify(prot_bytes, flags):
+    import kvdata
+    kd = kvdata.make_kv(3000, 11 + prot_bytes, prot_bytes, *flags)
+    g = _kv_dev(kd)
+    prot = engine.kv_protect_batch(g["base"], g["ko"], g["ks"], g["vo"], g["vs"], g["ops"],
+                                   g["seqs"], g["cfs"])
+    assert (host(prot).view(np.uint64) == kd["prot"]).all()
+    comp, ok, bad = engine.kv_verify_batch(g["base"], g["ko"], g["ks"], g["vo"], g["vs"],
+                                           prot_bytes, g["co"], g["ops"], g["seqs"], g["cfs"])
+    assert int(host(bad)[0]) == 0 and host(ok).all()
+    # corrupt key, value and stored checksum bytes of chosen entries
+    b2 = kd["base"].copy()
+    rng = np.random.default_rng(prot_bytes)
+    victims = sorted(set(rng.integers(0, 3000, 30).tolist()))
+    hit = set()
+    for j, i in enumerate(victims):
+        spots = [int(kd["co"][i]) + j % prot_bytes]
+        if kd["ks"][i]:
+            spots.append(int(kd["ko"][i]) + (j * 31) % int(kd["ks"][i]))
+        if kd["vs"][i]:
+            spots.append(int(kd["vo"][i]) + (j * 7919) % int(kd["vs"][i]))
+        b2[spots[j % len(spots)]] ^= 1 << (j % 8)
+        hit.add(i)
+    comp, ok, bad = engine.kv_verify_batch(d(b2), g["ko"], g["ks"], g["vo"], g["vs"], prot_bytes,
+                                           g["co"], g["ops"], g["seqs"], g["cfs"])
+    failed = set(np.nonzero(host(ok) == 0)[0].tolist())
+    # a flipped bit in the 1-byte truncation can collide only if the hash byte
+    # happens to match; with distinct single-bit flips every victim must fail
+    assert failed == hit and int(host(bad)[0]) == len(hit)
+
+
+def test_kv_out_of_range_and_bad_args():
+    base = d(np.zeros(100, np.uint8))
+    o = d(np.array([0, 90, 10], np.int64))
+    s = d(np.array([10, 20, 5], np.int32))
+    c = d(np.array([50, 50, 99], np.int64))
+    comp, ok, bad = engine.kv_verify_batch(base, o, s, o, s, 4, c)
+    okh = host(ok)
+    assert okh[1] == 0 and okh[2] == 0 and int(host(bad)[0]) >= 2
+    from forst_amd import ForstError
+    with pytest.raises(ForstError):
+        engine.kv_verify_batch(base, o, s, o, s, 3, c)
+
+
+def test_kv_full_size_roundtrip():
+    """1 M memtable-shaped entries (16-64 B keys, 0-1000 B values, 8-byte
+    protection): write side computes, read side verifies, a 2000-entry sample
+    against the oracle, 50 injected flips detected exactly."""
+    n = 1 << 20
+    rng = np.random.default_rng(99)
+    ks = rng.integers(16, 65, n).astype(np.int64)
+    vs = rng.integers(0, 1001, n).astype(np.int64)
+    ko = np.zeros(n, np.int64)
+    ko[1:] = np.cumsum(ks[:-1] + vs[:-1] + 8)
+    vo = ko + ks
+    co = vo + vs
+    total = int(co[-1]) + 8
+    alloc = (total + 255) // 256 * 256
+    base = torch.empty(alloc, dtype=torch.uint8, device=DEV)
+    engine.fill_stream(base, 0, 0xF0E57000A15)
+    dko, dks, dvo, dvs = d(ko), d(ks.astype(np.int32)), d(vo), d(vs.astype(np.int32))
+    ops = d(rng.integers(0, 26, n).astype(np.uint8))
+    seqs = d(rng.integers(0, 2**62, n).astype(np.int64))
+    prot = engine.kv_protect_batch(base, dko, dks, dvo, dvs, ops, seqs)
+    # Encode(8): LE bytes at co
+    pb = prot.view(torch.uint8).view(n, 8)
+    idx = d(co)[:, None] + torch.arange(8, device=DEV)[None, :]
+    base[idx.reshape(-1)] = pb.reshape(-1)
+    comp, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, 8, d(co), ops, seqs)
+    assert int(host(bad)[0]) == 0
+    hb = host(base)
+    hp = host(prot).view(np.uint64)
+    hops, hseq = host(ops), host(seqs).view(np.uint64)
+    for i in rng.choice(n, 2000, replace=False):
+        want = O.kv_protect(hb[ko[i]:ko[i] + ks[i]], hb[vo[i]:vo[i] + vs[i]], int(hops[i]),
+                            seq=int(hseq[i]))
+        assert int(hp[i]) == want
+    victims = rng.choice(n, 50, replace=False)
+    base[d(ko[victims] + 3)] ^= 0x20
+    _, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, 8, d(co), ops, seqs)
+    assert int(host(bad)[0]) == 50
+    assert set(np.nonzero(host(ok) == 0)[0].tolist()) == set(victims.tolist())

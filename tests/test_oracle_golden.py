@@ -167,3 +167,54 @@ def test_stream_matches_oracle_fill():
         a = stream.stream(0x1234, start, n)
         b = O.fill_stream(start, n, 0x1234)
         assert (a == b).all()
+
+
+# ---- a15: Hash64 (XXPH3 0.7.2 preview) and per-KV protection ---------------
+
+def test_hash64_kats(kats):
+    # util/hash_test.cc:162-232 Hash64(s, n, 0)
+    for hexs, want in kats["hash_test"]:
+        assert O.hash64(bytes.fromhex(hexs), 0) == want, hexs
+
+
+def test_hash64_reference_vectors(ref_vectors):
+    # every length class (0-16, 17-128, 129-240, long with/without a last
+    # stripe, multiples of 1024) for seed 0 and seed kSeedV, by the reference
+    v, blob = ref_vectors
+    arr = np.frombuffer(blob, dtype=np.uint8)
+    for r in v["vectors"]:
+        d = arr[r["off"]:r["off"] + r["n"]]
+        assert O.hash64(d, 0) == r["hash64_s0"], r["n"]
+        assert O.hash64(d, O.KV_SEED_V) == r["hash64_s1"], r["n"]
+
+
+def test_kv_field_hashes_reference(ref_vectors):
+    # NPHash64 of op type / sequence / column family with their seeds
+    # (db/kv_checksum.h:84-88, :296-460), values from the reference's Hash64
+    kv = ref_vectors[0]["kv_fields"]
+    for op, want in kv["op"]:
+        assert O.hash64(bytes([op]), O.KV_SEED_O) == want
+    for seq, want in kv["seq"]:
+        assert O.hash64(seq.to_bytes(8, "little"), O.KV_SEED_S) == want
+    for cf, want in kv["cf"]:
+        assert O.hash64(cf.to_bytes(4, "little"), O.KV_SEED_C) == want
+
+
+def test_kv_protect_composition(ref_vectors):
+    # ProtectKVO(k, v, op).ProtectS(seq).ProtectC(cf) == XOR of the field
+    # hashes (kv_checksum.h:296-307, :420-460); XOR is an involution, so
+    # Strip == Protect (kv_checksum.h:391-470)
+    v, blob = ref_vectors
+    arr = np.frombuffer(blob, dtype=np.uint8)
+    kv = v["kv_fields"]
+    for t, r in enumerate(v["vectors"][:120]):
+        key = arr[r["off"]:r["off"] + min(r["n"], 40)]
+        val = arr[r["off"]:r["off"] + r["n"]]
+        op, hop = kv["op"][t % len(kv["op"])]
+        seq, hseq = kv["seq"][t % len(kv["seq"])]
+        cf, hcf = kv["cf"][t % len(kv["cf"])]
+        hk = O.hash64(key, 0)
+        assert O.kv_protect(key, val) == hk ^ r["hash64_s1"]
+        assert O.kv_protect(key, val, op) == hk ^ r["hash64_s1"] ^ hop
+        assert O.kv_protect(key, val, op, seq=seq) == hk ^ r["hash64_s1"] ^ hop ^ hseq
+        assert O.kv_protect(key, val, op, seq=seq, cf=cf) == hk ^ r["hash64_s1"] ^ hop ^ hseq ^ hcf

@@ -512,6 +512,281 @@ __global__ void __launch_bounds__(kThreads) xxh3_stream_kernel(BlockArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// XXH3 v2 ("rows"): four messages per wave, one per 16-lane row.
+//
+// In the one-message-per-wave layout every 16 bytes of input cost a 4-level
+// cross-lane stripe sum (two DPP row rotations + permlane16/32 swaps) for each
+// of two 64-bit accumulators -- about three times the hash arithmetic itself.
+// Here row r (lanes 16r..16r+15) owns a message; lane t = 4 s4 + p of the row
+// takes stripes s4, s4+4, s4+8, s4+12 (accumulator pair p) of each 1 KiB
+// XXH3-block: four global_load_dwordx4 per lane, each instruction reading 256
+// contiguous bytes per row.  The four stripes are summed in registers and the
+// row reduction is two DPP row rotations.  One step = one XXH3-block per row
+// (4 KiB per wave), with the next step's loads (data, last stripe, trailer
+// dwords, modifier / type byte) in flight while the current one computes.
+// Rows draw messages dynamically from the wave's contiguous share (a row that
+// finishes takes the next unassigned message), so mixed 4/16/64 KiB batches
+// stay balanced.  Descriptors come in 64-message batches held one per lane and
+// are fetched by the rows with ds_bpermute.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kNoMsg = 0xffffffffu;
+
+// a row's position: message (relative to the wave share) and XXH3-block;
+// row-uniform values, one copy per lane
+struct RowPos {
+  uint32_t off_lo, off_hi, size;
+  uint32_t rel;  // message index - kbeg, kNoMsg when the share is exhausted
+  uint32_t g;    // XXH3-block index
+};
+
+__device__ __forceinline__ uint64_t rp_off(const RowPos& p) {
+  return (static_cast<uint64_t>(p.off_hi) << 32) | p.off_lo;
+}
+
+template <int MODE>
+__device__ __forceinline__ bool rp_valid(const BlockArgs& a, const RowPos& p) {
+  if (p.rel == kNoMsg) return false;
+  const Desc d{rp_off(p), p.size, 0, 0};
+  return desc_in_range<MODE>(a, d);
+}
+
+struct RStep {
+  uint32_t x[4][5];  // 4 stripes x (16 bytes + the next dword)
+  uint32_t l[5];     // last stripe piece
+  uint32_t t0, t1;   // type byte / stored checksum dwords
+  uint32_t mod, extra;
+};
+
+template <int MODE>
+__device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, const RowPos& P,
+                                           uint64_t kbeg, RStep& d) {
+  const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
+  const uint64_t off = rp_off(P);
+  const bool valid = rp_valid<MODE>(a, P);
+  const bool lng = valid && P.size > 240;
+  const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
+  const uint32_t m = static_cast<uint32_t>(off & 3);
+  const uint64_t q0 = (off & ~3ull) + 1024ull * P.g + 64 * s4 + 16 * p;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
+    const uint64_t o = need ? q0 + 256 * k : 0;
+    const u32x4a4 v = ld16_a4(a.base + o);
+    d.x[k][0] = v.x;
+    d.x[k][1] = v.y;
+    d.x[k][2] = v.z;
+    d.x[k][3] = v.w;
+    // the dword after the piece only matters for unaligned starts; then it
+    // holds a message byte, so it never crosses into an unmapped page
+    d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
+  }
+  const bool lastp = lng && P.g == nb;
+  const uint64_t lq = off + P.size - 64 + 16 * p;
+  const uint32_t ml = static_cast<uint32_t>(lq & 3);
+  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+  const u32x4a4 v = ld16_a4(a.base + lo);
+  d.l[0] = v.x;
+  d.l[1] = v.y;
+  d.l[2] = v.z;
+  d.l[3] = v.w;
+  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+  // type byte at E = off + size, stored LE32 at E + 1 (verify); for compute /
+  // trailer without last_bytes[] only the type byte
+  const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
+  const uint64_t E = off + P.size;
+  const uint64_t t0 = (lastp && mem_last) ? (E & ~3ull) : 0;
+  d.t0 = ld4v(a.base + t0);
+  d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastp ? t0 + 4 : 0)) : 0u;
+  const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
+  d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
+  d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
+                                                                              : 0u;
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
+  __shared__ uint64_t cold[4 * kColdN];
+  if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
+  const uint64_t* ck = cold + kColdN * p;
+  // accumulate keys of the lane's four stripes, scramble keys of its pair
+  uint64_t K0[4], K1[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    K0[k] = sec64(8 * (s4 + 4 * k) + 16 * p);
+    K1[k] = sec64(8 * (s4 + 4 * k) + 16 * p + 8);
+  }
+  const uint64_t ks0 = sec64(128 + 16 * p), ks1 = sec64(136 + 16 * p);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  uint64_t kbeg, kend;
+  wave_share(a.n, nw, gw, kbeg, kend);
+  if (kbeg >= kend) return;
+  const uint64_t cnt = kend - kbeg;
+
+  // descriptor batches: lane j <-> message kbrel + j (cb), kbrel + 64 + j (nb)
+  DescBatch cb, nb;
+  uint64_t kbrel = 0;
+  load_batch<MODE>(a, kbeg, kend, lane, cb);
+  load_batch<MODE>(a, kbeg + kBatch, kend, lane, nb);
+  auto fetch = [&](uint32_t rel, RowPos& P) {
+    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
+    const int src = static_cast<int>(j & 63u);
+    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
+    const uint32_t sz_c = __shfl(cb.size, src);
+    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
+    const uint32_t sz_n = __shfl(nb.size, src);
+    const bool in_n = j >= 64;
+    P.off_lo = in_n ? lo_n : lo_c;
+    P.off_hi = in_n ? hi_n : hi_c;
+    P.size = in_n ? sz_n : sz_c;
+    P.rel = rel;
+    P.g = 0;
+  };
+  // rows start on messages 0..3 of the share
+  const uint32_t row = lane >> 4;
+  uint64_t next = 4;
+  RowPos C;
+  fetch(row, C);
+  if (row >= cnt) C.rel = kNoMsg;
+
+  // I = the position after P: next XXH3-block, or a newly assigned message
+  auto advance = [&](const RowPos& P, RowPos& I) {
+    const bool lng = rp_valid<MODE>(a, P) && P.size > 240;
+    const uint32_t nbP = (P.size - 1) >> 10;
+    const bool more = lng && P.g < nbP;
+    const bool need = P.rel != kNoMsg && !more;
+    const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
+    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+    const uint64_t nrel = next + rank;
+    RowPos F;
+    fetch(static_cast<uint32_t>(nrel), F);
+    if (nrel >= cnt) F.rel = kNoMsg;
+    next += static_cast<uint64_t>(__popcll(rows));
+    I = P;
+    if (more) I.g = P.g + 1;
+    if (need) I = F;
+    if (next >= kbrel + 2 * kBatch - 4 || next >= kbrel + kBatch) {
+      // every message of cb has been assigned: slide the batches
+      if (next >= kbrel + kBatch) {
+        kbrel += kBatch;
+        cb = nb;
+        load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
+      }
+    }
+  };
+
+  RowPos I;
+  advance(C, I);
+  RStep X, Y;
+  rows_issue<MODE>(a, lane, C, kbeg, X);
+  uint64_t acc0 = 0, acc1 = 0;
+  const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
+
+  auto step = [&](RStep& cu, RStep& nx) -> bool {
+    if (__ballot(C.rel != kNoMsg) == 0) return false;
+    rows_issue<MODE>(a, lane, I, kbeg, nx);
+    const uint64_t off = rp_off(C);
+    const bool valid = rp_valid<MODE>(a, C);
+    const bool lng = valid && C.size > 240;
+    const uint32_t nbC = (C.size - 1) >> 10, nbSC = ((C.size - 1) & 1023) >> 6;
+    const uint32_t m = static_cast<uint32_t>(off & 3);
+    // ---- one XXH3-block of every row (xxhash.h:5123-5140) ----
+    if (C.g == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
+      acc0 = ck[kColdI0];
+      acc1 = ck[kColdI1];
+    }
+    uint64_t sum0 = 0, sum1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      uint64_t d0, d1;
+      xx_words(cu.x[k], m, d0, d1);
+      const uint64_t c0 = mul32to64(d0 ^ K0[k]) + d1;  // acc[2p]   (xxhash.h:4926-4927)
+      const uint64_t c1 = d0 + mul32to64(d1 ^ K1[k]);  // acc[2p+1]
+      const bool use = C.g < nbC || s4 + 4 * k < nbSC;
+      sum0 += use ? c0 : 0ull;
+      sum1 += use ? c1 : 0ull;
+    }
+    sum0 += row_ror64<4>(sum0);  // the row's four stripe groups
+    sum1 += row_ror64<4>(sum1);
+    sum0 += row_ror64<8>(sum0);
+    sum1 += row_ror64<8>(sum1);
+    acc0 += sum0;
+    acc1 += sum1;
+    const bool full = C.g < nbC;
+    if (full) {  // xxhash.h:5126-5128
+      acc0 = scramble(acc0, ks0);
+      acc1 = scramble(acc1, ks1);
+    }
+    // ---- rows that finish a message in this step ----
+    const bool fin = C.rel != kNoMsg && !(lng && full);
+    if (__ballot(fin)) {
+      uint64_t h = 0;
+      {  // last stripe at len - 64, merge (xxhash.h:5146-5208)
+        uint64_t d0, d1;
+        const uint32_t ml = static_cast<uint32_t>((off + C.size) & 3);
+        xx_words(cu.l, ml, d0, d1);
+        const uint64_t a0 = acc0 + mul32to64(d0 ^ ck[kColdL0]) + d1;
+        const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ ck[kColdL1]);
+        uint64_t tm = mul128_fold64(a0 ^ ck[kColdM0], a1 ^ ck[kColdM1]);
+        tm += shfl_xor64(tm, 1);
+        tm += shfl_xor64(tm, 2);
+        h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
+      }
+      const uint64_t E = off + C.size;
+      const uint32_t tb = static_cast<uint32_t>(E & 3);
+      uint32_t lastb = (cu.t0 >> (8 * tb)) & 0xffu;
+      uint32_t stored = MODE == kModeVerify
+                            ? (tb == 3 ? cu.t1 : __builtin_amdgcn_alignbyte(cu.t1, cu.t0, tb + 1))
+                            : 0u;
+      if (fin && valid && !lng) {  // short input: the length-class formulas
+        const uint8_t* pp = a.base + off;
+        const uint64_t hs = xxh3_short(pp, C.size);
+        h = mk64(retire(static_cast<uint32_t>(hs)), retire(static_cast<uint32_t>(hs >> 32)));
+        if (MODE != kModeRaw) lastb = retire(ldu8(pp + C.size));
+        if (MODE == kModeVerify) stored = retire(ldu32(pp + C.size + 1));
+      }
+      if (has_extra) lastb = cu.extra;
+      const uint64_t i = kbeg + (C.rel == kNoMsg ? 0 : C.rel);
+      const bool mine = fin && t == 0;
+      bool ok = valid;
+      if (MODE == kModeRaw) {
+        if (mine && a.out64) a.out64[i] = valid ? h : 0ull;
+      } else if (MODE == kModeVerify) {
+        // ComputeBuiltinChecksum(kXXH3, data, size+1), format.cc:577-586
+        const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), lastb);
+        const uint32_t st = stored - cu.mod;
+        ok = valid && st == computed;
+        if (mine && a.out32) a.out32[i] = valid ? computed : 0u;
+        if (mine && a.stored_out) a.stored_out[i] = valid ? st : 0u;
+        if (mine && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+      } else {
+        const uint32_t out = modify_for_last_byte(static_cast<uint32_t>(h), lastb) + cu.mod;
+        if (mine && a.out32) a.out32[i] = valid ? out : 0u;
+        if (MODE == kModeTrailer && mine && valid) {
+          uint8_t* w = a.base_w + off + C.size;
+          w[0] = static_cast<uint8_t>(lastb);
+          stu32_bytes(w + 1, out);
+        }
+      }
+      if (MODE == kModeVerify) {
+        const uint64_t badm = __ballot(mine && !ok);
+        if (a.mismatches && badm && lane == 0)
+          atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
+      }
+    }
+    C = I;
+    advance(C, I);
+    return true;
+  };
+  while (step(X, Y) && step(Y, X)) {
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) xxh3_block_kernel_simple(BlockArgs a) {
   const uint32_t lane = threadIdx.x & 63;
@@ -617,6 +892,19 @@ uint32_t stream_occupancy() {
   return occ;
 }
 
+template <int MODE>
+uint32_t rows_occupancy() {
+  static const uint32_t occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_rows_kernel<MODE>, kThreads, 0) !=
+            hipSuccess ||
+        o < 1)
+      o = 1;
+    return static_cast<uint32_t>(o);
+  }();
+  return occ;
+}
+
 }  // namespace
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
@@ -631,6 +919,7 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   const char* variant = std::getenv("FORST_XXH3_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < 4096;
   const bool probe = variant && std::string(variant) == "probe_load" && mode == kModeVerify;
+  const bool v1 = variant && std::string(variant) == "v1";
 #define FORST_LAUNCH_XXH3(M, TAG)                                                          \
   do {                                                                                     \
     if (simple) {                                                                          \
@@ -643,11 +932,17 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
           1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));     \
       hipLaunchKernelGGL((xxh3_stream_kernel<kModeVerify, 1>), dim3(sg), dim3(kThreads), 0, \
                          stream, a);                                                       \
-    } else {                                                                               \
+    } else if (v1) {                                                                       \
       *name = "xxh3_stream_kernel<" TAG ">";                                               \
       const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
           1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));     \
       hipLaunchKernelGGL(xxh3_stream_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, a);   \
+    } else {                                                                               \
+      *name = "xxh3_rows_kernel<" TAG ">";                                                 \
+      const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
+          1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),                     \
+                                uint64_t(di.num_cus) * rows_occupancy<M>())));             \
+      hipLaunchKernelGGL(xxh3_rows_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, a);     \
     }                                                                                      \
   } while (0)
   switch (mode) {

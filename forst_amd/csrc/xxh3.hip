@@ -670,13 +670,10 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
     I = P;
     if (more) I.g = P.g + 1;
     if (need) I = F;
-    if (next >= kbrel + 2 * kBatch - 4 || next >= kbrel + kBatch) {
-      // every message of cb has been assigned: slide the batches
-      if (next >= kbrel + kBatch) {
-        kbrel += kBatch;
-        cb = nb;
-        load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
-      }
+    if (next >= kbrel + kBatch) {  // every message of cb is assigned: slide the batches
+      kbrel += kBatch;
+      cb = nb;
+      load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
     }
   };
 

@@ -1094,6 +1094,330 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// CRC32C rows kernel (v3): one block per 16-lane row.
+//
+// In the one-block-per-wave kernels every block pays a full-wave finish
+// (row-end shifts, DPP reduction, round-end shifts, tail step), a head set-up
+// and a scalar block set-up; for 4 KiB blocks that is a third of the work.
+// Here row r (lanes 16r..16r+15) owns a block and walks it in 1 KiB rounds:
+// chain c (0, 1) of lane t owns the 32-byte segment [512c + 32t, +32) of
+// every round, the hop to the next round is J3 = shift by 1024 - 32 + 4 bytes
+// fused with the first dword step.  The four rows finish their blocks with
+// ONE instruction stream: A[15 - t] moves each chain state to the end of the
+// row, a 4-level DPP XOR reduces the row, B[1] (shift by 512) joins chain 0 to
+// chain 1, and one k-byte slicing step adds the <= 3 tail bytes and the type
+// byte.  Rows draw blocks dynamically from the wave's contiguous share (as in
+// xxh3_rows_kernel); the head of a block is handled in round 0 of its row by
+// zeroing the words in front of the message and injecting S0 into the head
+// word, with rows at round 0 and rows in the middle of a block running the
+// same code (J3(0) = 0).
+//
+// LDS: [0, 64K) G and J3 interleaved as in the v2 kernel, [64K, 124K) A[1..15],
+// [124K, 128K) B[1].
+// ---------------------------------------------------------------------------
+constexpr uint32_t kRowRound = 1024;
+constexpr uint32_t kRowChain = 512;
+constexpr uint32_t kLds3Bytes = kOffB2 + 4096;
+constexpr uint32_t kNoBlk = 0xffffffffu;
+
+__device__ __forceinline__ void fill_tables3(uint32_t* L) {
+  const uint32_t tid = threadIdx.x;
+  for (uint32_t i = tid; i < 16384; i += kThreads) {
+    const uint32_t e = i >> 6, d = i & 63, t = (d >> 3) & 3;
+    L[i] = d < 32 ? kCrcG[t * 256 + e] : kCrcJ3[t * 256 + e];
+  }
+  for (uint32_t i = tid; i < 15 * 1024; i += kThreads) L[kOffA2 / 4 + i] = kCrcA[i];
+  for (uint32_t i = tid; i < 1024; i += kThreads) L[kOffB2 / 4 + i] = kCrcB[i];
+  __syncthreads();
+}
+
+// a row's position (block of the wave share, 1 KiB round) and the block's
+// window, derived once when the block is assigned; row-uniform, one copy per
+// lane
+struct CRowPos {
+  uint32_t off_lo, off_hi, size, rel, g;
+  uint32_t w0_lo, w0_hi;  // round-0 window start (int64, may be < 0)
+  uint32_t R;             // rounds
+  uint32_t pk;            // cA:1 tA:4 jA:3 q:3 nt:2 m:2 valid:1 slow:1
+  __device__ __forceinline__ uint64_t off() const {
+    return (static_cast<uint64_t>(off_hi) << 32) | off_lo;
+  }
+  __device__ __forceinline__ int64_t w0() const {
+    return static_cast<int64_t>((static_cast<uint64_t>(w0_hi) << 32) | w0_lo);
+  }
+  __device__ __forceinline__ uint32_t cA() const { return pk & 1u; }
+  __device__ __forceinline__ uint32_t tA() const { return (pk >> 1) & 15u; }
+  __device__ __forceinline__ uint32_t jA() const { return (pk >> 5) & 7u; }
+  __device__ __forceinline__ uint32_t q() const { return (pk >> 8) & 7u; }
+  __device__ __forceinline__ uint32_t nt() const { return (pk >> 11) & 3u; }
+  __device__ __forceinline__ uint32_t m() const { return (pk >> 13) & 3u; }
+  __device__ __forceinline__ bool valid() const { return (pk >> 15) & 1u; }
+  __device__ __forceinline__ bool slow() const { return (pk >> 16) & 1u; }
+};
+
+template <int MODE>
+__device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
+  const uint64_t off = P.off();
+  const bool valid = P.rel != kNoBlk && desc_in_range<MODE>(a, Desc{off, P.size, 0, 0});
+  const uint64_t E = off + P.size + (mem_last_byte<MODE>(a) ? 1u : 0u);
+  const uint64_t ws = off & ~3ull;
+  const uint64_t we = E & ~3ull;
+  const uint64_t d4 = we - ws;
+  uint32_t R = static_cast<uint32_t>((d4 + kRowRound - 1) / kRowRound);
+  int64_t w0 = static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRowRound;
+  const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - w0);
+  const uint32_t cA = hA >> 9, tA = (hA >> 5) & 15u, jA = (hA >> 2) & 7u;
+  const int64_t seg_head = static_cast<int64_t>(ws) - 4 * static_cast<int64_t>(jA);
+  const uint32_t q = seg_head < 0 ? static_cast<uint32_t>(-seg_head) >> 2 : 0u;
+  const uint32_t nt = static_cast<uint32_t>(E - we);
+  const uint32_t m = static_cast<uint32_t>(off & 3);
+  const bool slow = !valid || d4 < 64;
+  if (slow) {  // the slow path loads on its own; dummy round loads at [0, 1 KiB)
+    R = 1;
+    w0 = 0;
+  }
+  P.R = R;
+  P.w0_lo = static_cast<uint32_t>(w0);
+  P.w0_hi = static_cast<uint32_t>(static_cast<uint64_t>(w0) >> 32);
+  P.pk = (slow ? 0u : (cA | (tA << 1) | (jA << 5) | (q << 8))) | (nt << 11) | (m << 13) |
+         (valid ? 1u << 15 : 0u) | (slow ? 1u << 16 : 0u);
+}
+
+struct CRStep {
+  uint32_t w[2][8];
+  uint32_t t0, t1, mod, extra;
+};
+
+template <int MODE>
+__device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, const CRowPos& P,
+                                           uint64_t kbeg, CRStep& d) {
+  const uint32_t t = lane & 15;
+  const int64_t w0 = P.w0();
+  const uint32_t cA = P.cA(), tA = P.tA();
+#pragma unroll
+  for (uint32_t c = 0; c < 2; ++c) {
+    int64_t so = w0 + static_cast<int64_t>(P.g) * kRowRound + kRowChain * c + kSeg2 * t;
+    // round 0: segments in front of the head hold no message byte (their
+    // words are zeroed), a head segment in front of the buffer is loaded
+    // from 0 and realigned
+    const bool pre = P.g == 0 && (c < cA || (c == cA && t < tA));
+    so = (pre || so < 0) ? 0 : so;
+    const uint8_t* sp = a.base + so;
+#pragma unroll
+    for (int q = 0; q < 2; ++q) {
+      const u32x4a4 v = ld16_a4(sp + 16 * q);
+      d.w[c][4 * q + 0] = v.x;
+      d.w[c][4 * q + 1] = v.y;
+      d.w[c][4 * q + 2] = v.z;
+      d.w[c][4 * q + 3] = v.w;
+    }
+  }
+  // tail dword at the window end (last round of a fast block only)
+  const uint32_t nt = P.nt();
+  const bool lastr = !P.slow() && P.g + 1 >= P.R;
+  const uint64_t we = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
+  const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
+  d.t0 = ld4v(a.base + t0);
+  d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastr && nt ? t0 + 4 : t0)) : 0u;
+  const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
+  d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
+  d.extra = MODE == kModeRaw ? (a.init_crcs ? a.init_crcs[idx] : 0u)
+                             : (a.last_bytes ? a.last_bytes[idx] : 0u);
+}
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
+  __shared__ uint32_t L[kLds3Bytes / 4];
+  fill_tables3(L);
+  const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t t = lane & 15;
+  const Lanes2 K = lanes2(lane);
+  const uint32_t s0c[4] = {uniform(kCrcS0[0]), uniform(kCrcS0[1]), uniform(kCrcS0[2]),
+                           uniform(kCrcS0[3])};
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  uint64_t kbeg, kend;
+  wave_share(a.n, nw, gw, kbeg, kend);
+  if (kbeg >= kend) return;
+  const uint64_t cnt = kend - kbeg;
+  const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
+
+  DescBatch cb, nb;
+  uint64_t kbrel = 0;
+  load_batch<MODE>(a, kbeg, kend, lane, cb);
+  load_batch<MODE>(a, kbeg + kBatch, kend, lane, nb);
+  auto fetch = [&](uint64_t rel, CRowPos& P) {
+    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
+    const int src = static_cast<int>(j & 63u);
+    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
+    const uint32_t sz_c = __shfl(cb.size, src);
+    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
+    const uint32_t sz_n = __shfl(nb.size, src);
+    const bool in_n = j >= 64;
+    P.off_lo = in_n ? lo_n : lo_c;
+    P.off_hi = in_n ? hi_n : hi_c;
+    P.size = in_n ? sz_n : sz_c;
+    P.rel = rel < cnt ? static_cast<uint32_t>(rel) : kNoBlk;
+    P.g = 0;
+    crow_derive<MODE>(a, P);
+  };
+  uint64_t next = 4;
+  CRowPos C;
+  fetch(lane >> 4, C);
+  auto advance = [&](const CRowPos& P, CRowPos& I) {
+    const bool more = P.rel != kNoBlk && !P.slow() && P.g + 1 < P.R;
+    const bool need = P.rel != kNoBlk && !more;
+    const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
+    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+    CRowPos F;
+    fetch(next + rank, F);
+    next += static_cast<uint64_t>(__popcll(rows));
+    I = P;
+    if (more) I.g = P.g + 1;
+    if (need) I = F;
+    if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
+      kbrel += kBatch;
+      cb = nb;
+      load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
+    }
+  };
+  CRowPos I;
+  advance(C, I);
+  CRStep X, Y;
+  crow_issue<MODE>(a, lane, C, kbeg, X);
+  uint32_t s[2] = {0, 0};
+
+  auto step = [&](CRStep& cu, CRStep& nx) -> bool {
+    if (__ballot(C.rel != kNoBlk) == 0) return false;
+    crow_issue<MODE>(a, lane, I, kbeg, nx);
+    const bool fast = C.rel != kNoBlk && !C.slow();
+    const bool r0 = C.g == 0;
+    // ---- one 1 KiB round of every row ----
+    uint32_t w[2][8];
+#pragma unroll
+    for (int c = 0; c < 2; ++c)
+#pragma unroll
+      for (int j = 0; j < 8; ++j) w[c][j] = cu.w[c][j];
+    if (__ballot(fast && r0)) {  // some row starts a block: its head
+      const uint32_t cA = C.cA(), tA = C.tA(), jA = C.jA(), q = C.q(), m = C.m();
+      const uint32_t bm = 0xffffffffu << (8 * m);
+      const uint32_t S0 = MODE == kModeRaw ? unstep_m(~cu.extra, m)
+                                           : (m == 0 ? s0c[0] : m == 1 ? s0c[1] : m == 2 ? s0c[2] : s0c[3]);
+#pragma unroll
+      for (uint32_t c = 0; c < 2; ++c) {
+        const bool hl = fast && r0 && c == cA && t == tA;  // the head lane of the row
+        if (__ballot(hl && q != 0)) {  // head segment loaded from 0: shift up q dwords
+          uint32_t sh[8];
+#pragma unroll
+          for (int j = 0; j < 8; ++j) {
+            uint32_t v = 0;
+#pragma unroll
+            for (int qq = 1; qq < 8; ++qq)
+              if (qq <= j) v = (q == static_cast<uint32_t>(qq)) ? w[c][j - qq] : v;
+            sh[j] = v;
+          }
+#pragma unroll
+          for (int j = 0; j < 8; ++j) w[c][j] = (hl && q != 0) ? sh[j] : w[c][j];
+        }
+        const uint32_t js = !(fast && r0) ? 0u
+                            : (c < cA || (c == cA && t < tA)) ? 8u
+                            : hl ? jA
+                                 : 0u;
+#pragma unroll
+        for (uint32_t j = 0; j < 8; ++j) {
+          uint32_t v = j < js ? 0u : w[c][j];
+          v = (hl && j == jA) ? ((v & bm) ^ S0) : v;
+          w[c][j] = v;
+        }
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < 2; ++c) {
+      uint32_t lj[4], lg[4];
+      rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);  // J3(0) = 0: a row at round 0 starts fresh
+      rep_look<false>(Lb, K, w[c][0], lg);
+      uint32_t x = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]),
+                        xor3(lg[2], lg[3], w[c][1]));
+#pragma unroll
+      for (int j = 2; j < 8; ++j) x = g_then(Lb, K, x, w[c][j]);
+      s[c] = g_then(Lb, K, x, 0u);
+    }
+    // ---- rows that finish a block in this step ----
+    const bool fin = C.rel != kNoBlk && (C.slow() || C.g + 1 >= C.R);
+    if (__ballot(fin)) {
+      // chain states to the row end (A[15 - t]), row XOR, chain 0 over chain 1
+      const bool lo0 = t == 15;
+      const uint32_t abase = kOffA2 + 4096 * (14 - t);
+      uint32_t a0 = lo0 ? s[0] : shift_at(Lb, abase, s[0]);
+      uint32_t a1 = lo0 ? s[1] : shift_at(Lb, abase, s[1]);
+      a0 = row_shr_xor<1>(a0);
+      a1 = row_shr_xor<1>(a1);
+      a0 = row_shr_xor<2>(a0);
+      a1 = row_shr_xor<2>(a1);
+      a0 = row_shr_xor<4>(a0);
+      a1 = row_shr_xor<4>(a1);
+      a0 = row_shr_xor<8>(a0);
+      a1 = row_shr_xor<8>(a1);
+      uint32_t crc = 0, stored = 0;
+      const uint32_t nt = C.nt();
+      if (fin && lo0) {
+        const uint32_t st = shift_at(Lb, kOffB2, a0) ^ a1;
+        uint32_t y = nt ? (cu.t0 & (0xffffffffu >> (32 - 8 * nt))) : 0u;
+        uint32_t k = nt;
+        if (has_extra) {
+          y |= (cu.extra & 0xffu) << (8 * k);
+          ++k;
+        }
+        crc = ~step_k(Lb, K, st, y, k);
+        if (MODE == kModeVerify) stored = nt ? __builtin_amdgcn_alignbyte(cu.t1, cu.t0, nt) : cu.t0;
+      }
+      if (fin && lo0 && C.slow() && C.valid()) {
+        const uint8_t* pp = a.base + C.off();
+        const uint32_t init = MODE == kModeRaw ? cu.extra : 0u;
+        crc = small_crc2(Lb, K, pp, C.size + (mem_last_byte<MODE>(a) ? 1u : 0u), init,
+                         has_extra ? 1u : 0u, cu.extra);
+        if (MODE == kModeVerify) stored = retire(ldu32(pp + C.size + 1));
+        crc = retire(crc);
+      }
+      const bool valid = C.valid();
+      const bool mine = fin && lo0;
+      const uint64_t i = kbeg + (C.rel == kNoBlk ? 0 : C.rel);
+      bool ok = valid;
+      if (MODE == kModeRaw) {
+        if (mine && a.out32) a.out32[i] = valid ? crc : 0u;
+      } else if (MODE == kModeVerify) {
+        const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
+        const uint32_t st = stored - cu.mod;
+        ok = valid && st == computed;
+        if (mine && a.out32) a.out32[i] = valid ? computed : 0u;
+        if (mine && a.stored_out) a.stored_out[i] = valid ? st : 0u;
+        if (mine && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+      } else {
+        const uint32_t out = crc_mask(crc) + cu.mod;  // format.cc:594-600 + builder.cc:1340-1345
+        if (mine && a.out32) a.out32[i] = valid ? out : 0u;
+        if (MODE == kModeTrailer && mine && valid) {
+          uint8_t* pw = a.base_w + C.off() + C.size;
+          if (a.last_bytes) pw[0] = static_cast<uint8_t>(cu.extra);
+          stu32_bytes(pw + 1, out);
+        }
+      }
+      if (MODE == kModeVerify) {
+        const uint64_t badm = __ballot(mine && !ok);
+        if (a.mismatches && badm && lane == 0)
+          atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
+      }
+    }
+    C = I;
+    advance(C, I);
+    return true;
+  };
+  while (step(X, Y) && step(Y, X)) {
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kThreads)
     crc32c_block_kernel_simple(BlockArgs a) {
@@ -1184,6 +1508,12 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   const char* variant = std::getenv("FORST_CRC_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < kRB;
   const bool v1 = variant && std::string(variant) == "v1";
+  // default: the rows kernel (one block per 16-lane row) for small blocks,
+  // where the per-block finish dominates; the v2 kernel (two 4 KiB steps in
+  // flight per wave) otherwise.  Mean block size from the launch arguments.
+  const bool small_blocks = a.base_len / a.n <= 6144;
+  const bool rows = (variant && std::string(variant) == "rows") ||
+                    ((!variant || !*variant) && small_blocks);
   // diagnostics: probe_load (loads only), probe_rounds (no finish),
   // probe_nohead (no round-0 head handling); results are not checksums
   const int probe = !variant ? 0
@@ -1197,6 +1527,9 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
       *name = "crc32c_block_kernel_simple<" TAG ">";                                      \
       hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,    \
                          stream, a);                                                      \
+    } else if (rows) {                                                                    \
+      *name = "crc32c_rows_kernel<" TAG ">";                                              \
+      hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, a); \
     } else if (v1) {                                                                      \
       *name = "crc32c_stream_kernel<" TAG ">";                                            \
       hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \

@@ -147,6 +147,67 @@ def run_config(name, steps, warmup, rank, world, seed_base=None):
     return res
 
 
+def run_wal(steps, warmup, n_records=10_000_000):
+    """C5 WAL replay: 10 M logical records log-uniform in
+    [32, 32768] B framed by log::Writer's rules; writer-side record CRC pass
+    (log_writer.cc EmitPhysicalRecord) + reader-side verify of every physical
+    record CRC (log_reader.cc ReadPhysicalRecord).  Algorithmic bytes:
+    verify  = whole log read + per log block status/nrec/fail_off (9 B);
+    writer  = headers+payloads read + offset (8) + CRC written twice (in place
+              and out, 4+4) per physical record."""
+    from forst_amd import engine, workload
+
+    w = workload.make_wal_batch(n_records, workload.SEEDS["C5"])
+    offs = torch.from_numpy(w.rec_offsets.view(np.int64)).cuda()
+    crc = torch.empty(len(w.rec_offsets), dtype=torch.uint32, device="cuda")
+    nb = w.n_log_blocks
+    st = torch.empty(nb, dtype=torch.uint8, device="cuda")
+    nrec = torch.empty(nb, dtype=torch.uint32, device="cuda")
+    fail = torch.empty(nb, dtype=torch.uint32, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    L = engine.lib()
+    s0 = engine._stream(None)
+
+    def verify():
+        engine.check(L.forst_wal_verify_batch(w.log.data_ptr(), w.total, 0, nb, 0,
+                                              st.data_ptr(), nrec.data_ptr(), fail.data_ptr(),
+                                              bad.data_ptr(), s0))
+
+    def write():
+        engine.wal_record_crc_batch(w.log, offs, write_in_place=True, out=crc)
+
+    for _ in range(max(1, warmup)):
+        write()
+        verify()
+    torch.cuda.synchronize()
+    bad.zero_()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        e[0].record()
+        write()
+        e[1].record()
+        verify()
+        e[2].record()
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0, "WAL blocks failed verification in the timed region"
+    assert int(nrec.sum().item()) == len(w.rec_offsets)
+    t_w = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
+    t_v = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
+    rec_bytes = int(w.rec_lengths.astype(np.int64).sum()) + 7 * len(w.rec_offsets)
+    alg_v = w.total + 9 * nb
+    alg_w = rec_bytes + 16 * len(w.rec_offsets)
+    out = {"desc": f"{n_records} records log-uniform 32..32768 B, "
+                   f"{w.total / GIB:.1f} GiB log, {len(w.rec_offsets)} physical records",
+           "verify_GiBps": round(w.total / t_v / GIB, 1),
+           "verify_ms": round(t_v * 1e3, 3),
+           "verify_roofline_frac": round(alg_v / t_v / 1e9 / HBM_PEAK_GBS, 4),
+           "writer_crc_GiBps": round(rec_bytes / t_w / GIB, 1),
+           "writer_crc_ms": round(t_w * 1e3, 3),
+           "writer_roofline_frac": round(alg_w / t_w / 1e9 / HBM_PEAK_GBS, 4)}
+    del w
+    return out
+
+
 def cpu_baseline(b, ctype, budget_s=12.0):
     """Time the oracle (our CPU restatement, compiled -O3 -march=x86-64-v3 with
     SSE4.2 crc32 3-way + AVX2 XXH3) on a bounded sample of the same blocks."""
@@ -281,6 +342,9 @@ def main():
                 "verify_roofline_frac": round(r["kernels"]["verify"]["frac"], 4),
                 "trailer_kernel_GiBps": round(r["kernels"]["trailer"]["gibs_checksummed"], 1),
                 "trailer_roofline_frac": round(r["kernels"]["trailer"]["frac"], 4)}
+    if world == 1 and not args.no_extras and args.config == "C2":
+        extras["C5_wal"] = run_wal(max(3, args.steps // 2), 1)
+        torch.cuda.empty_cache()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

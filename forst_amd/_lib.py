@@ -59,6 +59,7 @@ def lib():
         "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp,
                                       u64, vp]),
+        "forst_wal_layout": (i, [vp, u64, i, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp]),
         "forst_fill_stream": (i, [vp, u64, u64, u64, vp]),
     }
     for name, (res, args) in sigs.items():

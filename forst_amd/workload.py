@@ -7,12 +7,14 @@ bytes are the splitmix64 stream of the config's seed (byte i of the buffer is
 byte i of the stream); trailers are written by the engine's own trailer kernel
 (write side) and then read back by the verify kernel (read side).
 """
+import ctypes
 from dataclasses import dataclass
 
 import numpy as np
 import torch
 
 from . import engine
+from ._lib import check, lib
 
 TRAILER = 5  # table/block_based/block_based_table_reader.h:75 kBlockTrailerSize
 
@@ -97,3 +99,71 @@ def log_uniform_lengths(n, lo, hi, seed):
         k = _splitmix(np.uint64(seed) + idx * np.uint64(0x9E3779B97F4A7C15))
     u = (k >> np.uint64(11)).astype(np.float64) / float(1 << 53)
     return np.exp(np.log(lo) + u * (np.log(hi) - np.log(lo))).astype(np.uint32)
+
+
+@dataclass
+class WalBatch:
+    log: torch.Tensor        # uint8 [total] (device): the log image
+    rec_offsets: np.ndarray  # uint64 header offsets of the physical records (host)
+    rec_lengths: np.ndarray  # uint32 payload lengths
+    rec_types: np.ndarray    # uint8 RecordType
+    n_records: int           # logical records
+    total: int
+    seed: int
+
+    @property
+    def n_log_blocks(self):
+        return (self.total + 32767) // 32768
+
+
+def wal_layout(lengths, recyclable=False):
+    """log::Writer::AddRecord's physical-record layout (forst_wal_layout).
+    Returns (rec_offsets, rec_lengths, rec_types, pad_offsets, pad_lengths, total)."""
+    lengths = np.ascontiguousarray(lengths, dtype=np.uint32)
+    n = len(lengths)
+    np_, npad, tot = ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64()
+    L = lib()
+    check(L.forst_wal_layout(lengths.ctypes.data, n, int(recyclable), None, None, None, 0, None,
+                             None, 0, ctypes.byref(np_), ctypes.byref(npad), ctypes.byref(tot)))
+    offs = np.empty(np_.value, np.uint64)
+    lens = np.empty(np_.value, np.uint32)
+    types = np.empty(np_.value, np.uint8)
+    poffs = np.empty(max(1, npad.value), np.uint64)
+    plens = np.empty(max(1, npad.value), np.uint32)
+    check(L.forst_wal_layout(lengths.ctypes.data, n, int(recyclable), offs.ctypes.data,
+                             lens.ctypes.data, types.ctypes.data, np_.value, poffs.ctypes.data,
+                             plens.ctypes.data, npad.value, ctypes.byref(np_), ctypes.byref(npad),
+                             ctypes.byref(tot)))
+    return offs, lens, types, poffs[:npad.value], plens[:npad.value], tot.value
+
+
+def make_wal_batch(n_records, seed, lo=32, hi=32768, recyclable=False, log_number=0,
+                   device="cuda", lengths=None):
+    """C5-shaped WAL image built on the device: logical record
+    lengths log-uniform in [lo, hi], framed by log::Writer's rules
+    (forst_wal_layout); payload bytes are the splitmix64 stream of `seed`,
+    headers [crc:4 len:2 type:1 (lognum:4)] are written in place, block-tail
+    pads zeroed and the CRCs filled by the writer-side kernel
+    (forst_wal_record_crc_batch)."""
+    if lengths is None:
+        lengths = log_uniform_lengths(n_records, lo, hi, seed)
+    offs, lens, types, poffs, plens, total = wal_layout(lengths, recyclable)
+    alloc = max(256, (total + 255) // 256 * 256)
+    log = torch.empty(alloc, dtype=torch.uint8, device=device)
+    engine.fill_stream(log, 0, seed)
+    log = log[:total]
+    d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
+    hdr = [(4, (lens & 0xFF).astype(np.uint8)), (5, (lens >> 8).astype(np.uint8)), (6, types)]
+    if recyclable:
+        for k in range(4):
+            hdr.append((7 + k, np.full(len(offs), (log_number >> (8 * k)) & 0xFF, np.uint8)))
+    for k, v in hdr:
+        log[d_offs + k] = torch.from_numpy(v).to(device)
+    if len(poffs):  # zero-filled block tails (log_writer.cc:88-97)
+        plens64 = plens.astype(np.int64)
+        starts = np.repeat(poffs.astype(np.int64), plens64)
+        within = np.arange(int(plens64.sum()), dtype=np.int64) - np.repeat(
+            np.cumsum(plens64) - plens64, plens64)
+        log[torch.from_numpy(starts + within).to(device)] = 0
+    engine.wal_record_crc_batch(log, d_offs, write_in_place=True)
+    return WalBatch(log, offs, lens, types, len(lengths), total, seed)

@@ -161,6 +161,17 @@ int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                                uint64_t n_records, int write_in_place,
                                uint32_t* crc_out, void* stream);
 
+/* Host utility (no GPU call): the physical-record layout log::Writer::AddRecord
+ * produces for logical records of the given lengths (db/log_writer.cc:65-160,
+ * no compression): header offset, payload length and RecordType of every
+ * physical record, the zero-padded block tails, and the image size.  Pass NULL
+ * arrays (capacity 0) to count first.  FORST_EINVAL if a capacity is short. */
+int forst_wal_layout(const uint32_t* lengths, uint64_t n_records, int recyclable,
+                     uint64_t* rec_offsets, uint32_t* rec_lengths, uint8_t* rec_types,
+                     uint64_t capacity, uint64_t* pad_offsets, uint32_t* pad_lengths,
+                     uint64_t pad_capacity, uint64_t* n_phys, uint64_t* n_pads,
+                     uint64_t* total_bytes);
+
 /* NPHash64 / Hash64 (util/hash.h:45-62, util/hash.cc:81 ->
  * XXPH3_64bits_withSeed, util/xxph3.h:1733; xxHash 0.7.2 preview):
  * out[i] = Hash64(base + offsets[i], lengths[i], seeds ? seeds[i] : seed).

@@ -58,3 +58,49 @@ def shim_selftest(tmp_path_factory):
 def test_host_shim_pure_helpers(shim_selftest):
     out = subprocess.check_output([shim_selftest, "pure"], text=True)
     assert "PASS" in out, out
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_layout_matches_writer_framing(recyclable):
+    """forst_wal_layout (host utility, no GPU call) reproduces log::Writer's
+    fragmentation (db/log_writer.cc:65-160) exactly as the oracle frames it:
+    physical-record offsets, lengths, types, zero-filled block tails."""
+    import numpy as np
+    from forst_amd import workload
+    from oracle import oracle as O
+    hs = 11 if recyclable else 7
+    rng = np.random.default_rng(8)
+    lens = workload.log_uniform_lengths(3000, 32, 32768, 0xF0E5700005)
+    lens[:6] = [0, 1, 7, 32761, 32762, 70000]
+    # from a block start, each of these leaves a 1..hs-1 byte block tail -> padding
+    tail = (32768 - hs - rng.integers(1, hs, 200)).astype(np.uint32)
+    lens = np.concatenate([tail, lens, np.zeros(5, np.uint32), [200000]]).astype(np.uint32)
+    offs, l, t, po, pl, tot = workload.wal_layout(lens, recyclable)
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, oo, ol = O.wal_frame(payload, lens, recyclable=recyclable, log_number=7)
+    assert tot == len(buf)
+    assert (offs == oo).all() and (l == ol).all()
+    assert (t == buf[offs.astype(np.int64) + 6]).all()
+    assert len(po) >= 100
+    for o, n in zip(po, pl):
+        assert 0 < n < hs and (int(o) + int(n)) % 32768 == 0
+        assert not buf[int(o):int(o) + int(n)].any()
+    # every byte is a header, a payload byte or a pad byte
+    assert int(l.astype(np.int64).sum()) + hs * len(offs) + int(pl.astype(np.int64).sum()) == tot
+    # no fragment straddles a log block
+    assert ((offs % 32768) + hs + l <= 32768).all()
+
+
+def test_wal_layout_capacity_errors():
+    import numpy as np
+    from forst_amd import ForstError
+    L = _lib.lib()
+    lens = np.array([40000, 5], np.uint32)
+    offs = np.zeros(1, np.uint64)
+    n = ctypes.c_uint64()
+    rc = L.forst_wal_layout(lens.ctypes.data, 2, 0, offs.ctypes.data, None, None, 1, None, None,
+                            0, ctypes.byref(n), None, None)
+    assert rc != 0 and n.value == 3
+    with pytest.raises(ForstError):
+        _lib.check(L.forst_wal_layout(None, 2, 0, None, None, None, 0, None, None, 0, None, None,
+                                      None))

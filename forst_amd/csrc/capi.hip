@@ -6,6 +6,7 @@
 #include <hip/hip_runtime.h>
 
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <mutex>
 #include <string>
@@ -54,6 +55,59 @@ const DeviceInfo& device_info() {
     }
   });
   return g_info[dev];
+}
+
+namespace {
+std::once_flag g_pool_once[kMaxDevices];
+hipMemPool_t g_pool[kMaxDevices];
+hipError_t g_pool_err[kMaxDevices];
+}  // namespace
+
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
+  const int dev = device_info().device;
+  if (dev < 0 || dev >= kMaxDevices) return hipErrorInvalidDevice;
+  std::call_once(g_pool_once[dev], [dev] {
+    hipMemPoolProps props;
+    std::memset(&props, 0, sizeof(props));
+    props.allocType = hipMemAllocationTypePinned;
+    props.location.type = hipMemLocationTypeDevice;
+    props.location.id = dev;
+    g_pool_err[dev] = hipMemPoolCreate(&g_pool[dev], &props);
+    if (g_pool_err[dev] == hipSuccess) {
+      uint64_t keep = UINT64_MAX;  // freed blocks stay in the pool for the next call
+      g_pool_err[dev] = hipMemPoolSetAttribute(g_pool[dev], hipMemPoolAttrReleaseThreshold, &keep);
+    }
+  });
+  if (g_pool_err[dev] != hipSuccess) return g_pool_err[dev];
+  return hipMallocFromPoolAsync(p, bytes ? bytes : 16, g_pool[dev], stream);
+}
+
+hipError_t scratch_free(void* p, hipStream_t stream) { return p ? hipFreeAsync(p, stream) : hipSuccess; }
+
+hipError_t feed_setup(BlockArgs& a, uint64_t nw, hipStream_t stream) {
+  // half the descriptors as equal static shares (no claims while the
+  // machine fills), the rest in claimed 64-descriptor chunks that absorb
+  // the byte imbalance of mixed block sizes
+  const char* f = std::getenv("FORST_FEED");
+  const std::string mode = f ? f : "";
+  a.ticket = nullptr;
+  if (mode == "static") {  // one contiguous share per wave (A/B reference)
+    a.share1 = (a.n + 64 * nw - 1) / (64 * nw) * 64;
+    if (a.share1 * nw > a.n) a.share1 = a.n / (64 * nw) * 64;
+    return hipSuccess;
+  }
+  a.share1 = a.n / (2 * 64 * nw) * 64;
+  if (mode == "rr") return hipSuccess;
+  void* p = nullptr;
+  hipError_t e = scratch_alloc(&p, 64 * sizeof(unsigned long long), stream);
+  if (e != hipSuccess) return e;
+  e = hipMemsetAsync(p, 0, sizeof(unsigned long long), stream);
+  if (e != hipSuccess) {
+    (void)scratch_free(p, stream);
+    return e;
+  }
+  a.ticket = static_cast<unsigned long long*>(p);
+  return hipSuccess;
 }
 
 namespace {

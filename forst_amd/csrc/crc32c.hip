@@ -1239,16 +1239,19 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
                            uniform(kCrcS0[3])};
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-  uint64_t kbeg, kend;
-  wave_share(a.n, nw, gw, kbeg, kend);
-  if (kbeg >= kend) return;
-  const uint64_t cnt = kend - kbeg;
   const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
 
+  // descriptor batches from the work feed: lane j <-> descriptor cg + j (cb),
+  // ng + j (nb); a row's rel is the descriptor's global index (n < 2^32 - 1)
+  BatchFeed feed;
+  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  if (cg >= a.n) return;
+  uint64_t ng = feed_next(a, nw, lane, feed);
   DescBatch cb, nb;
-  uint64_t kbrel = 0;
-  load_batch<MODE>(a, kbeg, kend, lane, cb);
-  load_batch<MODE>(a, kbeg + kBatch, kend, lane, nb);
+  uint64_t kbrel = 0;  // stream position of cb's first entry
+  load_batch<MODE>(a, cg, a.n, lane, cb);
+  load_batch<MODE>(a, ng, a.n, lane, nb);
+  const uint64_t kbeg = 0;
   auto fetch = [&](uint64_t rel, CRowPos& P) {
     const uint32_t j = static_cast<uint32_t>(rel - kbrel);
     const int src = static_cast<int>(j & 63u);
@@ -1260,7 +1263,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
     P.off_lo = in_n ? lo_n : lo_c;
     P.off_hi = in_n ? hi_n : hi_c;
     P.size = in_n ? sz_n : sz_c;
-    P.rel = rel < cnt ? static_cast<uint32_t>(rel) : kNoBlk;
+    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
+    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoBlk;
     P.g = 0;
     crow_derive<MODE>(a, P);
   };
@@ -1281,7 +1285,9 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
     if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
       kbrel += kBatch;
       cb = nb;
-      load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
+      cg = ng;
+      ng = feed_next(a, nw, lane, feed);
+      load_batch<MODE>(a, ng, a.n, lane, nb);
     }
   };
   CRowPos I;
@@ -1512,8 +1518,9 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   // where the per-block finish dominates; the v2 kernel (two 4 KiB steps in
   // flight per wave) otherwise.  Mean block size from the launch arguments.
   const bool small_blocks = a.base_len / a.n <= 6144;
-  const bool rows = (variant && std::string(variant) == "rows") ||
-                    ((!variant || !*variant) && small_blocks);
+  // (the rows kernel indexes descriptors with 32 bits)
+  const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
+                                            ((!variant || !*variant) && small_blocks));
   // diagnostics: probe_load (loads only), probe_rounds (no finish),
   // probe_nohead (no round-0 head handling); results are not checksums
   const int probe = !variant ? 0
@@ -1529,7 +1536,13 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
                          stream, a);                                                      \
     } else if (rows) {                                                                    \
       *name = "crc32c_rows_kernel<" TAG ">";                                              \
-      hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, a); \
+      BlockArgs b = a;                                                                    \
+      hipError_t fe = feed_setup(b, uint64_t(grid) * kWaves, stream);                     \
+      if (fe != hipSuccess) return fe;                                                    \
+      hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, b); \
+      fe = hipGetLastError();                                                             \
+      const hipError_t ff = scratch_free(b.ticket, stream);                               \
+      return fe != hipSuccess ? fe : ff;                                                  \
     } else if (v1) {                                                                      \
       *name = "crc32c_stream_kernel<" TAG ">";                                            \
       hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \
@@ -1673,7 +1686,7 @@ __global__ void __launch_bounds__(kThreads) wal_record_crc_kernel(WalArgs a) {
 
 }  // namespace
 
-hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
+hipError_t launch_wal_verify_wave(const WalArgs& a, hipStream_t stream,
                              const char** name) {
   const DeviceInfo& di = device_info();
   if (a.n_blocks == 0) return hipSuccess;
@@ -1684,7 +1697,7 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
   return hipGetLastError();
 }
 
-hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,
+hipError_t launch_wal_record_crc_wave(const WalArgs& a, hipStream_t stream,
                                  const char** name) {
   const DeviceInfo& di = device_info();
   if (a.n_records == 0) return hipSuccess;

@@ -30,6 +30,11 @@ struct BlockArgs {
   uint8_t* ok_out;             // nullable (verify)
   unsigned long long* mismatches;  // nullable (verify)
   uint64_t n;
+  // rows kernels' work feed (stream_common.h): a static first share of
+  // share1 descriptors per wave, then 64-descriptor chunks claimed from
+  // *ticket (zeroed per launch) or, without one, dealt round-robin
+  unsigned long long* ticket;
+  uint64_t share1;
 };
 
 struct WalArgs {
@@ -83,6 +88,14 @@ struct DeviceInfo {
   bool ok;
 };
 const DeviceInfo& device_info();  // current device (lazily initialised)
+
+// stream-ordered scratch from a per-device pool that keeps freed memory
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream);
+hipError_t scratch_free(void* p, hipStream_t stream);
+// work feed of a rows-kernel launch over nw waves (stream_common.h): sets
+// share1 and, unless FORST_FEED=static|rr, a zeroed ticket counter that the
+// caller releases with scratch_free(a.ticket) after the launch
+hipError_t feed_setup(BlockArgs& a, uint64_t nw, hipStream_t stream);
 
 // Launchers (return hipError_t). `kernel_name` receives a static string.
 hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,

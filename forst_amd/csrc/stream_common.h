@@ -24,6 +24,56 @@ __device__ __forceinline__ void wave_share(uint64_t n, uint64_t nw, uint64_t gw,
   kend = kbeg + q + (gw < rem ? 1 : 0);
 }
 
+// Work feed of the rows kernels: a wave consumes a stream of 64-descriptor
+// batches -- first its static share [gw * share1, (gw + 1) * share1)
+// (share1 a multiple of 64, nw * share1 <= n), then 64-descriptor chunks
+// starting at nw * share1 + 64 * t, t claimed from a.ticket (one atomic per
+// chunk; a wave whose blocks ran long simply claims fewer chunks), or dealt
+// round-robin (t = gw, gw + nw, ...) when the launch has no ticket counter
+// (a.ticket points at 64 counters, [0] zeroed per launch).
+// Chunks never straddle a batch, so a batch is one contiguous run
+// [g, g + 64) of descriptors (entries >= n are empty).  Once a batch starts
+// at >= n every later one does too and the feed stops claiming.
+struct BatchFeed {
+  uint64_t g;    // start of the last batch handed out
+  uint64_t lim;  // end of the static share / chunk it belongs to
+  uint64_t rr;   // round-robin ticket (no counter)
+};
+
+__device__ __forceinline__ uint64_t feed_claim(const BlockArgs& a, uint64_t nw, uint32_t lane,
+                                               BatchFeed& f) {
+  uint64_t t;
+  if (a.ticket) {
+    // the whole wave issues the atomic (no divergent branch in the hot loop):
+    // lane 0 claims on ticket[0], the other lanes add 0 to their own slots
+    const unsigned long long v = atomicAdd(a.ticket + lane, lane == 0 ? 1ull : 0ull);
+    t = uniform64(v);
+  } else {
+    t = f.rr;
+    f.rr += nw;
+  }
+  f.g = nw * a.share1 + static_cast<uint64_t>(kBatch) * t;
+  f.lim = f.g + kBatch;
+  return f.g;
+}
+
+__device__ __forceinline__ uint64_t feed_first(const BlockArgs& a, uint64_t nw, uint64_t gw,
+                                               uint32_t lane, BatchFeed& f) {
+  f.rr = gw;
+  if (a.share1 == 0) return feed_claim(a, nw, lane, f);
+  f.g = gw * a.share1;
+  f.lim = f.g + a.share1;
+  return f.g;
+}
+
+__device__ __forceinline__ uint64_t feed_next(const BlockArgs& a, uint64_t nw, uint32_t lane,
+                                              BatchFeed& f) {
+  if (f.g >= a.n) return f.g;  // exhausted: stays exhausted, no more claims
+  f.g += kBatch;
+  if (f.g < f.lim) return f.g;
+  return feed_claim(a, nw, lane, f);
+}
+
 // per-lane descriptor batch (lane j <-> block kb + j)
 struct DescBatch {
   uint32_t off_lo, off_hi, size, mod, extra;  // extra: last byte, or init (raw CRC)

@@ -623,17 +623,19 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
   const uint64_t ks0 = sec64(128 + 16 * p), ks1 = sec64(136 + 16 * p);
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
-  uint64_t kbeg, kend;
-  wave_share(a.n, nw, gw, kbeg, kend);
-  if (kbeg >= kend) return;
-  const uint64_t cnt = kend - kbeg;
-
-  // descriptor batches: lane j <-> message kbrel + j (cb), kbrel + 64 + j (nb)
+  // descriptor batches from the work feed (stream_common.h): lane j <->
+  // message cg + j (cb), ng + j (nb); a row's rel is the message's global
+  // index (n < 2^32 - 1), kbrel the stream position of cb's first entry
+  BatchFeed feed;
+  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  if (cg >= a.n) return;
+  uint64_t ng = feed_next(a, nw, lane, feed);
+  const uint64_t kbeg = 0;
   DescBatch cb, nb;
   uint64_t kbrel = 0;
-  load_batch<MODE>(a, kbeg, kend, lane, cb);
-  load_batch<MODE>(a, kbeg + kBatch, kend, lane, nb);
-  auto fetch = [&](uint32_t rel, RowPos& P) {
+  load_batch<MODE>(a, cg, a.n, lane, cb);
+  load_batch<MODE>(a, ng, a.n, lane, nb);
+  auto fetch = [&](uint64_t rel, RowPos& P) {
     const uint32_t j = static_cast<uint32_t>(rel - kbrel);
     const int src = static_cast<int>(j & 63u);
     const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
@@ -644,15 +646,15 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
     P.off_lo = in_n ? lo_n : lo_c;
     P.off_hi = in_n ? hi_n : hi_c;
     P.size = in_n ? sz_n : sz_c;
-    P.rel = rel;
+    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
+    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoMsg;
     P.g = 0;
   };
-  // rows start on messages 0..3 of the share
+  // rows start on messages 0..3 of the stream
   const uint32_t row = lane >> 4;
   uint64_t next = 4;
   RowPos C;
   fetch(row, C);
-  if (row >= cnt) C.rel = kNoMsg;
 
   // I = the position after P: next XXH3-block, or a newly assigned message
   auto advance = [&](const RowPos& P, RowPos& I) {
@@ -662,10 +664,8 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
     const bool need = P.rel != kNoMsg && !more;
     const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
     const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
-    const uint64_t nrel = next + rank;
     RowPos F;
-    fetch(static_cast<uint32_t>(nrel), F);
-    if (nrel >= cnt) F.rel = kNoMsg;
+    fetch(next + rank, F);
     next += static_cast<uint64_t>(__popcll(rows));
     I = P;
     if (more) I.g = P.g + 1;
@@ -673,7 +673,9 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
     if (next >= kbrel + kBatch) {  // every message of cb is assigned: slide the batches
       kbrel += kBatch;
       cb = nb;
-      load_batch<MODE>(a, kbeg + kbrel + kBatch, kend, lane, nb);
+      cg = ng;
+      ng = feed_next(a, nw, lane, feed);
+      load_batch<MODE>(a, ng, a.n, lane, nb);
     }
   };
 
@@ -916,7 +918,8 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   const char* variant = std::getenv("FORST_XXH3_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < 4096;
   const bool probe = variant && std::string(variant) == "probe_load" && mode == kModeVerify;
-  const bool v1 = variant && std::string(variant) == "v1";
+  // the rows kernel indexes descriptors with 32 bits
+  const bool v1 = (variant && std::string(variant) == "v1") || a.n >= 0xffffffffull;
 #define FORST_LAUNCH_XXH3(M, TAG)                                                          \
   do {                                                                                     \
     if (simple) {                                                                          \
@@ -939,7 +942,13 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
       const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
           1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),                     \
                                 uint64_t(di.num_cus) * rows_occupancy<M>())));             \
-      hipLaunchKernelGGL(xxh3_rows_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, a);     \
+      BlockArgs b = a;                                                                     \
+      hipError_t fe = feed_setup(b, uint64_t(sg) * kWaves, stream);                        \
+      if (fe != hipSuccess) return fe;                                                     \
+      hipLaunchKernelGGL(xxh3_rows_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, b);     \
+      fe = hipGetLastError();                                                              \
+      const hipError_t ff = scratch_free(b.ticket, stream);                                \
+      return fe != hipSuccess ? fe : ff;                                                   \
     }                                                                                      \
   } while (0)
   switch (mode) {

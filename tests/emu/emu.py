@@ -128,6 +128,15 @@ def wal_verify(log, log_number=0):
     return st, nrec, fail, int(bad[0])
 
 
+def wal_record_crc(log, header_offsets, write_in_place=True):
+    log = _aligned(log)
+    offs = np.ascontiguousarray(header_offsets, dtype=np.uint64)
+    out = np.zeros(len(offs), np.uint32)
+    _chk(lib().forst_wal_record_crc_batch(_p(log), log.nbytes, _p(offs), len(offs),
+                                          int(write_in_place), _p(out), None))
+    return out, log
+
+
 def hash64(base, offs, lens, seeds=None, seed=0):
     base = _aligned(base)
     offs = np.ascontiguousarray(offs, np.uint64)

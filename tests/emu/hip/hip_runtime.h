@@ -14,6 +14,7 @@
 #include <barrier>
 #include <cstdint>
 #include <cstdio>
+#include <cstdlib>
 #include <cstring>
 #include <functional>
 #include <memory>
@@ -195,6 +196,43 @@ inline emu_u32x2 __builtin_amdgcn_permlane32_swap(uint32_t old, uint32_t src, bo
 }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
+}
+
+// stream-ordered allocation / copies: host memory, everything synchronous
+typedef void* hipMemPool_t;
+constexpr hipError_t hipErrorInvalidDevice = 101;
+enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2 };
+enum { hipMemAllocationTypePinned = 1, hipMemLocationTypeDevice = 1,
+       hipMemPoolAttrReleaseThreshold = 4 };
+struct hipMemPoolProps {
+  int allocType;
+  int handleTypes;
+  struct { int type; int id; } location;
+  void* win32SecurityAttributes;
+  size_t maxSize;
+  unsigned char reserved[56];
+};
+inline hipError_t hipMemPoolCreate(hipMemPool_t* p, const hipMemPoolProps*) {
+  *p = reinterpret_cast<hipMemPool_t>(1);
+  return hipSuccess;
+}
+inline hipError_t hipMemPoolSetAttribute(hipMemPool_t, int, void*) { return hipSuccess; }
+inline hipError_t hipMallocFromPoolAsync(void** p, size_t n, hipMemPool_t, hipStream_t) {
+  *p = std::aligned_alloc(256, (n + 255) & ~size_t(255));
+  return *p ? hipSuccess : 2;
+}
+inline hipError_t hipFreeAsync(void* p, hipStream_t) {
+  std::free(p);
+  return hipSuccess;
+}
+inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind, hipStream_t) {
+  std::memcpy(d, s, n);
+  return hipSuccess;
+}
+inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
+  std::memset(d, v, n);
+  return hipSuccess;
 }
 
 #define hipLaunchKernelGGL(K, G, B, SH, ST, ...) ::emu::launch(K, G, B, __VA_ARGS__)

@@ -90,6 +90,50 @@ def test_emu_wal():
     assert bad == 0 and (st == 0).all() and int(nrec.sum()) == len(poffs)
 
 
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_emu_wal_pipeline_statuses(recyclable, monkeypatch):
+    """walk/scan/fill/raw-CRC/status pipeline == the serial per-block reader
+    (FORST_WAL_VARIANT=wave) on every status: CRC failure, bad length, old
+    record, zero padding, truncated tail; writer-side CRCs restore the image."""
+    rng = np.random.default_rng(2)
+    lens = rng.integers(0, 9000, 90).astype(np.uint32)
+    lens[:4] = [0, 32761, 5, 70000]
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=recyclable, log_number=9)
+    hs = 11 if recyclable else 7
+    b = buf.copy()
+    nb = (len(b) + 32767) // 32768
+    blk = (poffs // 32768).astype(np.int64)
+    firsts = [int(np.nonzero(blk == k)[0][0]) for k in range(nb) if (blk == k).any()]
+    k0, k1, k2, k3 = firsts[1], firsts[3], firsts[5], firsts[7]
+    assert plens[k0] > 0
+    b[int(poffs[k0]) + hs] ^= 0x40                        # CRC covers the payload
+    b[int(poffs[k1]) + 4:int(poffs[k1]) + 6] = 0xff              # length past the block
+    if recyclable:
+        b[int(poffs[k2]) + 7] ^= 1                          # older log number
+    b[int(poffs[k3]):int(poffs[k3]) + 7] = 0               # zero type/length
+    b = b[:len(b) - 3]                                     # truncated tail
+    got = emu.wal_verify(b, log_number=9)
+    monkeypatch.setenv("FORST_WAL_VARIANT", "wave")
+    want = emu.wal_verify(b, log_number=9)
+    monkeypatch.delenv("FORST_WAL_VARIANT")
+    for g, w in zip(got[:3], want[:3]):
+        assert (g == w).all()
+    assert got[3] == want[3] and got[3] >= 2
+    assert got[0][blk[k0]] == 1 and got[0][blk[k1]] == 2 and got[0][blk[k3]] == 3
+    if recyclable:
+        assert got[0][blk[k2]] == 4
+    # writer side, with one out-of-range offset
+    w = buf.copy()
+    for o in poffs:
+        w[int(o):int(o) + 4] = 0
+    offs = np.concatenate([poffs.astype(np.uint64), [len(buf) - 3]])
+    crcs, img = emu.wal_record_crc(w, offs)
+    assert (img[:len(buf)] == buf).all() and crcs[-1] == 0
+    assert (crcs[:-1] == np.frombuffer(b"".join(buf[int(o):int(o) + 4].tobytes()
+                                                for o in poffs), np.uint32)).all()
+
+
 def test_emu_crc_stream_batches_and_edges():
     """> 64 blocks per wave (descriptor/result batch switches), the 64-byte
     fast-path threshold, every start alignment, a block at the buffer start

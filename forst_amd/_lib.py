@@ -30,7 +30,7 @@ def exported_symbols():
     hdr = os.path.join(os.path.dirname(_HERE), "include", "forst_checksum.h")
     with open(hdr) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|const char\*)\s+(forst_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|uint32_t|const char\*)\s+(forst_\w+)\(", text, re.M)))
 
 
 def lib():
@@ -52,6 +52,9 @@ def lib():
         "forst_block_trailer_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
         "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
+        "forst_crc32c_buffer": (i, [vp, u64, u32, vp, vp]),
+        "forst_crc32c_combine_batch": (i, [vp, vp, vp, vp, u64, vp]),
+        "forst_crc32c_combine": (u32, [u32, u32, u64]),
         "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
         "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
         "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),

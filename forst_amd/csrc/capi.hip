@@ -250,6 +250,30 @@ FORST_API int forst_crc32c_batch(const uint8_t* base, uint64_t base_len,
   return dispatch_blocks(FORST_kCRC32c, kModeRaw, a, stream);
 }
 
+FORST_API int forst_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
+                                  void* stream) {
+  if (!out || (len && (!base || !aligned4(base))))
+    return set_error(FORST_EINVAL, "out must be non-null, base non-null and 4-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  return hip_status(launch_crc32c_buffer(base, len, init, out, static_cast<hipStream_t>(stream),
+                                         &g_last_kernel),
+                    "crc32c_buffer launch");
+}
+
+FORST_API int forst_crc32c_combine_batch(const uint32_t* crc1, const uint32_t* crc2,
+                                         const uint64_t* len2, uint32_t* out, uint64_t n,
+                                         void* stream) {
+  if (n == 0) return FORST_OK;
+  if (!crc1 || !crc2 || !len2 || !out)
+    return set_error(FORST_EINVAL, "crc1/crc2/len2/out must be non-null");
+  int rc = check_device();
+  if (rc) return rc;
+  return hip_status(launch_crc32c_combine_batch(crc1, crc2, len2, out, n,
+                                                static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "crc32c_combine launch");
+}
+
 FORST_API int forst_xxh3_64_batch(const uint8_t* base, uint64_t base_len,
                                   const uint64_t* offsets, const uint32_t* lengths,
                                   uint64_t* out, uint64_t n_buffers, void* stream) {

@@ -111,6 +111,11 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream,
                              const char** kernel_name);
 hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream,
                                  const char** kernel_name);
+hipError_t launch_crc32c_combine_batch(const uint32_t* crc1, const uint32_t* crc2,
+                                       const uint64_t* len2, uint32_t* out, uint64_t n,
+                                       hipStream_t stream, const char** kernel_name);
+hipError_t launch_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
+                                hipStream_t stream, const char** kernel_name);
 hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n,
                               uint64_t seed, hipStream_t stream);

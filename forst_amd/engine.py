@@ -131,6 +131,33 @@ def crc32c_batch(base, offsets, lengths, init_crcs=None, out=None, stream=None):
     return out
 
 
+def crc32c_buffer(base, init=0, out=None, stream=None):
+    """crc32c::Extend(init, base) over one device buffer of any size
+    (FileChecksumGenCrc32c, util/file_checksum_helper.h:22).  Returns a
+    1-element uint32 device tensor."""
+    _dev_u8(base)
+    if out is None:
+        out = torch.empty(1, dtype=torch.uint32, device=base.device)
+    check(lib().forst_crc32c_buffer(base.data_ptr(), base.numel(), init & 0xFFFFFFFF,
+                                    out.data_ptr(), _stream(stream)))
+    return out
+
+
+def crc32c_combine_batch(crc1, crc2, len2, out=None, stream=None):
+    """crc32c::Crc32cCombine per element (util/crc32c.h:32), device arrays."""
+    n = crc1.numel()
+    if out is None:
+        out = torch.empty(n, dtype=torch.uint32, device=crc1.device)
+    check(lib().forst_crc32c_combine_batch(crc1.data_ptr(), crc2.data_ptr(), len2.data_ptr(),
+                                           out.data_ptr(), n, _stream(stream)))
+    return out
+
+
+def crc32c_combine(crc1, crc2, len2):
+    """host crc32c::Crc32cCombine (no GPU call)."""
+    return lib().forst_crc32c_combine(crc1 & 0xFFFFFFFF, crc2 & 0xFFFFFFFF, len2)
+
+
 def xxh3_64_batch(base, offsets, lengths, out=None, stream=None):
     """XXH3_64bits per buffer (util/xxhash.h:5311)."""
     n = _desc(offsets, lengths)

@@ -25,9 +25,16 @@
  *   forst_crc32c_batch          <- crc32c::Extend / crc32c::Value
  *                                  (util/crc32c.h:25, :35)
  *   forst_xxh3_64_batch         <- XXH3_64bits (util/xxhash.h:933/:5311)
+ *   forst_crc32c_buffer         <- crc32c::Extend over one large buffer, as
+ *                                  FileChecksumGenCrc32c::Update
+ *                                  (util/file_checksum_helper.h:22) and the
+ *                                  WritableFileWriter handoff CRC
+ *                                  (file/writable_file_writer.cc:100-212)
+ *   forst_crc32c_combine[_batch]<- crc32c::Crc32cCombine (util/crc32c.h:32,
+ *                                  crc32c.cc:1279)
  *   forst_wal_verify_batch      <- log::Reader::ReadPhysicalRecord CRC check
- *                                  (db/log_reader.cc:450-531), one 32 KiB log
- *                                  block per wave
+ *                                  (db/log_reader.cc:450-531) of every 32 KiB
+ *                                  log block
  *   forst_wal_record_crc_batch  <- log::Writer::EmitPhysicalRecord CRC
  *                                  (db/log_writer.cc:228-263)
  *   forst_hash64_batch          <- Hash64 / NPHash64 (util/hash.cc:81-88)
@@ -40,8 +47,11 @@
  *  - All array/buffer pointers are DEVICE pointers (hipMalloc'd, or host
  *    memory registered/mapped so the GPU can read it).  The caller owns every
  *    buffer.  `stream` is a hipStream_t (NULL = default stream).  Calls are
- *    asynchronous and stream-ordered; no call allocates, copies or
- *    synchronises, so a caller may capture them in a hipGraph.
+ *    asynchronous and stream-ordered.  Scratch (work-feed counters, WAL
+ *    record descriptors, chunk CRCs) comes from an engine-owned per-device
+ *    memory pool with stream-ordered alloc/free and is zeroed with
+ *    hipMemsetAsync; no call copies to the host or synchronises except
+ *    forst_wal_verify_batch, which reads the record total back once.
  *  - `base` must be 4-byte aligned; blocks live at base + offsets[i] and may
  *    start at any byte (SST blocks are packed back-to-back with 5-byte
  *    trailers, so starts are unaligned).  base_len bounds every access: a
@@ -132,6 +142,21 @@ int forst_crc32c_batch(const uint8_t* base, uint64_t base_len,
                        const uint64_t* offsets, const uint32_t* lengths,
                        const uint32_t* init_crcs, uint32_t* out,
                        uint64_t n_buffers, void* stream);
+
+/* *out (device) = crc32c::Extend(init, base, len): one buffer of any size,
+ * checksummed in 64 KiB chunks at streaming rate and folded with the combine
+ * identity crc(A||B) = x^(8|B|) * crc(A) ^ crc(B).  init = 0 gives
+ * crc32c::Value. */
+int forst_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
+                        void* stream);
+
+/* out[i] = crc32c::Crc32cCombine(crc1[i], crc2[i], len2[i]) (device arrays). */
+int forst_crc32c_combine_batch(const uint32_t* crc1, const uint32_t* crc2,
+                               const uint64_t* len2, uint32_t* out, uint64_t n, void* stream);
+
+/* Host utility (no GPU call): crc32c::Crc32cCombine(crc1, crc2, len2), the
+ * CRC of A||B from crc(A), crc(B) and |B|. */
+uint32_t forst_crc32c_combine(uint32_t crc1, uint32_t crc2, uint64_t len2);
 
 /* out[i] = XXH3_64bits(base+offsets[i], lengths[i])  (xxHash 0.8.1, seed 0). */
 int forst_xxh3_64_batch(const uint8_t* base, uint64_t base_len,

@@ -196,9 +196,17 @@ uint32_t oracle_crc32c_value(const void* p, size_t n) {
   return oracle_crc32c_extend(0, p, n);
 }
 
-/* raw state shifted by nbytes zero bytes */
+/* raw state shifted by nbytes zero bytes: x^(8 nbytes) = (x^8)^nbytes, exact
+ * for every 64-bit count (the reference walks the bits of len/4 over 62
+ * powers, util/crc32c.cc:1200-1224, also exact; 8 * nbytes would wrap) */
 uint32_t oracle_crc32c_shift(uint32_t state, uint64_t nbytes) {
-  return gf_mul(state, gf_xpow(8 * nbytes));
+  uint32_t m = 0x80000000u; /* 1 */
+  uint32_t sq = 0x00800000u; /* x^8 */
+  for (; nbytes; nbytes >>= 1) {
+    if (nbytes & 1) m = gf_mul(m, sq);
+    sq = gf_mul(sq, sq);
+  }
+  return gf_mul(state, m);
 }
 
 /* util/crc32c.cc:1279 Crc32cCombine: crc(A||B) from crc(A), crc(B), |B|.

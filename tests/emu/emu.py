@@ -28,7 +28,9 @@ def lib():
             "forst_block_checksum_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
             "forst_block_trailer_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp]),
             "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
-            "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
+                "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
+            "forst_crc32c_buffer": (i, [vp, u64, u32, vp, vp]),
+            "forst_crc32c_combine": (u32, [u32, u32, u64]),
             "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
             "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
             "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
@@ -126,6 +128,13 @@ def wal_verify(log, log_number=0):
     _chk(lib().forst_wal_verify_batch(_p(log), log.nbytes, 0, nb, log_number, _p(st), _p(nrec),
                                       _p(fail), _p(bad), None))
     return st, nrec, fail, int(bad[0])
+
+
+def crc32c_buffer(base, init=0):
+    base = _aligned(base)
+    out = np.zeros(1, np.uint32)
+    _chk(lib().forst_crc32c_buffer(_p(base), base.nbytes, init, _p(out), None))
+    return int(out[0])
 
 
 def wal_record_crc(log, header_offsets, write_in_place=True):

@@ -194,6 +194,7 @@ inline emu_u32x2 __builtin_amdgcn_permlane32_swap(uint32_t old, uint32_t src, bo
   r[1] = hi ? src : o_partner;
   return r;
 }
+inline uint32_t atomicXor(uint32_t* p, uint32_t v) { return __atomic_fetch_xor(p, v, __ATOMIC_RELAXED); }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }

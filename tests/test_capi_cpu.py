@@ -104,3 +104,26 @@ def test_wal_layout_capacity_errors():
     with pytest.raises(ForstError):
         _lib.check(L.forst_wal_layout(None, 2, 0, None, None, None, 0, None, None, 0, None, None,
                                       None))
+
+
+def test_crc32c_combine_host_matches_reference_tests():
+    """forst_crc32c_combine == crc32c::Crc32cCombine: util/crc32c_test.cc:128-170
+    cases (basic, order matters, full cover over 0..4095-byte suffixes, big
+    size) against the oracle's Extend."""
+    import numpy as np
+    from forst_amd import engine
+    from oracle import oracle as O
+    a, b = O.crc32c_value(b"hello "), O.crc32c_value(b"world")
+    assert engine.crc32c_combine(a, b, 5) == O.crc32c_value(b"hello world")
+    assert engine.crc32c_combine(b, a, 6) != O.crc32c_value(b"hello world")
+    rng = np.random.default_rng(3)
+    s1 = rng.integers(0, 256, 1 << 20, dtype=np.uint8).tobytes()
+    c1 = O.crc32c_value(s1)
+    for n in list(range(0, 300)) + [1023, 1024, 4095, 65537]:
+        s2 = rng.integers(0, 256, n, dtype=np.uint8).tobytes()
+        assert engine.crc32c_combine(c1, O.crc32c_value(s2), n) == O.crc32c_extend(c1, s2)
+    s2 = rng.integers(0, 256, 16 * 1024 * 1024 - 1, dtype=np.uint8).tobytes()
+    assert engine.crc32c_combine(c1, O.crc32c_value(s2), len(s2)) == O.crc32c_extend(c1, s2)
+    for n in (1 << 33, (1 << 40) + 7, (1 << 63) + 5):  # shift powers beyond memory sizes
+        assert engine.crc32c_combine(0, 0, n) == 0
+        assert engine.crc32c_combine(c1, 0, n) == O.crc32c_combine(c1, 0, n)

@@ -259,3 +259,12 @@ def test_emu_kv_protect_verify(prot_bytes, flags):
                                   d["ops"], d["seqs"], d["cfs"])
     want_bad = {77} | ({40} if int(d["vs"][40]) > 0 else set())
     assert set(np.nonzero(ok == 0)[0].tolist()) == want_bad and bad == len(want_bad)
+
+
+def test_emu_crc32c_buffer():
+    """whole-buffer CRC: 64 KiB chunk CRCs folded with the combine identity"""
+    rng = np.random.default_rng(31)
+    buf = rng.integers(0, 256, 3 * 65536 + 777, dtype=np.uint8)
+    for n in (0, 1, 63, 65535, 65536, 65537, 2 * 65536 + 5, len(buf)):
+        for init in (0, 0xDEADBEEF):
+            assert emu.crc32c_buffer(buf[:n], init) == O.crc32c_extend(init, buf[:n].tobytes())

@@ -501,3 +501,38 @@ def test_full_size_c5_properties():
     vb = (w.rec_offsets[victims] // 32768).astype(np.int64)
     assert set(np.nonzero(st)[0].tolist()) == set(vb.tolist()) and (st[vb] == 1).all()
     assert (host(fail)[vb].astype(np.int64) == (w.rec_offsets[victims] % 32768)).all()
+
+
+# ---- a3: Crc32cCombine and whole-buffer CRC32C ----------------------------
+
+def test_crc32c_buffer_vs_oracle():
+    rng = np.random.default_rng(77)
+    buf = rng.integers(0, 256, 5 * 65536 + 1234, dtype=np.uint8)
+    dbuf = d(buf)
+    for n in (0, 1, 3, 64, 65535, 65536, 65537, 3 * 65536 + 17, len(buf)):
+        for init in (0, 0x12345678):
+            got = int(host(engine.crc32c_buffer(dbuf[:n], init))[0])
+            assert got == O.crc32c_extend(init, buf[:n].tobytes()), (n, init)
+
+
+def test_crc32c_buffer_large():
+    """1 GiB + 3 bytes in one call (16385 chunks through the block kernel)"""
+    n = (1 << 30) + 3
+    dev = torch.empty(n + 253, dtype=torch.uint8, device=DEV)
+    engine.fill_stream(dev, 0, 0xC0FFEE)
+    want = O.crc32c_extend(0xFFFF0000, host(dev[:n]).tobytes())
+    assert int(host(engine.crc32c_buffer(dev[:n], 0xFFFF0000))[0]) == want
+
+
+def test_crc32c_combine_batch_vs_oracle():
+    rng = np.random.default_rng(78)
+    n = 5000
+    c1 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    c2 = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    ln = rng.integers(0, 2**40, n, dtype=np.uint64)
+    ln[:6] = [0, 1, 3, 4, 65536, (1 << 63) + 5]
+    got = host(engine.crc32c_combine_batch(d(c1.view(np.int32)), d(c2.view(np.int32)),
+                                           d(ln.view(np.int64)))).view(np.uint32)
+    want = np.array([O.crc32c_combine(int(a), int(b), int(c)) for a, b, c in zip(c1, c2, ln)],
+                    np.uint32)
+    assert (got == want).all()

@@ -34,7 +34,9 @@ def main():
                     help="ENV=VALUE (empty value = unset); several comma-joined allowed")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--mode", default="verify", choices=["verify", "trailer"])
+    ap.add_argument("--mode", default="verify", choices=["verify", "trailer", "pair"],
+                    help="pair: trailer then verify per rep (bench.py's step), verify timed")
+    ap.add_argument("--computed", action="store_true", help="verify also stores computed[]")
     args = ap.parse_args()
     variants = args.var or [""]
     res = {}
@@ -42,6 +44,7 @@ def main():
         n, spec, ct = CONFIGS[cfg]
         b = workload.make_sst_batch(n, spec, 0xF0E5700002, ctype=ct)
         ok = torch.empty(n, dtype=torch.uint8, device="cuda")
+        comp = torch.empty(n, dtype=torch.uint32, device="cuda") if args.computed else None
         bad = torch.zeros(1, dtype=torch.int64, device="cuda")
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
@@ -57,12 +60,24 @@ def main():
                 e0 = torch.cuda.Event(enable_timing=True)
                 e1 = torch.cuda.Event(enable_timing=True)
                 # warm
-                engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=None,
+                engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=comp,
                                           stored=None, ok=ok, mismatches=bad)
+                if args.mode == "pair":
+                    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(2)]
+                           for _ in range(args.reps)]
+                    for r in range(args.reps):
+                        engine.block_trailer_batch(ct, b.base, b.offsets, b.sizes, b.types)
+                        evs[r][0].record()
+                        engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=comp,
+                                                  stored=None, ok=ok, mismatches=bad)
+                        evs[r][1].record()
+                    torch.cuda.synchronize()
+                    times[v].append(np.mean([x.elapsed_time(y) for x, y in evs]) / 1e3)
+                    continue
                 e0.record()
                 for _ in range(args.reps):
                     if args.mode == "verify":
-                        engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=None,
+                        engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=comp,
                                                   stored=None, ok=ok, mismatches=bad)
                     else:
                         engine.block_trailer_batch(ct, b.base, b.offsets, b.sizes, b.types)

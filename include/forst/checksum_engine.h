@@ -63,6 +63,10 @@ inline uint32_t Unmask(uint32_t m) {
   uint32_t rot = m - 0xa282ead8ul;
   return (rot >> 17) | (rot << 15);
 }
+// util/crc32c.h:32 (host GF(2) arithmetic in the engine library)
+inline uint32_t Crc32cCombine(uint32_t crc1, uint32_t crc2, size_t crc2len) {
+  return forst_crc32c_combine(crc1, crc2, crc2len);
+}
 }  // namespace crc32c
 
 // table/format.h:119

@@ -39,6 +39,12 @@ static void pure() {
   CHECK(crc != crc32c::Mask(crc));
   CHECK(crc == crc32c::Unmask(crc32c::Mask(crc)));
   CHECK(crc == crc32c::Unmask(crc32c::Unmask(crc32c::Mask(crc32c::Mask(crc)))));
+  // util/crc32c_test.cc:128-142
+  const uint32_t c1 = crc32c_ref(reinterpret_cast<const uint8_t*>("hello "), 6);
+  const uint32_t c2 = crc32c_ref(reinterpret_cast<const uint8_t*>("world"), 5);
+  const uint32_t c3 = crc32c_ref(reinterpret_cast<const uint8_t*>("hello world"), 11);
+  CHECK(crc32c::Crc32cCombine(c1, c2, 5) == c3);
+  CHECK(crc32c::Crc32cCombine(c2, c1, 6) != c3);
   // table/format.h:119
   CHECK(ChecksumModifierForContext(0, 12345) == 0);
   CHECK(ChecksumModifierForContext(7, 0x100000001ull) == (7u ^ 2u));

@@ -53,6 +53,11 @@ def lib():
         "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_buffer": (i, [vp, u64, u32, vp, vp]),
+        "forst_sst_footer_decode": (i, [vp, u64, u64, vp]),
+        "forst_sst_index_handles": (i, [vp, u64, i, i, vp, vp, u64, vp]),
+        "forst_sst_properties_decode": (i, [vp, u64, vp]),
+        "forst_sst_last_error": (ctypes.c_char_p, []),
+        "forst_sst_verify_file": (i, [vp, u64, vp, ctypes.c_char_p, vp, vp]),
         "forst_crc32c_combine_batch": (i, [vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_combine": (u32, [u32, u32, u64]),
         "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),

@@ -126,6 +126,7 @@ class BlockChecksumEngine {
                       std::vector<uint64_t>* failed = nullptr);
 
   const ChecksumStats& stats() const { return stats_; }
+  void* stream() const { return stream_; }
 
  private:
   Status EnsureScratch(uint64_t n);
@@ -139,5 +140,20 @@ class BlockChecksumEngine {
   unsigned long long* d_bad_ = nullptr;
   uint64_t cap_ = 0;
 };
+
+// BlockBasedTable::VerifyChecksum (block_based_table_reader.cc:2457) for one
+// SST file: host_file (host memory) is decoded on the host, dev_file (the
+// same bytes in device memory) supplies every checksum computed on the GPU.
+struct SstVerifyReport {
+  uint32_t format_version = 0;
+  int checksum_type = 0;
+  uint32_t index_type = 0;
+  uint64_t blocks_verified = 0;
+  uint64_t data_blocks = 0, meta_blocks = 0, index_partitions = 0;
+  std::vector<uint64_t> failed;  // indexes into [meta blocks..., data blocks...]
+};
+Status VerifySstFileChecksums(BlockChecksumEngine& engine, const uint8_t* host_file,
+                              uint64_t file_size, const uint8_t* dev_file,
+                              const std::string& file_name, SstVerifyReport* report = nullptr);
 
 }  // namespace forstdb

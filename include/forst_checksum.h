@@ -88,6 +88,8 @@ enum forst_checksum_type {
 #define FORST_EUNSUPPORTED (-2)  /* reserved: ChecksumType not handled (all 5 are) */
 #define FORST_EHIP (-3)          /* HIP runtime error (see forst_last_error) */
 #define FORST_ENODEV (-4)        /* no gfx950 device / code object not loadable */
+#define FORST_ECORRUPT (-5)      /* corrupt file structure (SST footer / block format);
+                                    message in forst_sst_last_error() */
 
 /* WAL per-log-block status (forst_wal_verify_batch) -- mirrors the reader's
  * outcomes of ReadPhysicalRecord (db/log_reader.h kBadRecord*, kEof). */
@@ -243,6 +245,74 @@ int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
 /* Kernel timing hooks for bench.py: name of the kernel launched by the last
  * call on this thread and the launch configuration used. */
 const char* forst_last_kernel(void);
+
+/* ---- SST files (BlockBasedTable::VerifyChecksum, ----------------------------
+ * table/block_based/block_based_table_reader.cc:2457-2574) ----------------- */
+
+/* Footer::DecodeFrom (table/format.cc:355-463): every footer version of the
+ * block-based table (legacy magic = format_version 0, 1..6).  For
+ * format_version >= 6 the footer checksum is ComputeBuiltinChecksum(type,
+ * footer_zeroed, 53) + footer_checksum_modifier and must equal
+ * stored_footer_checksum (the verify entry point below checks it on the GPU). */
+typedef struct forst_sst_footer {
+  uint64_t table_magic_number;
+  uint64_t footer_offset;
+  uint64_t metaindex_offset, metaindex_size;
+  uint64_t index_offset, index_size; /* 0, 0 when in the metaindex (fv >= 6) */
+  uint32_t format_version;
+  int32_t checksum_type;
+  uint32_t base_context_checksum;
+  uint32_t stored_footer_checksum;
+  uint32_t footer_checksum_modifier;
+  uint32_t block_trailer_size;
+  uint32_t footer_len;
+  uint8_t footer_zeroed[53];
+} forst_sst_footer;
+
+/* Table properties the checksum walk needs (table/meta_blocks.cc:81-140,
+ * block_based_table_reader.cc:948-972). index_type: 0 kBinarySearch,
+ * 1 kHashSearch, 2 kTwoLevelIndexSearch, 3 kBinarySearchWithFirstKey. */
+typedef struct forst_sst_properties {
+  uint32_t index_type;
+  uint64_t index_value_is_delta_encoded;
+  uint64_t index_key_is_user_key;
+  uint64_t num_data_blocks;
+  uint64_t index_partitions;
+  uint64_t format_version;
+  uint64_t data_size;
+} forst_sst_properties;
+
+typedef struct forst_sst_verify_result {
+  int32_t status; /* forstdb::Status::Code: 0 OK, 2 Corruption, 3 NotSupported, ... */
+  uint32_t format_version;
+  int32_t checksum_type;
+  uint32_t index_type;
+  uint64_t blocks_verified; /* block checksums computed on the GPU */
+  uint64_t data_blocks, meta_blocks, index_partitions;
+  uint64_t n_failed;
+  char message[512]; /* Status::ToString(), the reference's Corruption text */
+} forst_sst_verify_result;
+
+/* Host utilities (no GPU call). tail = the last tail_len (<= 53) bytes of a
+ * file of file_size bytes. */
+int forst_sst_footer_decode(const uint8_t* tail, uint64_t tail_len, uint64_t file_size,
+                            forst_sst_footer* out);
+/* Block handles of an index block / index partition (IndexValue,
+ * table/format.cc:105-148; value delta encoding, optional first key). */
+int forst_sst_index_handles(const uint8_t* block, uint64_t block_size, int value_delta_encoded,
+                            int has_first_key, uint64_t* offsets, uint64_t* sizes,
+                            uint64_t capacity, uint64_t* n);
+int forst_sst_properties_decode(const uint8_t* block, uint64_t block_size,
+                                forst_sst_properties* out);
+const char* forst_sst_last_error(void);
+
+/* Whole-file verify: host_file = the file bytes in host memory (structure is
+ * decoded there), dev_file = the same bytes in device memory (every checksum
+ * -- footer, metaindex, properties, index, partitions, all meta and data
+ * blocks -- is computed on the GPU).  The result carries the reference's
+ * Status for the first failure in VerifyChecksum's order. Synchronous. */
+int forst_sst_verify_file(const uint8_t* host_file, uint64_t file_size, const uint8_t* dev_file,
+                          const char* file_name, forst_sst_verify_result* out, void* stream);
 
 #ifdef __cplusplus
 }

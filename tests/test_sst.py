@@ -1,0 +1,198 @@
+"""Whole-SST-file checksum verification (§8f-1, BlockBasedTable::VerifyChecksum,
+block_based_table_reader.cc:2457-2574).
+
+CPU: host decoders (footer of every format version, index blocks with and
+without value delta encoding / first keys, partitions, properties) against
+the files tests/sstgen.py writes, and the reference's footer error texts.
+GPU: forst_sst_verify_file over whole files -- every checksum on the device
+-- returns OK with the right block counts, and for injected corruption the
+reference's exact Status text of the first failing block.
+
+File-level layout parity is unpinned (tests/sstgen.py header); every block
+checksum is pinned through the oracle."""
+import struct
+
+import numpy as np
+import pytest
+
+import sstgen
+from forst_amd import sst
+from oracle import oracle as O
+
+CASES = [  # (fv, ctype, index_type, restart_interval)
+    (0, 1, 0, 1), (1, 2, 0, 1), (2, 3, 0, 1), (3, 4, 1, 1), (4, 1, 0, 4), (5, 4, 3, 1),
+    (5, 1, 2, 1), (5, 3, 3, 4), (6, 1, 0, 1), (6, 4, 2, 4), (6, 2, 3, 1), (6, 0, 0, 1),
+]
+
+
+def make(fv, ct, it, ri, seed=3, **kw):
+    w = sstgen.SstWriter(fv=fv, ctype=ct, index_type=it, base_context=0x5EED1234 + seed,
+                         restart_interval=ri, seed=seed)
+    return w, w.build(**kw)
+
+
+def blocks_of(w, kind):
+    return [(o, n) for k, o, n in w.blocks if k == kind]
+
+
+@pytest.mark.parametrize("fv,ct,it,ri", CASES)
+def test_host_decoders(fv, ct, it, ri):
+    w, f = make(fv, ct, it, ri)
+    ft = sst.decode_footer(f)
+    assert ft.format_version == fv
+    assert ft.checksum_type == (1 if fv == 0 else ct)
+    mi = blocks_of(w, "metaindex")[0]
+    assert (ft.metaindex_offset, ft.metaindex_size) == mi
+    ix = blocks_of(w, "index")[0]
+    if fv < 6:
+        assert (ft.index_offset, ft.index_size) == ix
+        assert ft.base_context_checksum == 0
+    else:
+        assert ft.base_context_checksum == w.bcc
+        assert ft.footer_offset == w.footer_offset
+        assert ft.footer_checksum_modifier == O.checksum_modifier_for_context(w.bcc, w.footer_offset)
+    pr = blocks_of(w, "properties")[0]
+    p = sst.properties(f[pr[0]:pr[0] + pr[1]])
+    assert p.index_type == it and p.num_data_blocks == 40
+    assert p.index_value_is_delta_encoded == (1 if fv >= 4 else 0)
+    offs, sizes = sst.index_handles(f[ix[0]:ix[0] + ix[1]], p.index_value_is_delta_encoded,
+                                    it == 3)
+    want = blocks_of(w, "partition" if it == 2 else "data")
+    assert list(zip(offs.tolist(), sizes.tolist())) == want
+    if it == 2:
+        got = []
+        for o, n in want:
+            po, ps = sst.index_handles(f[o:o + n], p.index_value_is_delta_encoded, False)
+            got += list(zip(po.tolist(), ps.tolist()))
+        assert got == blocks_of(w, "data")
+
+
+def test_footer_errors():
+    w, f = make(6, 1, 0, 1)
+    f = bytearray(f)
+    with pytest.raises(sst.SstCorruption, match="too short"):
+        sst.decode_footer(bytes(20))
+    bad = bytearray(f)
+    bad[-12:-8] = struct.pack("<I", 9)
+    with pytest.raises(sst.SstCorruption, match="Corrupt or unsupported format_version: 9"):
+        sst.decode_footer(bad)
+    bad = bytearray(f)
+    bad[-53] = 7
+    with pytest.raises(sst.SstCorruption, match="Corrupt or unsupported checksum type: 7"):
+        sst.decode_footer(bad)
+    bad = bytearray(f)
+    bad[-52] = 0x3f
+    with pytest.raises(sst.SstCorruption, match="Bad extended magic number: 0x3F007A00"):
+        sst.decode_footer(bad)
+    bad = bytearray(f)
+    bad[-44:-40] = bytes(4)
+    with pytest.raises(sst.SstCorruption, match="Invalid base context checksum"):
+        sst.decode_footer(bad)
+    bad = bytearray(f)
+    bad[-8:] = struct.pack("<Q", 0x8242229663BF9564)  # plain table: no block checksums
+    with pytest.raises(Exception, match="not a block-based table"):
+        sst.decode_footer(bad)
+
+
+def test_index_block_errors():
+    w, f = make(5, 1, 0, 1)
+    ix = blocks_of(w, "index")[0]
+    blk = bytearray(f[ix[0]:ix[0] + ix[1]])
+    blk[-4:] = struct.pack("<I", 10**6)  # num_restarts past the block
+    with pytest.raises(sst.SstCorruption):
+        sst.index_handles(bytes(blk), True)
+
+
+# ---------------------------------------------------------------- GPU ----
+
+def _expected_mismatch(w, f, off, n, fname):
+    """reader_common.cc:50-60 message for the block at off"""
+    ct = w.ctype
+    stored = struct.unpack("<I", f[off + n + 1:off + n + 5])[0]
+    mod = O.checksum_modifier_for_context(w.bcc, off)
+    stored = (stored - mod) & 0xFFFFFFFF
+    computed = O.compute_builtin_checksum(ct, f[off:off + n + 1])
+    if ct == 1:
+        stored, computed = O.unmask(stored), O.unmask(computed)
+    ctx = "(context removed)" if mod else ""
+    return (f"Corruption: block checksum mismatch: stored{ctx} = {stored}, computed = "
+            f"{computed}, type = {ct}  in {fname} offset {off} size {n}")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,ct,it,ri", CASES)
+def test_verify_file_ok(fv, ct, it, ri):
+    w, f = make(fv, ct, it, ri)
+    r = sst.verify_file(f, file_name="000042.sst")
+    assert r.status == 0, r.message
+    assert r.data_blocks == 40 and r.n_failed == 0
+    assert r.format_version == fv and r.index_type == it
+    n_meta = 1 + (fv >= 6)  # filter (+ rocksdb.index)
+    assert r.meta_blocks == n_meta
+    assert r.index_partitions == (5 if it == 2 else 0)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,ct,it,ri", [(5, 1, 0, 1), (6, 4, 2, 4), (6, 1, 3, 1), (2, 3, 0, 1)])
+def test_verify_file_corruption(fv, ct, it, ri):
+    name = "/db/000777.sst"
+    w, f = make(fv, ct, it, ri, seed=9)
+    data = blocks_of(w, "data")
+    # data blocks 7 and 30 corrupted: the first is reported, both counted
+    b = bytearray(f)
+    for i in (7, 30):
+        o, n = data[i]
+        b[o + n // 2] ^= 0x20
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.status == 2 and r.n_failed == 2
+    o, n = data[7]
+    assert r.message.decode() == _expected_mismatch(w, bytes(b), o, n, name)
+    # a stored checksum byte
+    b = bytearray(f)
+    o, n = data[39]
+    b[o + n + 2] ^= 1
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.message.decode() == _expected_mismatch(w, bytes(b), o, n, name)
+    # the filter (meta) block is checked before any data block
+    b = bytearray(f)
+    fo, fn = blocks_of(w, "filter")[0]
+    b[fo + 3] ^= 4
+    o, n = data[0]
+    b[o] ^= 4
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.n_failed == 2
+    assert r.message.decode() == _expected_mismatch(w, bytes(b), fo, fn, name)
+    # the index block is read (and verified) before its entries are trusted
+    b = bytearray(f)
+    io, in_ = blocks_of(w, "index")[0]
+    b[io + in_ - 6] ^= 0x80
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.status == 2
+    assert r.message.decode() == _expected_mismatch(w, bytes(b), io, in_, name)
+
+
+@pytest.mark.gpu
+def test_verify_file_footer_checksum():
+    name = "x.sst"
+    for ct in (0, 1, 4):
+        w, f = make(6, ct, 0, 1)
+        b = bytearray(f)
+        b[-30] ^= 1  # reserved (unchecked) padding, covered by the footer checksum
+        r = sst.verify_file(bytes(b), file_name=name)
+        if ct == 0:  # kNoChecksum: computed = 0 + modifier, padding not covered
+            assert r.status == 0, r.message
+            b = bytearray(f)
+            b[-47] ^= 1  # the stored footer checksum itself
+            r = sst.verify_file(bytes(b), file_name=name)
+        assert r.status == 2
+        assert r.message.decode() == (f"Corruption: Footer at {w.footer_offset} checksum "
+                                      f"mismatch in {name}")
+
+
+@pytest.mark.gpu
+def test_verify_file_large():
+    """2000 data blocks, partitioned index, fv6 kXXH3"""
+    w, f = make(6, 4, 2, 1, seed=5, n_data=2000, partition_size=64)
+    r = sst.verify_file(f, file_name="big.sst")
+    assert r.status == 0 and r.data_blocks == 2000, r.message
+    assert r.index_partitions == 32

@@ -191,6 +191,17 @@ def run_wal(steps, warmup, n_records=10_000_000):
     torch.cuda.synchronize()
     assert int(bad.item()) == 0, "WAL blocks failed verification in the timed region"
     assert int(nrec.sum().item()) == len(w.rec_offsets)
+    # a14: XXH3 of every logical record (gather of multi-fragment records +
+    # two raw XXH3 batches); includes its one stream synchronisation
+    hs = []
+    for _ in range(max(2, steps // 2)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        hh, _ = engine.wal_record_xxh3_batch(w.log, offs)
+        torch.cuda.synchronize()
+        hs.append(time.perf_counter() - t0)
+    assert hh.numel() == w.n_records
+    t_h = float(np.median(hs))
     t_w = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
     t_v = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
     rec_bytes = int(w.rec_lengths.astype(np.int64).sum()) + 7 * len(w.rec_offsets)
@@ -203,7 +214,9 @@ def run_wal(steps, warmup, n_records=10_000_000):
            "verify_roofline_frac": round(alg_v / t_v / 1e9 / HBM_PEAK_GBS, 4),
            "writer_crc_GiBps": round(rec_bytes / t_w / GIB, 1),
            "writer_crc_ms": round(t_w * 1e3, 3),
-           "writer_roofline_frac": round(alg_w / t_w / 1e9 / HBM_PEAK_GBS, 4)}
+           "writer_roofline_frac": round(alg_w / t_w / 1e9 / HBM_PEAK_GBS, 4),
+           "record_xxh3_GiBps": round(rec_bytes / t_h / GIB, 1),
+           "record_xxh3_ms": round(t_h * 1e3, 3)}
     del w
     return out
 

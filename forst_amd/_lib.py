@@ -53,6 +53,7 @@ def lib():
         "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_buffer": (i, [vp, u64, u32, vp, vp]),
+        "forst_wal_record_xxh3_batch": (i, [vp, u64, vp, u64, vp, vp, vp, vp]),
         "forst_sst_footer_decode": (i, [vp, u64, u64, vp]),
         "forst_sst_index_handles": (i, [vp, u64, i, i, vp, vp, u64, vp]),
         "forst_sst_properties_decode": (i, [vp, u64, vp]),

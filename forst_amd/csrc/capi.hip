@@ -250,6 +250,27 @@ FORST_API int forst_crc32c_batch(const uint8_t* base, uint64_t base_len,
   return dispatch_blocks(FORST_kCRC32c, kModeRaw, a, stream);
 }
 
+FORST_API int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
+                                          const uint64_t* header_offsets, uint64_t n_phys,
+                                          uint64_t* hashes, uint64_t* first_phys,
+                                          uint64_t* n_logical, void* stream) {
+  if (!n_logical) return set_error(FORST_EINVAL, "n_logical must be non-null");
+  *n_logical = 0;
+  if (n_phys == 0) return FORST_OK;
+  if (!log || !aligned4(log) || !header_offsets || !hashes)
+    return set_error(FORST_EINVAL, "log/header_offsets/hashes must be non-null, log 4-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  WalArgs a{};
+  a.log = log;
+  a.log_len = log_len;
+  a.header_offsets = header_offsets;
+  a.n_records = n_phys;
+  return hip_status(launch_wal_record_xxh3(a, hashes, first_phys, n_logical,
+                                           static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "wal_record_xxh3 launch");
+}
+
 FORST_API int forst_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
                                   void* stream) {
   if (!out || (len && (!base || !aligned4(base))))

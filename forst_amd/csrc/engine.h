@@ -116,6 +116,9 @@ hipError_t launch_crc32c_combine_batch(const uint32_t* crc1, const uint32_t* crc
                                        hipStream_t stream, const char** kernel_name);
 hipError_t launch_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
                                 hipStream_t stream, const char** kernel_name);
+hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out_first,
+                                  uint64_t* n_logical_host, hipStream_t stream,
+                                  const char** kernel_name);
 hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n,
                               uint64_t seed, hipStream_t stream);

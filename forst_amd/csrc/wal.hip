@@ -247,6 +247,183 @@ __global__ void __launch_bounds__(kTile) wal_rec_finish_kernel(WalArgs a, const 
   if (a.crc_out) a.crc_out[i] = c;
 }
 
+// ---- a14: XXH3 of logical records (log_reader.cc:95-165) --------------------
+// A logical record is a kFullType fragment, or kFirstType + kMiddleType* +
+// kLastType; the reader hashes it with XXH3_64bits (full) or the streaming API
+// over the fragments (= XXH3_64bits of their concatenation).  Full records are
+// hashed in place; the fragments of multi-fragment records are gathered into
+// one contiguous scratch run per record first.
+
+__device__ __forceinline__ uint32_t norm_type(uint32_t t) {  // recyclable -> legacy
+  return (t >= 5 && t <= 8) ? t - 4 : t;
+}
+
+struct FragInfo {
+  uint64_t off;  // payload offset in the log
+  uint32_t len, type;
+  bool ok;
+};
+
+__device__ __forceinline__ FragInfo frag_info(const WalArgs& a, uint64_t i) {
+  FragInfo f{0, 0, 0, false};
+  const uint64_t off = a.header_offsets[i];
+  if (off <= a.log_len && a.log_len - off >= kLogHdr) {
+    const uint8_t* h = a.log + off;
+    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
+    const uint32_t hs = recyclable_type(h[6]) ? kLogRHdr : kLogHdr;
+    if (a.log_len - off >= uint64_t(hs) + length) {
+      f.off = off + hs;
+      f.len = length;
+      f.type = norm_type(h[6]);
+      f.ok = f.type >= 1 && f.type <= 4;
+    }
+  }
+  return f;
+}
+
+// u64 exclusive scan in three passes: tile sums, one-workgroup scan of the
+// tile sums, tile-local scans plus tile prefix
+__global__ void __launch_bounds__(kTile) scan_tiles_kernel(const uint64_t* in, uint64_t n,
+                                                           uint64_t* tile_sum) {
+  __shared__ uint64_t sh[kTile];
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  sh[threadIdx.x] = i < n ? in[i] : 0;
+  __syncthreads();
+  for (uint32_t d = kTile / 2; d >= 1; d >>= 1) {
+    if (threadIdx.x < d) sh[threadIdx.x] += sh[threadIdx.x + d];
+    __syncthreads();
+  }
+  if (threadIdx.x == 0) tile_sum[blockIdx.x] = sh[0];
+}
+
+__global__ void __launch_bounds__(kScanThreads) scan_top_kernel(uint64_t* tile_sum,
+                                                                uint64_t n_tiles) {
+  __shared__ uint64_t sh[kScanThreads];
+  const uint32_t t = threadIdx.x;
+  uint64_t carry = 0;
+  for (uint64_t c0 = 0; c0 < n_tiles; c0 += kScanThreads) {
+    const uint64_t i = c0 + t;
+    const uint64_t v = i < n_tiles ? tile_sum[i] : 0;
+    sh[t] = v;
+    __syncthreads();
+    for (uint32_t d = 1; d < kScanThreads; d <<= 1) {
+      const uint64_t add = t >= d ? sh[t - d] : 0;
+      __syncthreads();
+      sh[t] += add;
+      __syncthreads();
+    }
+    if (i < n_tiles) tile_sum[i] = carry + sh[t] - v;  // in place: exclusive prefix
+    carry += sh[kScanThreads - 1];
+    __syncthreads();
+  }
+  if (t == 0) tile_sum[n_tiles] = carry;
+}
+
+__global__ void __launch_bounds__(kTile) scan_apply_kernel(const uint64_t* in, uint64_t n,
+                                                           const uint64_t* tile_prefix,
+                                                           uint64_t* out) {
+  __shared__ uint64_t sh[kTile];
+  const uint32_t t = threadIdx.x;
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + t;
+  const uint64_t v = i < n ? in[i] : 0;
+  sh[t] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < kTile; d <<= 1) {
+    const uint64_t add = t >= d ? sh[t - d] : 0;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  if (i < n) out[i] = tile_prefix[blockIdx.x] + sh[t] - v;
+}
+
+// start flags (kFullType / kFirstType)
+__global__ void __launch_bounds__(kTile) rec_start_kernel(WalArgs a, uint64_t* start) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i >= a.n_records) return;
+  const FragInfo f = frag_info(a, i);
+  start[i] = f.ok && (f.type == 1 || f.type == 2) ? 1 : 0;
+}
+
+// per logical record: first fragment and kind; per fragment: gathered length
+// (payload bytes of fragments owned by a kFirstType record, else 0)
+__global__ void __launch_bounds__(kTile) rec_owner_kernel(WalArgs a, const uint64_t* start,
+                                                          const uint64_t* lid_excl,
+                                                          uint64_t* first_phys, uint8_t* kind,
+                                                          uint64_t* glen) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i >= a.n_records) return;
+  const FragInfo f = frag_info(a, i);
+  if (start[i]) {
+    first_phys[lid_excl[i]] = i;
+    kind[lid_excl[i]] = static_cast<uint8_t>(f.type);
+  }
+  // the owner is the last start at or before i (lid_excl + start - 1)
+  const uint64_t owned = lid_excl[i] + start[i];
+  // provisional: every non-full fragment with an owner; rec_orphan_kernel
+  // clears the ones whose owner turns out to be a kFullType record
+  glen[i] = owned > 0 && f.ok && f.type != 1 ? f.len : 0;
+}
+
+// orphans after a kFullType owner are not gathered
+__global__ void __launch_bounds__(kTile) rec_orphan_kernel(WalArgs a, const uint64_t* start,
+                                                           const uint64_t* lid_excl,
+                                                           const uint8_t* kind, uint64_t* glen) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i >= a.n_records) return;
+  const uint64_t owned = lid_excl[i] + start[i];
+  if (owned == 0 || kind[owned - 1] != 2) glen[i] = 0;
+}
+
+// gather fragment payloads (one workgroup per fragment, byte lanes coalesced)
+__global__ void __launch_bounds__(kTile) rec_gather_kernel(WalArgs a, const uint64_t* glen,
+                                                           const uint64_t* goff, uint8_t* dst) {
+  for (uint64_t i = blockIdx.x; i < a.n_records; i += gridDim.x) {
+    const uint64_t n = glen[i];
+    if (n == 0) continue;
+    const FragInfo f = frag_info(a, i);
+    const uint8_t* src = a.log + f.off;
+    uint8_t* d = dst + goff[i];
+    for (uint64_t k = threadIdx.x; k < n; k += kTile) d[k] = src[k];
+  }
+}
+
+// descriptors per logical record: full records in place (batch A, base =
+// log), gathered records in scratch (batch B); the other batch gets length 0
+__global__ void __launch_bounds__(kTile) rec_desc_kernel(WalArgs a, uint64_t n_logical,
+                                                         const uint64_t* first_phys,
+                                                         const uint8_t* kind,
+                                                         const uint64_t* goff, uint64_t gtotal,
+                                                         uint64_t* a_off, uint32_t* a_len,
+                                                         uint64_t* b_off, uint32_t* b_len) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (j >= n_logical) return;
+  const uint64_t i = first_phys[j];
+  const FragInfo f = frag_info(a, i);
+  a_off[j] = 0;
+  a_len[j] = 0;
+  b_off[j] = 0;
+  b_len[j] = 0;
+  if (kind[j] == 1) {
+    a_off[j] = f.off;
+    a_len[j] = f.len;
+  } else {
+    const uint64_t end = j + 1 < n_logical ? goff[first_phys[j + 1]] : gtotal;
+    b_off[j] = goff[i];
+    b_len[j] = static_cast<uint32_t>(end - goff[i]);
+  }
+}
+
+__global__ void __launch_bounds__(kTile) rec_select_kernel(uint64_t n_logical, const uint8_t* kind,
+                                                           const uint64_t* ha, const uint64_t* hb,
+                                                           const uint64_t* first_phys,
+                                                           uint64_t* out, uint64_t* out_first) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (j >= n_logical) return;
+  out[j] = kind[j] == 1 ? ha[j] : hb[j];
+  if (out_first) out_first[j] = first_phys[j];
+}
+
 size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
 bool wave_variant() {
@@ -336,6 +513,96 @@ hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream, const cha
   if (e == hipSuccess) e = hipGetLastError();
   const hipError_t f = scratch_free(scratch, stream);
   return e != hipSuccess ? e : f;
+}
+
+}  // namespace forst
+
+namespace forst {
+
+hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out_first,
+                                  uint64_t* n_logical_host, hipStream_t stream,
+                                  const char** name) {
+  *n_logical_host = 0;
+  if (a.n_records == 0) return hipSuccess;
+  const uint64_t n = a.n_records, nt = (n + kTile - 1) / kTile;
+  const dim3 grid(static_cast<uint32_t>(nt));
+  // scratch: start, lid, glen, goff (u64 x n), first_phys (u64 x n), kind (u8 x n),
+  // tile sums (u64 x nt + 1), hashes A/B (u64 x n), descriptors (12 B x n x 2)
+  const size_t s8 = up256(8 * n), s1 = up256(n), st = up256(8 * (nt + 1)), s4 = up256(4 * n);
+  void* scratch = nullptr;
+  hipError_t e = scratch_alloc(&scratch, 7 * s8 + s1 + st + 2 * s8 + 2 * s4, stream);
+  if (e != hipSuccess) return e;
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint64_t* start = reinterpret_cast<uint64_t*>(p);
+  uint64_t* lid = reinterpret_cast<uint64_t*>(p + s8);
+  uint64_t* glen = reinterpret_cast<uint64_t*>(p + 2 * s8);
+  uint64_t* goff = reinterpret_cast<uint64_t*>(p + 3 * s8);
+  uint64_t* first = reinterpret_cast<uint64_t*>(p + 4 * s8);
+  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 5 * s8);
+  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 6 * s8);
+  uint8_t* kind = p + 7 * s8;
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 7 * s8 + s1);
+  uint64_t* a_off = reinterpret_cast<uint64_t*>(p + 7 * s8 + s1 + st);
+  uint64_t* b_off = reinterpret_cast<uint64_t*>(p + 8 * s8 + s1 + st);
+  uint32_t* a_len = reinterpret_cast<uint32_t*>(p + 9 * s8 + s1 + st);
+  uint32_t* b_len = reinterpret_cast<uint32_t*>(p + 9 * s8 + s1 + st + s4);
+  auto scan = [&](const uint64_t* in, uint64_t* outx) {
+    hipLaunchKernelGGL(scan_tiles_kernel, grid, dim3(kTile), 0, stream, in, n, tiles);
+    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanThreads), 0, stream, tiles, nt);
+    hipLaunchKernelGGL(scan_apply_kernel, grid, dim3(kTile), 0, stream, in, n, tiles, outx);
+  };
+  hipLaunchKernelGGL(rec_start_kernel, grid, dim3(kTile), 0, stream, a, start);
+  scan(start, lid);
+  uint64_t n_logical = 0, gtotal = 0;
+  if ((e = hipMemcpyAsync(&n_logical, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess) {
+    (void)scratch_free(scratch, stream);
+    return e;
+  }
+  hipLaunchKernelGGL(rec_owner_kernel, grid, dim3(kTile), 0, stream, a, start, lid, first, kind,
+                     glen);
+  hipLaunchKernelGGL(rec_orphan_kernel, grid, dim3(kTile), 0, stream, a, start, lid, kind, glen);
+  scan(glen, goff);
+  if ((e = hipMemcpyAsync(&gtotal, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess) {
+    (void)scratch_free(scratch, stream);
+    return e;
+  }
+  void* gbuf = nullptr;
+  if ((e = scratch_alloc(&gbuf, up256(gtotal + 256), stream)) != hipSuccess) {
+    (void)scratch_free(scratch, stream);
+    return e;
+  }
+  uint8_t* g = static_cast<uint8_t*>(gbuf);
+  const uint32_t ggrid = static_cast<uint32_t>(n < 65536 ? n : 65536);
+  hipLaunchKernelGGL(rec_gather_kernel, dim3(ggrid), dim3(kTile), 0, stream, a, glen, goff, g);
+  const dim3 lgrid(static_cast<uint32_t>((n_logical + kTile - 1) / kTile));
+  if (n_logical) {
+    hipLaunchKernelGGL(rec_desc_kernel, lgrid, dim3(kTile), 0, stream, a, n_logical, first, kind,
+                       goff, gtotal, a_off, a_len, b_off, b_len);
+    BlockArgs ba{};
+    ba.base = a.log;
+    ba.base_len = a.log_len;
+    ba.offsets = a_off;
+    ba.sizes = a_len;
+    ba.out64 = ha;
+    ba.n = n_logical;
+    e = launch_xxh3_blocks(kModeRaw, ba, stream, name);
+    if (e == hipSuccess) {
+      BlockArgs bb = ba;
+      bb.base = g;
+      bb.base_len = up256(gtotal + 256);
+      bb.offsets = b_off;
+      bb.sizes = b_len;
+      bb.out64 = hb;
+      e = launch_xxh3_blocks(kModeRaw, bb, stream, name);
+    }
+    hipLaunchKernelGGL(rec_select_kernel, lgrid, dim3(kTile), 0, stream, n_logical, kind, ha, hb,
+                       first, out, out_first);
+  }
+  if (e == hipSuccess) e = hipGetLastError();
+  *n_logical_host = n_logical;
+  const hipError_t f1 = scratch_free(gbuf, stream), f2 = scratch_free(scratch, stream);
+  return e != hipSuccess ? e : f1 != hipSuccess ? f1 : f2;
 }
 
 }  // namespace forst

@@ -7,6 +7,7 @@ forst_amd/lib/libforst_checksum.so.  Device buffers are torch CUDA tensors
 (torch is only plumbing for device memory and streams).  Calls are enqueued on
 torch's current stream.
 """
+import ctypes
 import enum
 
 import torch
@@ -200,6 +201,20 @@ def wal_record_crc_batch(log, header_offsets, write_in_place=True, out=None, str
                                            header_offsets.data_ptr(), n, int(write_in_place),
                                            out.data_ptr(), _stream(stream)))
     return out
+
+
+def wal_record_xxh3_batch(log, header_offsets, stream=None):
+    """XXH3_64bits per logical record (log_reader.cc:95-165).  Returns
+    (hashes int64 [n_logical], first physical record index [n_logical])."""
+    _dev_u8(log)
+    n = header_offsets.numel()
+    hashes = torch.empty(max(n, 1), dtype=torch.int64, device=log.device)
+    first = torch.empty(max(n, 1), dtype=torch.int64, device=log.device)
+    nl = ctypes.c_uint64()
+    check(lib().forst_wal_record_xxh3_batch(log.data_ptr(), log.numel(), header_offsets.data_ptr(),
+                                            n, hashes.data_ptr(), first.data_ptr(),
+                                            ctypes.byref(nl), _stream(stream)))
+    return hashes[:nl.value], first[:nl.value]
 
 
 def hash64_batch(base, offsets, lengths, seeds=None, seed=0, out=None, stream=None):

@@ -37,6 +37,8 @@
  *                                  log block
  *   forst_wal_record_crc_batch  <- log::Writer::EmitPhysicalRecord CRC
  *                                  (db/log_writer.cc:228-263)
+ *   forst_wal_record_xxh3_batch <- log::Reader::ReadRecord record checksum
+ *                                  XXH3 (db/log_reader.cc:95-165)
  *   forst_hash64_batch          <- Hash64 / NPHash64 (util/hash.cc:81-88)
  *   forst_kv_protect_batch      <- ProtectionInfo64 ProtectKV[O][S|C]
  *                                  (db/kv_checksum.h:296-460)
@@ -187,6 +189,21 @@ int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                                const uint64_t* header_offsets,
                                uint64_t n_records, int write_in_place,
                                uint32_t* crc_out, void* stream);
+
+/* XXH3_64bits of every logical record (log::Reader::ReadRecord record
+ * checksum, db/log_reader.cc:95-165, compared by WriteBatchInternal::
+ * UpdateProtectionInfo, db/write_batch.cc:3164-3181).  header_offsets = the
+ * physical records in log order (e.g. from forst_wal_layout); a logical
+ * record is a kFullType fragment or kFirstType + kMiddleType* + kLastType
+ * (recyclable types alike), hashed as the concatenation of its payloads.
+ * hashes[j] / first_phys[j] (device, capacity n_phys; first_phys nullable)
+ * for j < *n_logical (host).  Synchronises the stream once.  Defined for the
+ * fragment sequences log::Writer emits; malformed sequences are the reader's
+ * corruption path (forst_wal_verify_batch). */
+int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
+                                const uint64_t* header_offsets, uint64_t n_phys,
+                                uint64_t* hashes, uint64_t* first_phys, uint64_t* n_logical,
+                                void* stream);
 
 /* Host utility (no GPU call): the physical-record layout log::Writer::AddRecord
  * produces for logical records of the given lengths (db/log_writer.cc:65-160,

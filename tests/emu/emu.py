@@ -30,6 +30,7 @@ def lib():
             "forst_block_verify_batch": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
                 "forst_crc32c_batch": (i, [vp, u64, vp, vp, vp, vp, u64, vp]),
             "forst_crc32c_buffer": (i, [vp, u64, u32, vp, vp]),
+            "forst_wal_record_xxh3_batch": (i, [vp, u64, vp, u64, vp, vp, vp, vp]),
             "forst_crc32c_combine": (u32, [u32, u32, u64]),
             "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
             "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
@@ -135,6 +136,17 @@ def crc32c_buffer(base, init=0):
     out = np.zeros(1, np.uint32)
     _chk(lib().forst_crc32c_buffer(_p(base), base.nbytes, init, _p(out), None))
     return int(out[0])
+
+
+def wal_record_xxh3(log, header_offsets):
+    log = _aligned(log)
+    offs = np.ascontiguousarray(header_offsets, dtype=np.uint64)
+    h = np.zeros(max(1, len(offs)), np.uint64)
+    first = np.zeros(max(1, len(offs)), np.uint64)
+    nl = ctypes.c_uint64()
+    _chk(lib().forst_wal_record_xxh3_batch(_p(log), log.nbytes, _p(offs), len(offs), _p(h),
+                                           _p(first), ctypes.byref(nl), None))
+    return h[:nl.value], first[:nl.value]
 
 
 def wal_record_crc(log, header_offsets, write_in_place=True):

@@ -268,3 +268,20 @@ def test_emu_crc32c_buffer():
     for n in (0, 1, 63, 65535, 65536, 65537, 2 * 65536 + 5, len(buf)):
         for init in (0, 0xDEADBEEF):
             assert emu.crc32c_buffer(buf[:n], init) == O.crc32c_extend(init, buf[:n].tobytes())
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_emu_wal_record_xxh3(recyclable):
+    """a14: XXH3 of each logical record = XXH3 of its payload, whether one
+    fragment or First/Middle*/Last across log blocks"""
+    rng = np.random.default_rng(12)
+    lens = rng.integers(0, 3000, 40).astype(np.uint32)
+    lens[[3, 10, 20]] = [70000, 32761, 40000]
+    lens[5] = 0
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=recyclable, log_number=3)
+    h, first = emu.wal_record_xxh3(buf, poffs)
+    assert len(h) == len(lens)
+    starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    for j in range(len(lens)):
+        assert int(h[j]) == O.xxh3_64(payload[starts[j]:starts[j + 1]].tobytes()), j

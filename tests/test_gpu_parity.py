@@ -536,3 +536,39 @@ def test_crc32c_combine_batch_vs_oracle():
     want = np.array([O.crc32c_combine(int(a), int(b), int(c)) for a, b, c in zip(c1, c2, ln)],
                     np.uint32)
     assert (got == want).all()
+
+
+# ---- a14: XXH3 of logical WAL records -------------------------------------
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_record_xxh3(recyclable):
+    rng = np.random.default_rng(21)
+    lens = workload.log_uniform_lengths(3000, 1, 100000, 0xF0E5700005)
+    lens[:5] = [0, 32761, 32762, 65536 * 3, 1]
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=recyclable, log_number=77)
+    h, first = engine.wal_record_xxh3_batch(d(buf), d(poffs.astype(np.int64)))
+    h = host(h).view(np.uint64)
+    assert len(h) == len(lens)
+    starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    want = np.array([O.xxh3_64(payload[starts[j]:starts[j + 1]].tobytes())
+                     for j in range(len(lens))], np.uint64)
+    assert (h == want).all()
+
+
+def test_full_size_c5_record_xxh3():
+    """10 M logical records of C5: count, first fragments against the writer's
+    layout, 2000 sampled hashes against the oracle over the gathered bytes"""
+    w = workload.make_wal_batch(10_000_000, workload.SEEDS["C5"])
+    h, first = engine.wal_record_xxh3_batch(w.log, torch.from_numpy(
+        w.rec_offsets.view(np.int64)).to(DEV))
+    assert h.numel() == w.n_records
+    starts = np.nonzero((w.rec_types == 1) | (w.rec_types == 2))[0]
+    assert (host(first) == starts).all()
+    hh = host(h).view(np.uint64)
+    rng = np.random.default_rng(3)
+    ends = np.concatenate([starts[1:], [len(w.rec_offsets)]])
+    for j in rng.choice(w.n_records, 2000, replace=False):
+        parts = [host(w.log[int(w.rec_offsets[i]) + 7:int(w.rec_offsets[i]) + 7 +
+                            int(w.rec_lengths[i])]) for i in range(starts[j], ends[j])]
+        assert int(hh[j]) == O.xxh3_64(np.concatenate(parts).tobytes()), j

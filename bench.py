@@ -303,6 +303,7 @@ def end_to_end_pcie(b, ctype, chunk_blocks=1 << 16):
 def load_traffic(kernel_name, config):
     """HBM traffic per launch from the committed rocprofv3 PMC summary
     (profiles/*pmc*.json written by profiles/collect_pmc.py), or None."""
+    parts = kernel_name.split("+")  # a pass of several kernels: sum of their traffic
     best = None
     for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
         try:
@@ -310,9 +311,13 @@ def load_traffic(kernel_name, config):
                 d = json.load(fh)
         except Exception:
             continue
+        got = {}
         for row in d.get("kernels", []):
-            if row.get("config") == config and row.get("kernel", "").startswith(kernel_name):
-                best = row.get("hbm_bytes_per_launch")
+            for p in parts:
+                if row.get("config") == config and row.get("kernel", "").startswith(p):
+                    got[p] = row.get("hbm_bytes_per_launch")
+        if len(got) == len(parts) and all(v is not None for v in got.values()):
+            best = sum(got.values())
     return best
 
 

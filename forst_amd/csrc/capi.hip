@@ -21,6 +21,7 @@ namespace {
 
 thread_local std::string g_last_error;
 thread_local const char* g_last_kernel = "";
+thread_local std::string g_last_kernel_buf;
 
 constexpr int kMaxDevices = 64;
 DeviceInfo g_info[kMaxDevices];
@@ -132,10 +133,64 @@ int check_block_args(const uint8_t* base, const uint64_t* offsets, const uint32_
   return FORST_OK;
 }
 
+// trailer bytes [type][LE32 out] at each block end (split write side: the
+// streaming kernel runs in compute mode, the in-place writes come after it)
+__global__ void __launch_bounds__(256) trailer_scatter_kernel(BlockArgs a) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * 256 + threadIdx.x;
+  if (i >= a.n) return;
+  const uint64_t off = a.offsets[i];
+  const uint32_t n = a.sizes[i];
+  if (off > a.base_len || uint64_t(n) + 5 > a.base_len - off) return;
+  uint8_t* p = a.base_w + off + n;
+  const uint32_t v = a.out32[i];
+  p[0] = a.last_bytes[i];
+  p[1] = static_cast<uint8_t>(v);
+  p[2] = static_cast<uint8_t>(v >> 8);
+  p[3] = static_cast<uint8_t>(v >> 16);
+  p[4] = static_cast<uint8_t>(v >> 24);
+}
+
+hipError_t launch_blocks(int type, int mode, const BlockArgs& a, hipStream_t s);
+
 int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
   int rc = check_device();
   if (rc) return rc;
+  if (type < FORST_kNoChecksum || type > FORST_kXXH3)  // options_helper.h:34
+    return set_error(FORST_EINVAL, "unknown ChecksumType " + std::to_string(type));
   hipStream_t s = static_cast<hipStream_t>(stream);
+  // Write side: the streaming kernel runs in compute mode and the 5 trailer
+  // bytes per block are stored by a second, tiny kernel.  Trailer bytes are
+  // partial writes into 64 B memory sectors shared with block data (a
+  // read-modify-write below the L2); done inside the streaming kernel they
+  // cost 16 % of the pass (C2), split off 8 % (tools/gpu_trailer_ab.sh).
+  // FORST_TRAILER=fused keeps them in the streaming kernel (A/B reference).
+  const char* tv = std::getenv("FORST_TRAILER");
+  if (mode == kModeTrailer && !(tv && std::string(tv) == "fused") && a.n) {
+    BlockArgs c = a;
+    void* tmp = nullptr;
+    hipError_t e = hipSuccess;
+    if (!c.out32) {
+      e = scratch_alloc(&tmp, 4 * a.n, s);
+      c.out32 = static_cast<uint32_t*>(tmp);
+    }
+    if (e == hipSuccess) e = launch_blocks(type, kModeCompute, c, s);
+    if (e == hipSuccess) {
+      hipLaunchKernelGGL(trailer_scatter_kernel, dim3(static_cast<uint32_t>((a.n + 255) / 256)),
+                         dim3(256), 0, s, c);
+      e = hipGetLastError();
+      g_last_kernel_buf = std::string(g_last_kernel) + "+trailer_scatter_kernel";
+      g_last_kernel = g_last_kernel_buf.c_str();
+    }
+    if (tmp) {
+      const hipError_t f = scratch_free(tmp, s);
+      if (e == hipSuccess) e = f;
+    }
+    return hip_status(e, "kernel launch");
+  }
+  return hip_status(launch_blocks(type, mode, a, s), "kernel launch");
+}
+
+hipError_t launch_blocks(int type, int mode, const BlockArgs& a, hipStream_t s) {
   hipError_t e;
   switch (type) {
     case FORST_kCRC32c:
@@ -152,10 +207,9 @@ int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
       e = launch_xxhash_legacy_blocks(type == FORST_kxxHash64, mode, a, s, &g_last_kernel);
       break;
     default:
-      // options_helper.h:34 IsSupportedChecksumType rejects > kXXH3
-      return set_error(FORST_EINVAL, "unknown ChecksumType " + std::to_string(type));
+      return hipErrorInvalidValue;
   }
-  return hip_status(e, "kernel launch");
+  return e;
 }
 
 }  // namespace

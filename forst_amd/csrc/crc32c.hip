@@ -881,6 +881,13 @@ __device__ __forceinline__ uint32_t row_shr_xor(uint32_t v) {
                                                                0xf, 0xf, false));
 }
 
+// XOR of the 16 lanes of each row, valid in every lane of the row (DPP row_ror)
+template <int N>
+__device__ __forceinline__ uint32_t row_ror_xor(uint32_t v) {
+  return v ^ static_cast<uint32_t>(__builtin_amdgcn_update_dpp(0, static_cast<int>(v), 0x120 + N,
+                                                               0xf, 0xf, false));
+}
+
 // join the 2 x 64 chain states, fold in the tail bytes and the extra byte;
 // returns ~state (the crc32c::Extend value), wave-uniform
 __device__ __forceinline__ uint32_t stream_finish2(const uint8_t* __restrict__ Lb,
@@ -1154,6 +1161,7 @@ struct CRowPos {
   __device__ __forceinline__ uint32_t m() const { return (pk >> 13) & 3u; }
   __device__ __forceinline__ bool valid() const { return (pk >> 15) & 1u; }
   __device__ __forceinline__ bool slow() const { return (pk >> 16) & 1u; }
+  __device__ __forceinline__ bool xtra() const { return (pk >> 17) & 1u; }
 };
 
 template <int MODE>
@@ -1164,8 +1172,14 @@ __device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
   const uint64_t ws = off & ~3ull;
   const uint64_t we = E & ~3ull;
   const uint64_t d4 = we - ws;
-  uint32_t R = static_cast<uint32_t>((d4 + kRowRound - 1) / kRowRound);
-  int64_t w0 = static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRowRound;
+  // a window one dword longer than whole rounds (1/4 of back-to-back 4 KiB
+  // blocks: 4097 checksummed bytes starting at offset = 3 mod 4) ends one
+  // dword early; that dword is one slicing step in the finish instead of a
+  // fifth, almost empty round
+  // (block modes only: raw messages of arbitrary lengths rarely hit it)
+  const bool xtra = MODE != kModeRaw && (d4 & (kRowRound - 1)) == 4 && d4 > kRowRound;
+  uint32_t R = static_cast<uint32_t>(xtra ? d4 / kRowRound : (d4 + kRowRound - 1) / kRowRound);
+  int64_t w0 = static_cast<int64_t>(we) - (xtra ? 4 : 0) - static_cast<int64_t>(R) * kRowRound;
   const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - w0);
   const uint32_t cA = hA >> 9, tA = (hA >> 5) & 15u, jA = (hA >> 2) & 7u;
   const int64_t seg_head = static_cast<int64_t>(ws) - 4 * static_cast<int64_t>(jA);
@@ -1180,13 +1194,13 @@ __device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
   P.R = R;
   P.w0_lo = static_cast<uint32_t>(w0);
   P.w0_hi = static_cast<uint32_t>(static_cast<uint64_t>(w0) >> 32);
-  P.pk = (slow ? 0u : (cA | (tA << 1) | (jA << 5) | (q << 8))) | (nt << 11) | (m << 13) |
-         (valid ? 1u << 15 : 0u) | (slow ? 1u << 16 : 0u);
+  P.pk = (slow ? 0u : (cA | (tA << 1) | (jA << 5) | (q << 8) | (xtra ? 1u << 17 : 0u))) |
+         (nt << 11) | (m << 13) | (valid ? 1u << 15 : 0u) | (slow ? 1u << 16 : 0u);
 }
 
 struct CRStep {
   uint32_t w[2][8];
-  uint32_t t0, t1, mod, extra;
+  uint32_t t0, t1, t2, mod, extra;  // t2: the extra window dword (xtra)
 };
 
 template <int MODE>
@@ -1216,17 +1230,26 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
   // tail dword at the window end (last round of a fast block only)
   const uint32_t nt = P.nt();
   const bool lastr = !P.slow() && P.g + 1 >= P.R;
-  const uint64_t we = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
+  const bool xt = MODE != kModeRaw && P.xtra();
+  const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
+  const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
   const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
   d.t0 = ld4v(a.base + t0);
-  d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastr && nt ? t0 + 4 : t0)) : 0u;
+  // t1: the word after the tail (verify: stored checksum), else the extra
+  // window dword; t2: the extra window dword in verify mode
+  const uint64_t tx = lastr && xt ? wE : t0;
+  d.t1 = MODE == kModeRaw ? 0u
+                          : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
+  d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
   const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
   d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
   d.extra = MODE == kModeRaw ? (a.init_crcs ? a.init_crcs[idx] : 0u)
                              : (a.last_bytes ? a.last_bytes[idx] : 0u);
 }
 
-template <int MODE>
+// PROBE (diagnostics, never default): 1 = same loads and row bookkeeping,
+// no table work and no finish; 2 = no per-block finish
+template <int MODE, int PROBE = 0>
 __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
   fill_tables3(L);
@@ -1307,7 +1330,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[c][j] = cu.w[c][j];
-    if (__ballot(fast && r0)) {  // some row starts a block: its head
+    if (PROBE != 1 && __ballot(fast && r0)) {  // some row starts a block: its head
       const uint32_t cA = C.cA(), tA = C.tA(), jA = C.jA(), q = C.q(), m = C.m();
       const uint32_t bm = 0xffffffffu << (8 * m);
       const uint32_t S0 = MODE == kModeRaw ? unstep_m(~cu.extra, m)
@@ -1340,8 +1363,17 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
         }
       }
     }
+    if (PROBE == 1) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c) {
+      for (int c = 0; c < 2; ++c) {
+        uint32_t x = r0 ? 0u : s[c];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) x ^= w[c][j];
+        s[c] = x;
+      }
+    }
+#pragma unroll
+    for (int c = 0; c < (PROBE == 1 ? 0 : 2); ++c) {
       uint32_t lj[4], lg[4];
       rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);  // J3(0) = 0: a row at round 0 starts fresh
       rep_look<false>(Lb, K, w[c][0], lg);
@@ -1353,24 +1385,29 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
     }
     // ---- rows that finish a block in this step ----
     const bool fin = C.rel != kNoBlk && (C.slow() || C.g + 1 >= C.R);
-    if (__ballot(fin)) {
+    if (PROBE != 0 && fin && t == 15 && a.out32) a.out32[C.rel] = s[0] ^ s[1] ^ cu.t0;
+    if (PROBE == 0 && __ballot(fin)) {
       // chain states to the row end (A[15 - t]), row XOR, chain 0 over chain 1
       const bool lo0 = t == 15;
       const uint32_t abase = kOffA2 + 4096 * (14 - t);
       uint32_t a0 = lo0 ? s[0] : shift_at(Lb, abase, s[0]);
       uint32_t a1 = lo0 ? s[1] : shift_at(Lb, abase, s[1]);
-      a0 = row_shr_xor<1>(a0);
-      a1 = row_shr_xor<1>(a1);
-      a0 = row_shr_xor<2>(a0);
-      a1 = row_shr_xor<2>(a1);
-      a0 = row_shr_xor<4>(a0);
-      a1 = row_shr_xor<4>(a1);
-      a0 = row_shr_xor<8>(a0);
-      a1 = row_shr_xor<8>(a1);
+      a0 = row_ror_xor<1>(a0);
+      a1 = row_ror_xor<1>(a1);
+      a0 = row_ror_xor<2>(a0);
+      a1 = row_ror_xor<2>(a1);
+      a0 = row_ror_xor<4>(a0);
+      a1 = row_ror_xor<4>(a1);
+      a0 = row_ror_xor<8>(a0);
+      a1 = row_ror_xor<8>(a1);
       uint32_t crc = 0, stored = 0;
       const uint32_t nt = C.nt();
-      if (fin && lo0) {
-        const uint32_t st = shift_at(Lb, kOffB2, a0) ^ a1;
+      // lanes that finish the CRC: the row's last lane, and in trailer mode
+      // lanes 11..15, which store the 5 trailer bytes with one instruction
+      const bool calc = fin && (MODE == kModeTrailer ? t >= 11 : lo0);
+      if (calc) {
+        uint32_t st = shift_at(Lb, kOffB2, a0) ^ a1;
+        if (MODE != kModeRaw && C.xtra()) st = step_k(Lb, K, st, MODE == kModeVerify ? cu.t2 : cu.t1, 4);
         uint32_t y = nt ? (cu.t0 & (0xffffffffu >> (32 - 8 * nt))) : 0u;
         uint32_t k = nt;
         if (has_extra) {
@@ -1380,7 +1417,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
         crc = ~step_k(Lb, K, st, y, k);
         if (MODE == kModeVerify) stored = nt ? __builtin_amdgcn_alignbyte(cu.t1, cu.t0, nt) : cu.t0;
       }
-      if (fin && lo0 && C.slow() && C.valid()) {
+      if (calc && C.slow() && C.valid()) {
         const uint8_t* pp = a.base + C.off();
         const uint32_t init = MODE == kModeRaw ? cu.extra : 0u;
         crc = small_crc2(Lb, K, pp, C.size + (mem_last_byte<MODE>(a) ? 1u : 0u), init,
@@ -1404,10 +1441,14 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
       } else {
         const uint32_t out = crc_mask(crc) + cu.mod;  // format.cc:594-600 + builder.cc:1340-1345
         if (mine && a.out32) a.out32[i] = valid ? out : 0u;
-        if (MODE == kModeTrailer && mine && valid) {
-          uint8_t* pw = a.base_w + C.off() + C.size;
-          if (a.last_bytes) pw[0] = static_cast<uint8_t>(cu.extra);
-          stu32_bytes(pw + 1, out);
+        if (MODE == kModeTrailer) {
+          // the 5 trailer bytes [type][LE32] by lanes 11..15 of the row: one
+          // byte store per wave instead of five per finishing row
+          const uint32_t k = t - 11;
+          if (calc && valid && (k != 0 || a.last_bytes)) {
+            uint8_t* pw = a.base_w + C.off() + C.size;
+            pw[k] = static_cast<uint8_t>(k == 0 ? cu.extra : out >> (8 * (k - 1)));
+          }
         }
       }
       if (MODE == kModeVerify) {
@@ -1521,6 +1562,10 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   // (the rows kernel indexes descriptors with 32 bits)
   const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
                                             ((!variant || !*variant) && small_blocks));
+  const int rows_probe = !variant ? 0
+                         : std::string(variant) == "rows_probe_load"   ? 1
+                         : std::string(variant) == "rows_probe_nofin" ? 2
+                                                                       : 0;
   // diagnostics: probe_load (loads only), probe_rounds (no finish),
   // probe_nohead (no round-0 head handling); results are not checksums
   const int probe = !variant ? 0
@@ -1534,12 +1579,19 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
       *name = "crc32c_block_kernel_simple<" TAG ">";                                      \
       hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,    \
                          stream, a);                                                      \
-    } else if (rows) {                                                                    \
+    } else if (rows || (rows_probe && M == kModeVerify)) {                                \
       *name = "crc32c_rows_kernel<" TAG ">";                                              \
       BlockArgs b = a;                                                                    \
       hipError_t fe = feed_setup(b, uint64_t(grid) * kWaves, stream);                     \
       if (fe != hipSuccess) return fe;                                                    \
-      hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, b); \
+      if (rows_probe == 1)                                                                \
+        hipLaunchKernelGGL((crc32c_rows_kernel<kModeVerify, 1>), dim3(grid), dim3(kThreads), \
+                           0, stream, b);                                                 \
+      else if (rows_probe == 2)                                                           \
+        hipLaunchKernelGGL((crc32c_rows_kernel<kModeVerify, 2>), dim3(grid), dim3(kThreads), \
+                           0, stream, b);                                                 \
+      else                                                                                \
+        hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, b); \
       fe = hipGetLastError();                                                             \
       const hipError_t ff = scratch_free(b.ticket, stream);                               \
       return fe != hipSuccess ? fe : ff;                                                  \

@@ -96,7 +96,7 @@ def block_trailer_batch(ctype, base, offsets, sizes, last_bytes, modifiers=None,
     _dev_u8(base)
     check(lib().forst_block_trailer_batch(int(ctype), base.data_ptr(), base.numel(),
                                           offsets.data_ptr(), sizes.data_ptr(),
-                                          last_bytes.data_ptr(), _p(modifiers), _p(out),
+                                          _p(last_bytes), _p(modifiers), _p(out),
                                           n, _stream(stream)))
     return out
 

@@ -56,7 +56,7 @@ def main():
     write = load_counter(os.path.join(src, "write", "write_counter_collection.csv"))
     rows = []
     for k in sorted(set(fetch) | set(write)):
-        if not k.startswith(("crc32c", "xxh3", "wal", "noop")):
+        if not k.startswith(("crc32c", "xxh3", "wal", "noop", "trailer_scatter")):
             continue
         f = sum(fetch[k]) / len(fetch[k]) if fetch[k] else 0.0
         w = sum(write[k]) / len(write[k]) if write[k] else 0.0

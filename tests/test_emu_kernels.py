@@ -285,3 +285,21 @@ def test_emu_wal_record_xxh3(recyclable):
     starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
     for j in range(len(lens)):
         assert int(h[j]) == O.xxh3_64(payload[starts[j]:starts[j + 1]].tobytes()), j
+
+
+def test_emu_rows_extra_dword_windows():
+    """4096- and 1024·k-byte blocks at every start alignment: the rows kernel
+    ends windows that are one dword longer than whole rounds one dword early
+    and steps that dword in the finish"""
+    rng = np.random.default_rng(5)
+    sizes = np.array([4096, 4096, 4096, 4096, 1024, 2048, 3072, 4095, 4097, 8192] * 8, np.uint32)
+    offs = np.zeros(len(sizes), np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 5 + rng.integers(0, 4, len(sizes) - 1))
+    base = rng.integers(0, 256, int(offs[-1]) + int(sizes[-1]) + 4096, dtype=np.uint8)
+    types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
+    for t in (1, 4):
+        want = O.block_checksum_batch(t, base, offs, sizes)
+        assert (emu.block_checksum(t, base, offs, sizes) == want).all()
+        b2, out = emu.block_trailer(t, base, offs, sizes, types)
+        comp, st, ok, bad = emu.block_verify(t, b2, offs, sizes)
+        assert bad == 0 and ok.all()

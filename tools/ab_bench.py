@@ -34,7 +34,7 @@ def main():
                     help="ENV=VALUE (empty value = unset); several comma-joined allowed")
     ap.add_argument("--rounds", type=int, default=5)
     ap.add_argument("--reps", type=int, default=5)
-    ap.add_argument("--mode", default="verify", choices=["verify", "trailer", "pair"],
+    ap.add_argument("--mode", default="verify", choices=["verify", "trailer", "pair", "compute", "compute_mem"],
                     help="pair: trailer then verify per rep (bench.py's step), verify timed")
     ap.add_argument("--computed", action="store_true", help="verify also stores computed[]")
     args = ap.parse_args()
@@ -45,6 +45,7 @@ def main():
         b = workload.make_sst_batch(n, spec, 0xF0E5700002, ctype=ct)
         ok = torch.empty(n, dtype=torch.uint8, device="cuda")
         comp = torch.empty(n, dtype=torch.uint32, device="cuda") if args.computed else None
+        cout = torch.empty(n, dtype=torch.uint32, device="cuda")
         bad = torch.zeros(1, dtype=torch.int64, device="cuda")
         times = {v: [] for v in variants}
         for _ in range(args.rounds):
@@ -79,6 +80,10 @@ def main():
                     if args.mode == "verify":
                         engine.block_verify_batch(ct, b.base, b.offsets, b.sizes, computed=comp,
                                                   stored=None, ok=ok, mismatches=bad)
+                    elif args.mode.startswith("compute"):  # trailer without the stores
+                        engine.block_checksum_batch(
+                            ct, b.base, b.offsets, b.sizes,
+                            last_bytes=None if args.mode == "compute_mem" else b.types, out=cout)
                     else:
                         engine.block_trailer_batch(ct, b.base, b.offsets, b.sizes, b.types)
                 e1.record()

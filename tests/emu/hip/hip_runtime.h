@@ -202,6 +202,7 @@ inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v)
 // stream-ordered allocation / copies: host memory, everything synchronous
 typedef void* hipMemPool_t;
 constexpr hipError_t hipErrorInvalidDevice = 101;
+constexpr hipError_t hipErrorInvalidValue = 1;
 enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2 };
 enum { hipMemAllocationTypePinned = 1, hipMemLocationTypeDevice = 1,
        hipMemPoolAttrReleaseThreshold = 4 };

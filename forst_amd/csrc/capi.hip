@@ -162,7 +162,9 @@ int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
   // bytes per block are stored by a second, tiny kernel.  Trailer bytes are
   // partial writes into 64 B memory sectors shared with block data (a
   // read-modify-write below the L2); done inside the streaming kernel they
-  // cost 16 % of the pass (C2), split off 8 % (tools/gpu_trailer_ab.sh).
+  // cost 16 % of the pass (C2), split off 8 % (tools/gpu_trailer_ab.sh; a
+  // read-merge-write of the covering dwords in the scatter kernel measured
+  // the same).
   // FORST_TRAILER=fused keeps them in the streaming kernel (A/B reference).
   const char* tv = std::getenv("FORST_TRAILER");
   if (mode == kModeTrailer && !(tv && std::string(tv) == "fused") && a.n) {

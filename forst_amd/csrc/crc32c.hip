@@ -1555,10 +1555,12 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   const char* variant = std::getenv("FORST_CRC_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < kRB;
   const bool v1 = variant && std::string(variant) == "v1";
-  // default: the rows kernel (one block per 16-lane row) for small blocks,
-  // where the per-block finish dominates; the v2 kernel (two 4 KiB steps in
-  // flight per wave) otherwise.  Mean block size from the launch arguments.
-  const bool small_blocks = a.base_len / a.n <= 6144;
+  // default: the rows kernel (one block per 16-lane row) up to 20 KiB mean
+  // block size, the v2 kernel (two 4 KiB steps in flight per wave) above.
+  // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2 %; v2 wins on
+  // the 4/16/64 KiB mix by 4 % and at 64 KiB by 45 %, where the rows of a
+  // wave stream addresses 64 KiB apart)
+  const bool small_blocks = a.base_len / a.n <= 20480;
   // (the rows kernel indexes descriptors with 32 bits)
   const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
                                             ((!variant || !*variant) && small_blocks));

@@ -918,8 +918,13 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   const char* variant = std::getenv("FORST_XXH3_VARIANT");
   const bool simple = (variant && std::string(variant) == "simple") || a.base_len < 4096;
   const bool probe = variant && std::string(variant) == "probe_load" && mode == kModeVerify;
-  // the rows kernel indexes descriptors with 32 bits
-  const bool v1 = (variant && std::string(variant) == "v1") || a.n >= 0xffffffffull;
+  // the rows kernel indexes descriptors with 32 bits; uniform >= 48 KiB blocks
+  // go to v1 (rows of a wave streaming addresses 64 KiB apart camp on the
+  // same HBM channels: X64 rows 0.49 vs v1 0.62 of the peak; C3's 4/16/64 KiB
+  // mix stays on rows, 0.67 vs 0.53)
+  const bool big = a.base_len / a.n >= 49152;
+  const bool v1 = (variant && std::string(variant) == "v1") || a.n >= 0xffffffffull ||
+                  ((!variant || !*variant) && big);
 #define FORST_LAUNCH_XXH3(M, TAG)                                                          \
   do {                                                                                     \
     if (simple) {                                                                          \

@@ -32,6 +32,8 @@ import numpy as np  # noqa: E402
 import torch  # noqa: E402
 import torch.distributed as dist  # noqa: E402
 
+from forst_amd import shard  # noqa: E402
+
 HBM_PEAK_GBS = 8000.0  # MI355X_MICROARCH.md: 8.0 TB/s spec
 GIB = float(1 << 30)
 METRIC = "device-resident GiB/s checksummed (CRC32C/XXH3), 4–64 KiB blocks, 1/2/4/8 GPU"
@@ -47,28 +49,15 @@ CONFIGS = {
 
 
 def dist_setup():
-    world = int(os.environ.get("WORLD_SIZE", "1"))
-    rank = int(os.environ.get("RANK", "0"))
-    local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
-        torch.cuda.set_device(local)
-    if world > 1:
-        backend = "nccl" if torch.cuda.is_available() else "gloo"
-        dist.init_process_group(backend=backend)
-    return world, rank, local
+    return shard.setup()
 
 
 def barrier(world):
-    if world > 1:
-        dist.barrier()
+    shard.barrier(world)
 
 
 def max_over_ranks(x, world):
-    if world == 1:
-        return x
-    t = torch.tensor([x], dtype=torch.float64, device="cuda")
-    dist.all_reduce(t, op=dist.ReduceOp.MAX)
-    return float(t.item())
+    return shard.max_over_ranks(x, world)
 
 
 def algorithmic_bytes(kind, b):

@@ -1130,12 +1130,13 @@ constexpr uint32_t kNoBlk = 0xffffffffu;
 
 __device__ __forceinline__ void fill_tables3(uint32_t* L) {
   const uint32_t tid = threadIdx.x;
-  for (uint32_t i = tid; i < 16384; i += kThreads) {
+  const uint32_t nt = blockDim.x;
+  for (uint32_t i = tid; i < 16384; i += nt) {
     const uint32_t e = i >> 6, d = i & 63, t = (d >> 3) & 3;
     L[i] = d < 32 ? kCrcG[t * 256 + e] : kCrcJ3[t * 256 + e];
   }
-  for (uint32_t i = tid; i < 15 * 1024; i += kThreads) L[kOffA2 / 4 + i] = kCrcA[i];
-  for (uint32_t i = tid; i < 1024; i += kThreads) L[kOffB2 / 4 + i] = kCrcB[i];
+  for (uint32_t i = tid; i < 15 * 1024; i += nt) L[kOffA2 / 4 + i] = kCrcA[i];
+  for (uint32_t i = tid; i < 1024; i += nt) L[kOffB2 / 4 + i] = kCrcB[i];
   __syncthreads();
 }
 
@@ -1248,9 +1249,13 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
 }
 
 // PROBE (diagnostics, never default): 1 = same loads and row bookkeeping,
-// no table work and no finish; 2 = no per-block finish
-template <int MODE, int PROBE = 0>
-__global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
+// no table work and no finish; 2 = no per-block finish.
+// DEPTH 2: two steps of loads in flight per wave (three step buffers,
+// 12-wave workgroups at 3 waves/SIMD) instead of one.
+constexpr uint32_t kRowsD2Waves = 12;
+template <int MODE, int PROBE = 0, int DEPTH = 1>
+__global__ void __launch_bounds__(DEPTH == 2 ? 64 * kRowsD2Waves : kThreads)
+    crc32c_rows_kernel(BlockArgs a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
   fill_tables3(L);
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -1260,8 +1265,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
   const Lanes2 K = lanes2(lane);
   const uint32_t s0c[4] = {uniform(kCrcS0[0]), uniform(kCrcS0[1]), uniform(kCrcS0[2]),
                            uniform(kCrcS0[3])};
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (DEPTH == 2 ? kRowsD2Waves : kWaves);
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * (DEPTH == 2 ? kRowsD2Waves : kWaves) + wave;
   const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
 
   // descriptor batches from the work feed: lane j <-> descriptor cg + j (cb),
@@ -1313,15 +1318,19 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
       load_batch<MODE>(a, ng, a.n, lane, nb);
     }
   };
-  CRowPos I;
+  CRowPos I, I2;
   advance(C, I);
-  CRStep X, Y;
+  if (DEPTH == 2) advance(I, I2);
+  CRStep X, Y, Z;
   crow_issue<MODE>(a, lane, C, kbeg, X);
+  if (DEPTH == 2) crow_issue<MODE>(a, lane, I, kbeg, Y);
   uint32_t s[2] = {0, 0};
 
+  // cu: the current step's data (ready); nx: the buffer that receives the
+  // loads issued now (the position DEPTH steps ahead)
   auto step = [&](CRStep& cu, CRStep& nx) -> bool {
     if (__ballot(C.rel != kNoBlk) == 0) return false;
-    crow_issue<MODE>(a, lane, I, kbeg, nx);
+    crow_issue<MODE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
     const bool fast = C.rel != kNoBlk && !C.slow();
     const bool r0 = C.g == 0;
     // ---- one 1 KiB round of every row ----
@@ -1458,10 +1467,20 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
       }
     }
     C = I;
-    advance(C, I);
+    if (DEPTH == 2) {
+      I = I2;
+      advance(I, I2);
+    } else {
+      advance(C, I);
+    }
     return true;
   };
-  while (step(X, Y) && step(Y, X)) {
+  if (DEPTH == 2) {
+    while (step(X, Z) && step(Y, X) && step(Z, Y)) {
+    }
+  } else {
+    while (step(X, Y) && step(Y, X)) {
+    }
   }
 }
 
@@ -1568,6 +1587,7 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
                          : std::string(variant) == "rows_probe_load"   ? 1
                          : std::string(variant) == "rows_probe_nofin" ? 2
                                                                        : 0;
+  const bool rows_d2 = variant && std::string(variant) == "rows_d2";
   // diagnostics: probe_load (loads only), probe_rounds (no finish),
   // probe_nohead (no round-0 head handling); results are not checksums
   const int probe = !variant ? 0
@@ -1581,11 +1601,22 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
       *name = "crc32c_block_kernel_simple<" TAG ">";                                      \
       hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,    \
                          stream, a);                                                      \
-    } else if (rows || (rows_probe && M == kModeVerify)) {                                \
+    } else if (rows || rows_d2 || (rows_probe && M == kModeVerify)) {                     \
       *name = "crc32c_rows_kernel<" TAG ">";                                              \
       BlockArgs b = a;                                                                    \
       hipError_t fe = feed_setup(b, uint64_t(grid) * kWaves, stream);                     \
       if (fe != hipSuccess) return fe;                                                    \
+      if (rows_d2) {                                                                      \
+        BlockArgs b2 = b;                                                                 \
+        (void)scratch_free(b.ticket, stream);                                             \
+        fe = feed_setup(b2, uint64_t(grid) * kRowsD2Waves, stream);                       \
+        if (fe != hipSuccess) return fe;                                                  \
+        hipLaunchKernelGGL((crc32c_rows_kernel<M, 0, 2>), dim3(grid),                     \
+                           dim3(64 * kRowsD2Waves), 0, stream, b2);                       \
+        fe = hipGetLastError();                                                           \
+        const hipError_t ff2 = scratch_free(b2.ticket, stream);                           \
+        return fe != hipSuccess ? fe : ff2;                                               \
+      }                                                                                   \
       if (rows_probe == 1)                                                                \
         hipLaunchKernelGGL((crc32c_rows_kernel<kModeVerify, 1>), dim3(grid), dim3(kThreads), \
                            0, stream, b);                                                 \

@@ -196,3 +196,39 @@ def test_verify_file_large():
     r = sst.verify_file(f, file_name="big.sst")
     assert r.status == 0 and r.data_blocks == 2000, r.message
     assert r.index_partitions == 32
+
+
+def test_decoders_survive_random_corruption():
+    """Random byte flips in the structural blocks: every decoder either
+    returns an error or handles, never reads outside the block (the fuzz
+    loop would crash the process otherwise) and never loops forever."""
+    rng = np.random.default_rng(17)
+    for fv, ct, it, ri in [(5, 1, 0, 1), (6, 4, 2, 4), (6, 1, 3, 1), (2, 3, 1, 1)]:
+        w, f = make(fv, ct, it, ri)
+        for kind in ("index", "metaindex", "properties", "partition"):
+            blks = blocks_of(w, kind)
+            if not blks:
+                continue
+            o, n = blks[0]
+            for _ in range(300):
+                b = bytearray(f[o:o + n])
+                for _ in range(int(rng.integers(1, 6))):
+                    b[int(rng.integers(0, n))] = int(rng.integers(0, 256))
+                if rng.random() < 0.2:  # truncations too
+                    b = b[:int(rng.integers(0, n + 1))]
+                try:
+                    if kind == "properties":
+                        sst.properties(bytes(b))
+                    else:
+                        offs, sizes = sst.index_handles(bytes(b), fv >= 4, it == 3)
+                        assert len(offs) <= n  # at least one byte per entry
+                except sst.SstCorruption:
+                    pass
+        tail = bytearray(f[-53:])
+        for _ in range(300):
+            t = bytearray(tail)
+            t[int(rng.integers(0, 53))] ^= 1 << int(rng.integers(0, 8))
+            try:
+                sst.decode_footer(bytes(f[:-53]) + bytes(t))
+            except Exception as e:  # corruption / unsupported, never a crash
+                assert isinstance(e, sst.ForstError) or "block-based" in str(e)

@@ -375,16 +375,70 @@ __global__ void __launch_bounds__(kTile) rec_orphan_kernel(WalArgs a, const uint
   if (owned == 0 || kind[owned - 1] != 2) glen[i] = 0;
 }
 
-// gather fragment payloads (one workgroup per fragment, byte lanes coalesced)
+// gather fragment payloads: one workgroup per fragment, one destination-
+// aligned dword per lane (source realigned from two aligned dwords with
+// v_alignbyte); the partial dwords at either end are byte stores, since the
+// neighbouring fragments' bytes are written by other workgroups
+__device__ __forceinline__ uint32_t ld_any4(const uint8_t* p, const uint8_t* lo,
+                                            const uint8_t* hi) {
+  const uint64_t pa = reinterpret_cast<uint64_t>(p);
+  const uint8_t* q = reinterpret_cast<const uint8_t*>(pa & ~3ull);
+  const uint32_t m = static_cast<uint32_t>(pa & 3);
+  if (q < lo || q + 8 > hi) {  // near the log edges: byte loads
+    uint32_t v = 0;
+    for (uint32_t k = 0; k < 4; ++k)
+      if (p + k >= lo && p + k < hi) v |= static_cast<uint32_t>(p[k]) << (8 * k);
+    return v;
+  }
+  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(q);
+  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(q + 4);
+  return m ? __builtin_amdgcn_alignbyte(w1, w0, m) : w0;
+}
+
+// 16 source bytes at any alignment: a dword-aligned 16-byte load plus one
+// dword, realigned with v_alignbyte
+__device__ __forceinline__ u32x4a4 ld_any16(const uint8_t* p, const uint8_t* lo, const uint8_t* hi) {
+  const uint64_t pa = reinterpret_cast<uint64_t>(p);
+  const uint8_t* q = reinterpret_cast<const uint8_t*>(pa & ~3ull);
+  const uint32_t m = static_cast<uint32_t>(pa & 3);
+  u32x4a4 r;
+  if (q < lo || q + 20 > hi) {
+    r.x = ld_any4(p, lo, hi);
+    r.y = ld_any4(p + 4, lo, hi);
+    r.z = ld_any4(p + 8, lo, hi);
+    r.w = ld_any4(p + 12, lo, hi);
+    return r;
+  }
+  const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(q);
+  const uint32_t e = *reinterpret_cast<const uint32_t*>(q + 16);
+  if (m == 0) return v;
+  r.x = __builtin_amdgcn_alignbyte(v.y, v.x, m);
+  r.y = __builtin_amdgcn_alignbyte(v.z, v.y, m);
+  r.z = __builtin_amdgcn_alignbyte(v.w, v.z, m);
+  r.w = __builtin_amdgcn_alignbyte(e, v.w, m);
+  return r;
+}
+
 __global__ void __launch_bounds__(kTile) rec_gather_kernel(WalArgs a, const uint64_t* glen,
                                                            const uint64_t* goff, uint8_t* dst) {
+  const uint8_t* lo = a.log;
+  const uint8_t* hi = a.log + a.log_len;
   for (uint64_t i = blockIdx.x; i < a.n_records; i += gridDim.x) {
     const uint64_t n = glen[i];
     if (n == 0) continue;
     const FragInfo f = frag_info(a, i);
     const uint8_t* src = a.log + f.off;
     uint8_t* d = dst + goff[i];
-    for (uint64_t k = threadIdx.x; k < n; k += kTile) d[k] = src[k];
+    const uint64_t da = reinterpret_cast<uint64_t>(d);
+    const uint32_t head = static_cast<uint32_t>((16 - (da & 15)) & 15);  // to 16 B alignment
+    const uint64_t h = head < n ? head : n;
+    if (threadIdx.x < h) d[threadIdx.x] = src[threadIdx.x];
+    const uint64_t body = (n - h) & ~15ull;
+    u32x4a4* d16 = reinterpret_cast<u32x4a4*>(d + h);
+    for (uint64_t k = threadIdx.x; k < body / 16; k += kTile)
+      d16[k] = ld_any16(src + h + 16 * k, lo, hi);
+    const uint64_t tail = n - h - body;
+    if (threadIdx.x < tail) d[h + body + threadIdx.x] = src[h + body + threadIdx.x];
   }
 }
 

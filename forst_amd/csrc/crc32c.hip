@@ -687,7 +687,7 @@ __device__ __forceinline__ Blk2 blk2_setup_scalar(const BlockArgs& a, uint64_t k
   const uint32_t nt = static_cast<uint32_t>(E - b.we);
   const uint32_t m = static_cast<uint32_t>(b.off & 3);
   const bool slow = !valid || d4 < 64;
-  b.S0 = MODE == kModeRaw ? unstep_m(~b.extra, m) : kCrcS0[m];
+  b.S0 = MODE == kModeRaw && a.init_crcs ? unstep_m(~b.extra, m) : kCrcS0[m];
   if (slow) {  // the slow path loads on its own; dummy step loads at [0, 4 KiB)
     b.we = kRB2;
     b.R = 1;
@@ -730,7 +730,7 @@ __device__ __forceinline__ Derived2 derive2(const BlockArgs& a, const DescBatch&
   d.pk = slow ? ((nt << 13) | (valid ? 1u << 15 : 0u) | (1u << 16) | (m << 17))
               : (cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
                  (m << 17));
-  d.S0 = MODE == kModeRaw ? unstep_m(~cb.extra, m) : 0u;
+  d.S0 = MODE == kModeRaw ? (a.init_crcs ? unstep_m(~cb.extra, m) : kCrcS0[m]) : 0u;
   return d;
 }
 
@@ -1342,8 +1342,11 @@ __global__ void __launch_bounds__(DEPTH == 2 ? 64 * kRowsD2Waves : kThreads)
     if (PROBE != 1 && __ballot(fast && r0)) {  // some row starts a block: its head
       const uint32_t cA = C.cA(), tA = C.tA(), jA = C.jA(), q = C.q(), m = C.m();
       const uint32_t bm = 0xffffffffu << (8 * m);
-      const uint32_t S0 = MODE == kModeRaw ? unstep_m(~cu.extra, m)
-                                           : (m == 0 ? s0c[0] : m == 1 ? s0c[1] : m == 2 ? s0c[2] : s0c[3]);
+      // raw mode with per-message inits: the GF(2) unstep; without (crc32c::Value,
+      // every WAL record) S0 is the block modes' constant
+      const uint32_t S0 = MODE == kModeRaw && a.init_crcs
+                              ? unstep_m(~cu.extra, m)
+                              : (m == 0 ? s0c[0] : m == 1 ? s0c[1] : m == 2 ? s0c[2] : s0c[3]);
 #pragma unroll
       for (uint32_t c = 0; c < 2; ++c) {
         const bool hl = fast && r0 && c == cA && t == tA;  // the head lane of the row
@@ -1582,7 +1585,8 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   const bool small_blocks = a.base_len / a.n <= 20480;
   // (the rows kernel indexes descriptors with 32 bits)
   const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
-                                            ((!variant || !*variant) && small_blocks));
+                                            ((!variant || !*variant) &&
+                                             (a.kernel_hint ? a.kernel_hint == 1 : small_blocks)));
   const int rows_probe = !variant ? 0
                          : std::string(variant) == "rows_probe_load"   ? 1
                          : std::string(variant) == "rows_probe_nofin" ? 2

@@ -478,11 +478,122 @@ __global__ void __launch_bounds__(kTile) rec_select_kernel(uint64_t n_logical, c
   if (out_first) out_first[j] = first_phys[j];
 }
 
+// ---- raw CRC of a record list split by size (A/B variant) -------------------
+// WAL records span 7 B .. 32 KiB: with FORST_WAL_SPLIT=1 small ones go to the
+// rows kernel (one record per 16-lane row), large ones to the v2 kernel (one
+// per wave), results scattered back in record order.  Measured slower than
+// one rows launch over all records (C5 0.478 vs 0.499), so not the default.
+constexpr uint32_t kSplitBytes = 8192;
+
+__global__ void __launch_bounds__(kTile) split_flag_kernel(const uint32_t* len, uint64_t n,
+                                                           uint64_t* flag) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i < n) flag[i] = len[i] < kSplitBytes ? 1 : 0;
+}
+
+__global__ void __launch_bounds__(kTile) split_compact_kernel(
+    const uint64_t* off, const uint32_t* len, uint64_t n, const uint64_t* flag,
+    const uint64_t* pos, uint64_t* s_off, uint32_t* s_len, uint64_t* b_off, uint32_t* b_len) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i >= n) return;
+  if (flag[i]) {
+    s_off[pos[i]] = off[i];
+    s_len[pos[i]] = len[i];
+  } else {
+    b_off[i - pos[i]] = off[i];
+    b_len[i - pos[i]] = len[i];
+  }
+}
+
+__global__ void __launch_bounds__(kTile) split_scatter_kernel(uint64_t n, const uint64_t* flag,
+                                                              const uint64_t* pos,
+                                                              const uint32_t* s_out,
+                                                              const uint32_t* b_out,
+                                                              uint32_t* out) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
+  if (i < n) out[i] = flag[i] ? s_out[pos[i]] : b_out[i - pos[i]];
+}
+
 size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
 bool wave_variant() {
   const char* v = std::getenv("FORST_WAL_VARIANT");
   return v && std::string(v) == "wave";
+}
+
+}  // namespace
+
+namespace {
+
+// out[i] = crc32c::Extend(0, base + off[i], len[i]) for a record list
+// (FORST_WAL_SPLIT=1: split by size between the rows and v2 kernels)
+hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* off,
+                       const uint32_t* len, uint64_t n, uint32_t* out, hipStream_t stream,
+                       const char** name) {
+  BlockArgs b{};
+  b.base = base;
+  b.base_len = base_len;
+  b.offsets = off;
+  b.sizes = len;
+  b.out32 = out;
+  b.n = n;
+  // default: one launch (the rows kernel for this size mix); the split is an
+  // A/B variant (C5: 0.499 one launch vs 0.478 split, tools/wal_ab.py)
+  const char* sv = std::getenv("FORST_WAL_SPLIT");
+  if (!(sv && std::string(sv) == "1")) return launch_crc32c_blocks(kModeRaw, b, stream, name);
+  const uint64_t nt = (n + kTile - 1) / kTile;
+  const dim3 grid(static_cast<uint32_t>(nt));
+  const size_t s8 = up256(8 * n), s4 = up256(4 * n), st = up256(8 * (nt + 1));
+  void* scratch = nullptr;
+  hipError_t e = scratch_alloc(&scratch, 4 * s8 + 4 * s4 + st, stream);
+  if (e != hipSuccess) return e;
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint64_t* flag = reinterpret_cast<uint64_t*>(p);
+  uint64_t* pos = reinterpret_cast<uint64_t*>(p + s8);
+  uint64_t* s_off = reinterpret_cast<uint64_t*>(p + 2 * s8);
+  uint64_t* b_off = reinterpret_cast<uint64_t*>(p + 3 * s8);
+  uint32_t* s_len = reinterpret_cast<uint32_t*>(p + 4 * s8);
+  uint32_t* b_len = reinterpret_cast<uint32_t*>(p + 4 * s8 + s4);
+  uint32_t* s_out = reinterpret_cast<uint32_t*>(p + 4 * s8 + 2 * s4);
+  uint32_t* b_out = reinterpret_cast<uint32_t*>(p + 4 * s8 + 3 * s4);
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 4 * s8 + 4 * s4);
+  hipLaunchKernelGGL(split_flag_kernel, grid, dim3(kTile), 0, stream, len, n, flag);
+  hipLaunchKernelGGL(scan_tiles_kernel, grid, dim3(kTile), 0, stream, flag, n, tiles);
+  hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanThreads), 0, stream, tiles, nt);
+  hipLaunchKernelGGL(scan_apply_kernel, grid, dim3(kTile), 0, stream, flag, n, tiles, pos);
+  uint64_t n_small = 0;
+  if ((e = hipMemcpyAsync(&n_small, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+      (e = hipStreamSynchronize(stream)) != hipSuccess) {
+    (void)scratch_free(scratch, stream);
+    return e;
+  }
+  hipLaunchKernelGGL(split_compact_kernel, grid, dim3(kTile), 0, stream, off, len, n, flag, pos,
+                     s_off, s_len, b_off, b_len);
+  if (n_small) {
+    BlockArgs bs = b;
+    bs.offsets = s_off;
+    bs.sizes = s_len;
+    bs.out32 = s_out;
+    bs.n = n_small;
+    bs.kernel_hint = 1;
+    e = launch_crc32c_blocks(kModeRaw, bs, stream, name);
+  }
+  if (e == hipSuccess && n_small < n) {
+    BlockArgs bb = b;
+    bb.offsets = b_off;
+    bb.sizes = b_len;
+    bb.out32 = b_out;
+    bb.n = n - n_small;
+    bb.kernel_hint = 2;
+    e = launch_crc32c_blocks(kModeRaw, bb, stream, name);
+  }
+  if (e == hipSuccess) {
+    hipLaunchKernelGGL(split_scatter_kernel, grid, dim3(kTile), 0, stream, n, flag, pos, s_out,
+                       b_out, out);
+    e = hipGetLastError();
+  }
+  const hipError_t f = scratch_free(scratch, stream);
+  return e != hipSuccess ? e : f;
 }
 
 }  // namespace
@@ -526,16 +637,7 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream, const char** 
   s.computed = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(desc) + sz_off + sz_len);
   hipLaunchKernelGGL(wal_fill_kernel, grid, dim3(kTile), 0, stream, a, s);
   *name = "wal_walk_kernel";
-  if (total) {
-    BlockArgs b{};
-    b.base = a.log;
-    b.base_len = a.log_len;
-    b.offsets = s.desc_off;
-    b.sizes = s.desc_len;
-    b.out32 = s.computed;
-    b.n = total;
-    e = launch_crc32c_blocks(kModeRaw, b, stream, name);
-  }
+  if (total) e = crc_records(a.log, a.log_len, s.desc_off, s.desc_len, total, s.computed, stream, name);
   hipLaunchKernelGGL(wal_status_kernel, grid, dim3(kTile), 0, stream, a, s);
   if (e == hipSuccess) e = hipGetLastError();
   const hipError_t f1 = scratch_free(desc, stream), f2 = scratch_free(scratch, stream);
@@ -555,14 +657,7 @@ hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream, const cha
   uint32_t* comp = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(scratch) + sz_off + sz_len);
   const dim3 grid(static_cast<uint32_t>((n + kTile - 1) / kTile));
   hipLaunchKernelGGL(wal_rec_desc_kernel, grid, dim3(kTile), 0, stream, a, d_off, d_len);
-  BlockArgs b{};
-  b.base = a.log;
-  b.base_len = a.log_len;
-  b.offsets = d_off;
-  b.sizes = d_len;
-  b.out32 = comp;
-  b.n = n;
-  e = launch_crc32c_blocks(kModeRaw, b, stream, name);
+  e = crc_records(a.log, a.log_len, d_off, d_len, n, comp, stream, name);
   hipLaunchKernelGGL(wal_rec_finish_kernel, grid, dim3(kTile), 0, stream, a, d_len, comp);
   if (e == hipSuccess) e = hipGetLastError();
   const hipError_t f = scratch_free(scratch, stream);

@@ -36,12 +36,15 @@ def block_sizes(n, spec, seed):
     spec: int            -> all equal
           tuple of ints  -> equal shares of each class, shuffled (C3)
           ("dev", b)     -> uniform in [0.9 b, b] (block_size_deviation=10, C3b)
+          ("logu", lo, hi) -> log-uniform in [lo, hi] (the C5 record mix)
     """
     idx = np.arange(n, dtype=np.uint64)
     with np.errstate(over="ignore"):
         keys = _splitmix(np.uint64(seed ^ 0x5EED5EED5EED) + idx * np.uint64(0x9E3779B97F4A7C15))
     if isinstance(spec, int):
         return np.full(n, spec, dtype=np.uint32)
+    if isinstance(spec, tuple) and spec and spec[0] == "logu":  # log-uniform [lo, hi] (C5-like)
+        return log_uniform_lengths(n, int(spec[1]), int(spec[2]), seed)
     if isinstance(spec, tuple) and spec and spec[0] == "dev":
         b = int(spec[1])
         lo = (b * 9) // 10

@@ -90,11 +90,13 @@ def test_emu_wal():
     assert bad == 0 and (st == 0).all() and int(nrec.sum()) == len(poffs)
 
 
-@pytest.mark.parametrize("recyclable", [False, True])
-def test_emu_wal_pipeline_statuses(recyclable, monkeypatch):
+@pytest.mark.parametrize("recyclable,split", [(False, "0"), (True, "0"), (False, "1"),
+                                               (True, "1")])
+def test_emu_wal_pipeline_statuses(recyclable, split, monkeypatch):
     """walk/scan/fill/raw-CRC/status pipeline == the serial per-block reader
     (FORST_WAL_VARIANT=wave) on every status: CRC failure, bad length, old
     record, zero padding, truncated tail; writer-side CRCs restore the image."""
+    monkeypatch.setenv("FORST_WAL_SPLIT", split)  # 1: small / large records on two kernels
     rng = np.random.default_rng(2)
     lens = rng.integers(0, 9000, 90).astype(np.uint32)
     lens[:4] = [0, 32761, 5, 70000]

@@ -23,6 +23,8 @@ CONFIGS = {
     "C3": (1 << 20, (4096, 16384, 65536), 4), "C3CRC": (1 << 20, (4096, 16384, 65536), 1),
     "X4": (1 << 20, 4096, 4), "DEV4": (1 << 20, ("dev", 4096), 1),
     "C64": (1 << 18, 65536, 1), "X64": (1 << 18, 65536, 4),
+    "LOGU": (1 << 23, ("logu", 32, 32768), 1), "LOGU64": (1 << 23, ("logu", 64, 32768), 1),
+    "LOGU1K": (1 << 22, ("logu", 1024, 32768), 1),
     "H32": (1 << 20, 16384, 2), "H64": (1 << 20, 16384, 3), "H64S": (1 << 20, 4096, 3),
 }
 

@@ -339,7 +339,7 @@ def main():
     del b
     torch.cuda.empty_cache()
     if world == 1 and not args.no_extras and args.config == "C2":
-        for nm in ("NS16", "NS16X"):
+        for nm in ("NS16", "NS16X", "C3", "C4"):
             r = run_config(nm, max(3, args.steps // 2), 1, rank, world)
             r.pop("batch")
             torch.cuda.empty_cache()
@@ -348,7 +348,9 @@ def main():
                 "verify_kernel_GiBps": round(r["kernels"]["verify"]["gibs_checksummed"], 1),
                 "verify_roofline_frac": round(r["kernels"]["verify"]["frac"], 4),
                 "trailer_kernel_GiBps": round(r["kernels"]["trailer"]["gibs_checksummed"], 1),
-                "trailer_roofline_frac": round(r["kernels"]["trailer"]["frac"], 4)}
+                "trailer_roofline_frac": round(r["kernels"]["trailer"]["frac"], 4),
+                "verify_kernel": r["kernels"]["verify"]["name"],
+                "trailer_kernel": r["kernels"]["trailer"]["name"]}
     if world == 1 and not args.no_extras and args.config == "C2":
         extras["C5_wal"] = run_wal(max(3, args.steps // 2), 1)
         torch.cuda.empty_cache()

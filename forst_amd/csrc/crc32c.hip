@@ -1582,7 +1582,12 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
   // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2 %; v2 wins on
   // the 4/16/64 KiB mix by 4 % and at 64 KiB by 45 %, where the rows of a
   // wave stream addresses 64 KiB apart)
-  const bool small_blocks = a.base_len / a.n <= 20480;
+  // ... and only with at least four 64-block chunks per wave: the rows
+  // kernel's work feed deals 64-block chunks, so with fewer the last chunk is
+  // a large part of a wave's work (C4, 512 K x 16 KiB: rows 0.645, v2 0.714)
+  const uint64_t mean = a.base_len / a.n;
+  const bool small_blocks =
+      mean <= 20480 && (mean <= 8192 || a.n >= uint64_t(4) * kBatch * kWaves * grid);
   // (the rows kernel indexes descriptors with 32 bits)
   const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
                                             ((!variant || !*variant) &&

@@ -25,6 +25,7 @@ CONFIGS = {
     "C64": (1 << 18, 65536, 1), "X64": (1 << 18, 65536, 4),
     "LOGU": (1 << 23, ("logu", 32, 32768), 1), "LOGU64": (1 << 23, ("logu", 64, 32768), 1),
     "LOGU1K": (1 << 22, ("logu", 1024, 32768), 1),
+    "C4": (1 << 19, 16384, 1), "C4X": (1 << 19, 16384, 4),
     "H32": (1 << 20, 16384, 2), "H64": (1 << 20, 16384, 3), "H64S": (1 << 20, 4096, 3),
 }
 

@@ -8,7 +8,9 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-LIB_PATH = os.path.join(_HERE, "lib", "libforst_checksum.so")
+# FORST_LIB_PATH: another build of the same library (A/B of two builds in
+# separate processes, tools/gpu_build_ab.sh); the default is the in-tree build
+LIB_PATH = os.environ.get("FORST_LIB_PATH") or os.path.join(_HERE, "lib", "libforst_checksum.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 _lib = None

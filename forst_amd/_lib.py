@@ -61,6 +61,7 @@ def lib():
         "forst_sst_properties_decode": (i, [vp, u64, vp]),
         "forst_sst_last_error": (ctypes.c_char_p, []),
         "forst_sst_verify_file": (i, [vp, u64, vp, ctypes.c_char_p, vp, vp]),
+        "forst_sst_verify_files": (i, [vp, vp, vp, vp, u64, vp, u64, vp, vp]),
         "forst_crc32c_combine_batch": (i, [vp, vp, vp, vp, u64, vp]),
         "forst_crc32c_combine": (u32, [u32, u32, u64]),
         "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),

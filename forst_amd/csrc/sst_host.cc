@@ -17,6 +17,7 @@
 //   properties       table/meta_blocks.cc:56-140, block_based_table_reader.cc:
 //                    948-972 (index type, value delta flag, first-key flag)
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
 #include <string>
 #include <vector>
@@ -336,11 +337,14 @@ Status hip_status(hipError_t e, const char* what) {
 
 }  // namespace
 
-Status VerifySstFileChecksums(BlockChecksumEngine& eng, const uint8_t* host_file,
-                              uint64_t file_size, const uint8_t* dev_file,
-                              const std::string& file_name, SstVerifyReport* report) {
-  SstVerifyReport local;
-  SstVerifyReport& rep = report ? *report : local;
+// The whole VerifyChecksum walk of one file.  With `bulk` null the final
+// batch (every meta block, then every data block) is verified here; with
+// `bulk` set its handles are returned instead, already past every structural
+// check, so a multi-file caller can verify the blocks of many files in one
+// launch (VerifySstFilesChecksums below).
+static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, uint64_t file_size,
+                          const uint8_t* dev_file, const std::string& file_name,
+                          SstVerifyReport& rep, uint32_t* bcc_out, std::vector<Handle>* bulk) {
   rep = SstVerifyReport();
   hipStream_t st = static_cast<hipStream_t>(eng.stream());
   // 1. footer (ReadFooterFromFile, format.cc:486-553)
@@ -352,6 +356,7 @@ Status VerifySstFileChecksums(BlockChecksumEngine& eng, const uint8_t* host_file
   rep.checksum_type = f.checksum_type;
   const ChecksumType type = static_cast<ChecksumType>(f.checksum_type);
   const uint32_t bcc = f.base_context_checksum;
+  if (bcc_out) *bcc_out = bcc;
   // footer checksum (fv >= 6): ComputeBuiltinChecksum over the 53 footer bytes
   // with the field zeroed, + ChecksumModifierForContext(base, footer_offset),
   // on the GPU (compute mode: 52 bytes + the last one from memory)
@@ -491,19 +496,144 @@ Status VerifySstFileChecksums(BlockChecksumEngine& eng, const uint8_t* host_file
   // 5. every meta block, then every data block, in one launch
   std::vector<Handle> all(meta_blocks);
   all.insert(all.end(), data.begin(), data.end());
+  if (bulk) {
+    for (const Handle& h : all)
+      if (h.off > file_size || h.size > file_size - h.off || file_size - h.off - h.size < kBlockTrailer)
+        return Status::Corruption("block handle past end of file in " + file_name);
+    for (const Handle& h : all)
+      if (h.size > 0xffffffffull) return Status::NotSupported("block larger than 4 GiB");
+    bulk->swap(all);
+    return Status::OK();
+  }
   return verify(all, &rep.failed);
+}
+
+Status VerifySstFileChecksums(BlockChecksumEngine& eng, const uint8_t* host_file,
+                              uint64_t file_size, const uint8_t* dev_file,
+                              const std::string& file_name, SstVerifyReport* report) {
+  SstVerifyReport local;
+  return WalkSstFile(eng, host_file, file_size, dev_file, file_name, report ? *report : local,
+                     nullptr, nullptr);
+}
+
+// DB::VerifyChecksum over many files (db_impl.cc:6254 walks every live SST
+// file, convenience.cc:57 per file).  Structural blocks are checked per file
+// (they gate the decoding of what follows); the meta + data blocks of ALL
+// files then go to the GPU as one batch per checksum type over the arena,
+// with per-block context modifiers (fv >= 6 files carry their own base).
+std::vector<Status> VerifySstFilesChecksums(BlockChecksumEngine& eng,
+                                            const std::vector<SstFileRef>& files,
+                                            const uint8_t* dev_arena, uint64_t arena_len,
+                                            std::vector<SstVerifyReport>* reports) {
+  const size_t nf = files.size();
+  std::vector<Status> out(nf);
+  std::vector<SstVerifyReport> local;
+  std::vector<SstVerifyReport>& reps = reports ? *reports : local;
+  reps.assign(nf, SstVerifyReport());
+  hipStream_t st = static_cast<hipStream_t>(eng.stream());
+  struct Blk {
+    uint32_t file, idx;
+    uint64_t off;  // in the file
+    uint32_t size;
+  };
+  std::vector<Blk> by_type[5];
+  std::vector<uint32_t> bcc(nf, 0);
+  for (size_t f = 0; f < nf; ++f) {
+    const SstFileRef& r = files[f];
+    if (r.dev_offset > arena_len || r.file_size > arena_len - r.dev_offset) {
+      out[f] = Status::InvalidArgument("file " + r.file_name + " outside the device arena");
+      continue;
+    }
+    std::vector<Handle> bulk;
+    out[f] = WalkSstFile(eng, r.host_file, r.file_size, dev_arena + r.dev_offset, r.file_name,
+                         reps[f], &bcc[f], &bulk);
+    if (!out[f].ok()) continue;
+    const int t = reps[f].checksum_type;
+    if (t < 0 || t > 4) {
+      out[f] = Status::Corruption("Corrupt or unsupported checksum type: " + std::to_string(t));
+      continue;
+    }
+    for (size_t i = 0; i < bulk.size(); ++i)
+      by_type[t].push_back({uint32_t(f), uint32_t(i), bulk[i].off, uint32_t(bulk[i].size)});
+  }
+  for (int t = 0; t < 5; ++t) {
+    const std::vector<Blk>& v = by_type[t];
+    if (v.empty()) continue;
+    const uint64_t n = v.size();
+    std::vector<uint64_t> offs(n);
+    std::vector<uint32_t> sz(n), mods(n);
+    for (uint64_t i = 0; i < n; ++i) {
+      offs[i] = files[v[i].file].dev_offset + v[i].off;
+      sz[i] = v[i].size;
+      mods[i] = ChecksumModifierForContext(bcc[v[i].file], v[i].off);
+    }
+    // device layout: offsets | sizes | modifiers | computed | stored | ok | bad
+    const uint64_t need = n * (8 + 4 + 4 + 4 + 4 + 1) + 64;
+    void* d = nullptr;
+    Status s = hip_status(hipMallocAsync(&d, need, st), "hipMallocAsync");
+    std::vector<uint8_t> ok(n);
+    std::vector<uint32_t> computed(n), stored(n);
+    if (s.ok()) {
+      uint8_t* p = static_cast<uint8_t*>(d);
+      uint64_t* doffs = reinterpret_cast<uint64_t*>(p);
+      uint32_t* dsz = reinterpret_cast<uint32_t*>(p + n * 8);
+      uint32_t* dmod = dsz + n;
+      uint32_t* dcomp = dmod + n;
+      uint32_t* dstor = dcomp + n;
+      uint8_t* dok = reinterpret_cast<uint8_t*>(dstor + n);
+      unsigned long long* dbad =
+          reinterpret_cast<unsigned long long*>(p + ((n * 24 + n + 7) & ~uint64_t(7)));
+      unsigned long long bad = 0;
+      s = hip_status(hipMemcpyAsync(doffs, offs.data(), n * 8, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+      if (s.ok()) s = hip_status(hipMemcpyAsync(dsz, sz.data(), n * 4, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+      if (s.ok()) s = hip_status(hipMemcpyAsync(dmod, mods.data(), n * 4, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+      if (s.ok()) s = hip_status(hipMemsetAsync(dbad, 0, 8, st), "hipMemsetAsync");
+      if (s.ok()) {
+        int rc = forst_block_verify_batch(t, dev_arena, arena_len, doffs, dsz, dmod, dcomp, dstor,
+                                          dok, dbad, n, eng.stream());
+        if (rc) s = Status::IOError(std::string("verify launch: ") + forst_last_error());
+      }
+      if (s.ok()) s = hip_status(hipMemcpyAsync(&bad, dbad, 8, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+      if (s.ok()) s = hip_status(hipStreamSynchronize(st), "hipStreamSynchronize");
+      if (s.ok() && bad) {
+        s = hip_status(hipMemcpyAsync(ok.data(), dok, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+        if (s.ok()) s = hip_status(hipMemcpyAsync(computed.data(), dcomp, n * 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+        if (s.ok()) s = hip_status(hipMemcpyAsync(stored.data(), dstor, n * 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+        if (s.ok()) s = hip_status(hipStreamSynchronize(st), "hipStreamSynchronize");
+      } else {
+        std::fill(ok.begin(), ok.end(), 1);
+      }
+      (void)hipFreeAsync(d, st);
+    }
+    const ChecksumType type = static_cast<ChecksumType>(t);
+    for (uint64_t i = 0; i < n; ++i) {
+      const Blk& b = v[i];
+      if (!s.ok()) {
+        if (out[b.file].ok()) out[b.file] = s;
+        continue;
+      }
+      reps[b.file].blocks_verified += 1;
+      if (ok[i]) continue;
+      reps[b.file].failed.push_back(b.idx);
+      if (out[b.file].ok()) {  // blocks of a file are in walk order: first failure wins
+        uint32_t st_v = stored[i], co_v = computed[i];
+        if (type == kCRC32c) {  // reader_common.cc:50-54
+          st_v = crc32c::Unmask(st_v);
+          co_v = crc32c::Unmask(co_v);
+        }
+        out[b.file] = Status::Corruption(BlockChecksumMismatchMessage(
+            type, st_v, co_v, mods[i] != 0, files[b.file].file_name, b.off, b.size));
+      }
+    }
+  }
+  return out;
 }
 
 }  // namespace forstdb
 
-extern "C" __attribute__((visibility("default"))) int forst_sst_verify_file(
-    const uint8_t* host_file, uint64_t file_size, const uint8_t* dev_file, const char* file_name,
-    forst_sst_verify_result* out, void* stream) {
-  if (!host_file || !dev_file || !out) return FORST_EINVAL;
-  forstdb::BlockChecksumEngine eng(stream);
-  forstdb::SstVerifyReport rep;
-  forstdb::Status s = forstdb::VerifySstFileChecksums(eng, host_file, file_size, dev_file,
-                                                      file_name ? file_name : "", &rep);
+namespace {
+void fill_result(forst_sst_verify_result* out, const forstdb::Status& s,
+                 const forstdb::SstVerifyReport& rep) {
   std::memset(out, 0, sizeof(*out));
   out->status = s.code();
   out->blocks_verified = rep.blocks_verified;
@@ -515,5 +645,39 @@ extern "C" __attribute__((visibility("default"))) int forst_sst_verify_file(
   out->checksum_type = rep.checksum_type;
   out->index_type = rep.index_type;
   std::strncpy(out->message, s.ok() ? "OK" : s.ToString().c_str(), sizeof(out->message) - 1);
+}
+}  // namespace
+
+extern "C" __attribute__((visibility("default"))) int forst_sst_verify_files(
+    const uint8_t* const* host_files, const uint64_t* file_sizes, const uint64_t* dev_offsets,
+    const uint8_t* dev_arena, uint64_t arena_len, const char* const* file_names, uint64_t n_files,
+    forst_sst_verify_result* out, void* stream) {
+  if (n_files == 0) return FORST_OK;
+  if (!host_files || !file_sizes || !dev_offsets || !dev_arena || !out) return FORST_EINVAL;
+  std::vector<forstdb::SstFileRef> files(n_files);
+  for (uint64_t i = 0; i < n_files; ++i) {
+    if (!host_files[i]) return FORST_EINVAL;
+    files[i].host_file = host_files[i];
+    files[i].file_size = file_sizes[i];
+    files[i].dev_offset = dev_offsets[i];
+    files[i].file_name = (file_names && file_names[i]) ? file_names[i] : "";
+  }
+  forstdb::BlockChecksumEngine eng(stream);
+  std::vector<forstdb::SstVerifyReport> reps;
+  std::vector<forstdb::Status> st =
+      forstdb::VerifySstFilesChecksums(eng, files, dev_arena, arena_len, &reps);
+  for (uint64_t i = 0; i < n_files; ++i) fill_result(&out[i], st[i], reps[i]);
+  return FORST_OK;
+}
+
+extern "C" __attribute__((visibility("default"))) int forst_sst_verify_file(
+    const uint8_t* host_file, uint64_t file_size, const uint8_t* dev_file, const char* file_name,
+    forst_sst_verify_result* out, void* stream) {
+  if (!host_file || !dev_file || !out) return FORST_EINVAL;
+  forstdb::BlockChecksumEngine eng(stream);
+  forstdb::SstVerifyReport rep;
+  forstdb::Status s = forstdb::VerifySstFileChecksums(eng, host_file, file_size, dev_file,
+                                                      file_name ? file_name : "", &rep);
+  fill_result(out, s, rep);
   return FORST_OK;
 }

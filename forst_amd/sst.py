@@ -102,3 +102,32 @@ def verify_file(file_bytes, dev=None, file_name="", stream=None):
     _rc(lib().forst_sst_verify_file(a.ctypes.data, len(a), dev.data_ptr(), file_name.encode(),
                                     ctypes.byref(r), st))
     return r
+
+
+def verify_files(files, file_names=None, stream=None, align=256):
+    """DB::VerifyChecksum over many SST files: all files are staged in ONE
+    device arena (each at an `align`-aligned offset); structural blocks are
+    checked per file, the meta and data blocks of every file in one launch per
+    checksum type (forst_sst_verify_files).  Returns one VerifyResult per file."""
+    hs = [_host(f) for f in files]
+    names = file_names or [f"{i:06d}.sst" for i in range(len(hs))]
+    offs, pos = [], 0
+    for a in hs:
+        offs.append(pos)
+        pos += (len(a) + align - 1) // align * align
+    arena = np.zeros(max(pos, 1), dtype=np.uint8)
+    for a, o in zip(hs, offs):
+        arena[o:o + len(a)] = a
+    dev = torch.from_numpy(arena).to("cuda")
+    n = len(hs)
+    ptrs = (ctypes.c_void_p * n)(*[a.ctypes.data for a in hs])
+    sizes = (ctypes.c_uint64 * n)(*[len(a) for a in hs])
+    doffs = (ctypes.c_uint64 * n)(*offs)
+    enc = [s.encode() for s in names]
+    cnames = (ctypes.c_char_p * n)(*enc)
+    out = (VerifyResult * n)()
+    st = torch.cuda.current_stream().cuda_stream if stream is None else stream
+    torch.cuda.synchronize()
+    _rc(lib().forst_sst_verify_files(ptrs, sizes, doffs, ctypes.c_void_p(dev.data_ptr()),
+                                     ctypes.c_uint64(pos), cnames, ctypes.c_uint64(n), out, st))
+    return list(out)

@@ -156,4 +156,19 @@ Status VerifySstFileChecksums(BlockChecksumEngine& engine, const uint8_t* host_f
                               uint64_t file_size, const uint8_t* dev_file,
                               const std::string& file_name, SstVerifyReport* report = nullptr);
 
+// DB::VerifyChecksum over many SST files staged in one device arena (file i
+// at dev_arena + dev_offset): structural blocks per file, then the meta and
+// data blocks of every file in one batch launch per checksum type.  Returns
+// one Status per file (the same Status VerifySstFileChecksums returns).
+struct SstFileRef {
+  const uint8_t* host_file = nullptr;
+  uint64_t file_size = 0;
+  uint64_t dev_offset = 0;
+  std::string file_name;
+};
+std::vector<Status> VerifySstFilesChecksums(BlockChecksumEngine& engine,
+                                            const std::vector<SstFileRef>& files,
+                                            const uint8_t* dev_arena, uint64_t arena_len,
+                                            std::vector<SstVerifyReport>* reports = nullptr);
+
 }  // namespace forstdb

@@ -331,6 +331,18 @@ const char* forst_sst_last_error(void);
 int forst_sst_verify_file(const uint8_t* host_file, uint64_t file_size, const uint8_t* dev_file,
                           const char* file_name, forst_sst_verify_result* out, void* stream);
 
+/* DB::VerifyChecksum (db/db_impl/db_impl.cc:6254 -> convenience.cc:57 per
+ * file) over n_files SST files: file i is host_files[i] (file_sizes[i] bytes)
+ * in host memory and dev_arena[dev_offsets[i] ..] in device memory.  Each
+ * file's structural blocks are checked as in forst_sst_verify_file; the meta
+ * and data blocks of ALL files are then verified in one launch per checksum
+ * type.  out[i] = exactly what forst_sst_verify_file returns for file i.
+ * Synchronous. */
+int forst_sst_verify_files(const uint8_t* const* host_files, const uint64_t* file_sizes,
+                           const uint64_t* dev_offsets, const uint8_t* dev_arena,
+                           uint64_t arena_len, const char* const* file_names, uint64_t n_files,
+                           forst_sst_verify_result* out, void* stream);
+
 #ifdef __cplusplus
 }
 #endif

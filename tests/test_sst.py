@@ -232,3 +232,44 @@ def test_decoders_survive_random_corruption():
                 sst.decode_footer(bytes(f[:-53]) + bytes(t))
             except Exception as e:  # corruption / unsupported, never a crash
                 assert isinstance(e, sst.ForstError) or "block-based" in str(e)
+
+
+@pytest.mark.gpu
+def test_verify_files_batch():
+    """forst_sst_verify_files (DB::VerifyChecksum over many files, one bulk
+    launch per checksum type) returns, per file, exactly what
+    forst_sst_verify_file returns -- clean files and corrupted ones mixed."""
+    files, names = [], []
+    for k, (fv, ct, it, ri) in enumerate(CASES):
+        w, f = make(fv, ct, it, ri, seed=20 + k)
+        b = bytearray(f)
+        if k % 3 == 1:  # a data block of every third file corrupted
+            o, n = blocks_of(w, "data")[5 + k]
+            b[o + n // 3] ^= 0x10
+        elif k % 3 == 2 and fv >= 1:  # a filter (meta) block and a data block
+            fo, fn = blocks_of(w, "filter")[0]
+            b[fo + 1] ^= 2
+            o, n = blocks_of(w, "data")[0]
+            b[o] ^= 1
+        files.append(bytes(b))
+        names.append(f"/db/{100 + k:06d}.sst")
+    files.append(b"\0" * 10)  # too short for a footer
+    names.append("/db/short.sst")
+    rs = sst.verify_files(files, names)
+    assert len(rs) == len(files)
+    for f, name, r in zip(files, names, rs):
+        one = sst.verify_file(f, file_name=name)
+        assert (r.status, r.message) == (one.status, one.message), name
+        assert (r.n_failed, r.blocks_verified, r.data_blocks) == \
+            (one.n_failed, one.blocks_verified, one.data_blocks), name
+    assert sum(r.status == 2 for r in rs) >= 8
+
+
+@pytest.mark.gpu
+def test_verify_files_many():
+    """64 files of 300 blocks each (every type, fv 5/6) in one call: all OK."""
+    files = [make(5 + (k & 1), (k % 4) + 1, (0, 2, 3)[k % 3], 1, seed=100 + k, n_data=300)[1]
+             for k in range(64)]
+    rs = sst.verify_files(files)
+    assert all(r.status == 0 for r in rs), [r.message for r in rs if r.status]
+    assert all(r.data_blocks == 300 for r in rs)

@@ -127,3 +127,23 @@ def test_crc32c_combine_host_matches_reference_tests():
     for n in (1 << 33, (1 << 40) + 7, (1 << 63) + 5):  # shift powers beyond memory sizes
         assert engine.crc32c_combine(0, 0, n) == 0
         assert engine.crc32c_combine(c1, 0, n) == O.crc32c_combine(c1, 0, n)
+
+
+def test_sst_verify_files_argument_errors():
+    """forst_sst_verify_files rejects missing arrays before any HIP call, and
+    an empty file set is a no-op (no GPU needed for either)."""
+    L = _lib.lib()
+    n = 2
+    out = (ctypes.c_char * 4096)()
+    assert L.forst_sst_verify_files(None, None, None, None, 0, None, 0, out, None) == 0
+    sizes = (ctypes.c_uint64 * n)(100, 100)
+    offs = (ctypes.c_uint64 * n)(0, 256)
+    ptrs = (ctypes.c_void_p * n)(None, None)
+    assert L.forst_sst_verify_files(None, sizes, offs, ctypes.c_void_p(1), 512, None, n,
+                                    out, None) == -1
+    assert L.forst_sst_verify_files(ptrs, sizes, offs, None, 512, None, n, out, None) == -1
+    assert L.forst_sst_verify_files(ptrs, sizes, offs, ctypes.c_void_p(1), 512, None, n,
+                                    None, None) == -1
+    # a null host file pointer inside the array
+    assert L.forst_sst_verify_files(ptrs, sizes, offs, ctypes.c_void_p(1), 512, None, n,
+                                    out, None) == -1

@@ -2,26 +2,37 @@
 """bench.py -- device-resident block-checksum throughput on MI355X.
 
 Metric (BASELINE.json): device-resident GiB/s checksummed (CRC32C/XXH3).
-Default workload = configs[1] ("C2"): 1 M x 4 KiB SST blocks, kCRC32c,
-compute (write side: trailer kernel, ComputeBuiltinChecksumWithLastByte +
-trailer, block_based_table_builder.cc:1340) + verify (read side,
+Default workload = configs[1] ("C2"): 1 M x 4 KiB SST blocks per GPU,
+kCRC32c, compute (write side: trailer pass, ComputeBuiltinChecksumWithLastByte
++ trailer, block_based_table_builder.cc:1340) + verify (read side,
 VerifyBlockChecksum, reader_common.cc:26).  One step = both passes over the
-whole batch; checksummed bytes per pass = sum(size + 1).
+rank's blocks; checksummed bytes per pass = sum(size + 1).
 
-Multi-GPU: one process per GPU (torch.distributed.run), each rank owns its
-own shard of blocks (weak scaling, no data-path collective: blocks are
-independent -- SURVEY.md §8e); barrier + synchronize bracket the timed steps,
-the max over ranks is reported and value = all ranks' bytes / that time.
+Multi-GPU: `--gpus N` runs one process per GPU.  Launched
+without a torch.distributed environment, bench.py starts
+`torch.distributed.run --nproc-per-node N` itself (as a child process, before
+any GPU call) and exits with its code.  The N ranks share ONE described batch
+of N x n blocks (weak scaling: n blocks of work per GPU) and each takes its
+byte-balanced contiguous slice (forst_amd.shard.rank_slice) -- the bytes of a
+block are the same whichever rank hashes it.  No collective touches the data
+path: barrier + synchronize bracket the timed steps, the elapsed time is the
+max over ranks and value = all ranks' checksummed bytes / that time.
+`--dry-run` runs the same sharding on the CPU (gloo, no GPU call) and checks
+that the ranks cover every block exactly once.
 
-Also reported: per-kernel roofline (HIP events on the launch stream),
-the CPU baseline (oracle = our restatement, timed on this host), the
-north-star point (1 M x 16 KiB, CRC32C and XXH3) and the PCIe-inclusive
-end-to-end rate.
+Also reported: per-kernel roofline (HIP events on the launch stream, and the
+kernel-trace average of the committed rocprofv3 profile of the same config),
+HBM traffic from the committed PMC summary, the CPU baseline (oracle = our
+restatement, timed on this host), the north-star point (1 M x 16 KiB, CRC32C
+and XXH3), C3/C4, the WAL config C5 and the PCIe-inclusive end-to-end rates
+(DESIGN.md §6).
 """
 import argparse
 import glob
 import json
 import os
+import socket
+import subprocess
 import sys
 import time
 
@@ -39,42 +50,44 @@ GIB = float(1 << 30)
 METRIC = "device-resident GiB/s checksummed (CRC32C/XXH3), 4–64 KiB blocks, 1/2/4/8 GPU"
 
 CONFIGS = {
-    # name: (n_blocks, size spec, checksum, description)
+    # name: (blocks per GPU, size spec, checksum, description)
     "C2": (1 << 20, 4096, 1, "1 M x 4 KiB kCRC32c compute+verify"),
     "C3": (1 << 20, (4096, 16384, 65536), 4, "1 M mixed 4/16/64 KiB kXXH3 compute+verify"),
     "C4": (1 << 19, 16384, 1, "compaction-shaped 8 GiB/GPU of 16 KiB kCRC32c compute+verify"),
     "NS16": (1 << 20, 16384, 1, "north-star 1 M x 16 KiB kCRC32c compute+verify"),
     "NS16X": (1 << 20, 16384, 4, "north-star 1 M x 16 KiB kXXH3 compute+verify"),
 }
+SEEDS = {"C2": 0xF0E5700002, "C3": 0xF0E5700003, "C4": 0xF0E5700004,
+         "NS16": 0xF0E5700002, "NS16X": 0xF0E5700002}
 
 
-def dist_setup():
-    return shard.setup()
-
-
-def barrier(world):
-    shard.barrier(world)
-
-
-def max_over_ranks(x, world):
-    return shard.max_over_ranks(x, world)
-
-
-def algorithmic_bytes(kind, b):
+def algorithmic_bytes(kind, payload_bytes, n):
     """per-launch algorithmic HBM bytes:
     trailer: read n + type byte (1) + descriptor (12); write trailer (5)
     verify : read n+5 + descriptor (12); write computed (4) + ok (1)"""
     if kind == "trailer":
-        return b.payload_bytes + b.n * (1 + 12 + 5)
-    return b.payload_bytes + b.n * (5 + 12 + 4 + 1)
+        return payload_bytes + n * (1 + 12 + 5)
+    return payload_bytes + n * (5 + 12 + 4 + 1)
 
 
-def run_config(name, steps, warmup, rank, world, seed_base=None):
-    from forst_amd import engine, workload
+def describe(name, world):
+    """the global batch of a config at world size N: N x n blocks (weak
+    scaling), one splitmix64 byte stream; returns (sizes, ctype, desc, seed)"""
+    from forst_amd import workload
 
     n, spec, ctype, desc = CONFIGS[name]
-    seed = workload.SEEDS.get(name[:2], 0xF0E5700002) + rank * 0x1000
-    b = workload.make_sst_batch(n, spec, seed, ctype=ctype)
+    seed = SEEDS[name]
+    return workload.block_sizes(n * world, spec, seed), ctype, desc, seed
+
+
+def run_config(name, steps, warmup, rank, world):
+    from forst_amd import engine, workload
+
+    sizes_all, ctype, desc, seed = describe(name, world)
+    lo, hi, start = shard.rank_slice(sizes_all, rank, world)
+    b = workload.make_sst_batch(hi - lo, None, seed, ctype=ctype, sizes=sizes_all[lo:hi],
+                                stream_start=start)
+    n = b.n
     ok = torch.empty(n, dtype=torch.uint8, device="cuda")
     comp = torch.empty(n, dtype=torch.uint32, device="cuda")
     bad = torch.zeros(1, dtype=torch.int64, device="cuda")
@@ -92,7 +105,7 @@ def run_config(name, steps, warmup, rank, world, seed_base=None):
             ev[2].record()
 
     names = {}
-    for w in range(max(1, warmup)):
+    for _ in range(max(1, warmup)):
         engine.block_trailer_batch(ctype, b.base, b.offsets, b.sizes, b.types)
         names["trailer"] = engine.last_kernel()
         engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes, computed=comp,
@@ -100,32 +113,36 @@ def run_config(name, steps, warmup, rank, world, seed_base=None):
         names["verify"] = engine.last_kernel()
     torch.cuda.synchronize()
     bad.zero_()
+    # HIP events on the launch stream (torch's current stream, which the
+    # engine wrappers launch on)
     evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
-    barrier(world)
+    shard.barrier(world)
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k in range(steps):
         step(evs[k])
     torch.cuda.synchronize()
     t1 = time.perf_counter()
-    barrier(world)
-    elapsed = max_over_ranks(t1 - t0, world)
-    mism = int(bad.item())
+    shard.barrier(world)
+    elapsed = shard.max_over_ranks(t1 - t0, world)
+    mism = shard.sum_over_ranks(int(bad.item()), world)
     assert mism == 0, f"{mism} blocks failed verification in the timed region"
+    blocks_total = shard.sum_over_ranks(n, world)
+    assert blocks_total == len(sizes_all), "ranks must cover the described batch"
     t_tr = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
     t_vf = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
-    bytes_per_step = 2 * b.checksummed_bytes
+    bytes_all = int(sizes_all.astype(np.int64).sum()) + len(sizes_all)  # checksummed, all ranks
     res = {
-        "name": name, "desc": desc, "n": n, "ctype": ctype,
-        "elapsed": elapsed, "steps": steps,
-        "gibs_total": bytes_per_step * steps * world / elapsed / GIB,
+        "name": name, "desc": desc, "n": n, "n_total": len(sizes_all), "ctype": ctype,
+        "elapsed": elapsed, "steps": steps, "shard": [lo, hi],
+        "gibs_total": 2 * bytes_all * steps / elapsed / GIB,
         "ms_per_step": elapsed / steps * 1e3,
         "kernels": {
-            "trailer": {"name": names["trailer"],
-                        "avg_s": t_tr, "alg_bytes": algorithmic_bytes("trailer", b),
+            "trailer": {"name": names["trailer"], "avg_s": t_tr,
+                        "alg_bytes": algorithmic_bytes("trailer", b.payload_bytes, n),
                         "gibs_checksummed": b.checksummed_bytes / t_tr / GIB},
-            "verify": {"name": names["verify"],
-                       "avg_s": t_vf, "alg_bytes": algorithmic_bytes("verify", b),
+            "verify": {"name": names["verify"], "avg_s": t_vf,
+                       "alg_bytes": algorithmic_bytes("verify", b.payload_bytes, n),
                        "gibs_checksummed": b.checksummed_bytes / t_vf / GIB},
         },
         "batch": b,
@@ -143,7 +160,8 @@ def run_wal(steps, warmup, n_records=10_000_000):
     record CRC (log_reader.cc ReadPhysicalRecord).  Algorithmic bytes:
     verify  = whole log read + per log block status/nrec/fail_off (9 B);
     writer  = headers+payloads read + offset (8) + CRC written twice (in place
-              and out, 4+4) per physical record."""
+              and out, 4+4) per physical record;
+    record XXH3 (a14) = payload bytes read + 8 B header offset + 8 B hash."""
     from forst_amd import engine, workload
 
     w = workload.make_wal_batch(n_records, workload.SEEDS["C5"])
@@ -180,8 +198,7 @@ def run_wal(steps, warmup, n_records=10_000_000):
     torch.cuda.synchronize()
     assert int(bad.item()) == 0, "WAL blocks failed verification in the timed region"
     assert int(nrec.sum().item()) == len(w.rec_offsets)
-    # a14: XXH3 of every logical record (gather of multi-fragment records +
-    # two raw XXH3 batches); includes its one stream synchronisation
+    # a14: XXH3 of every logical record; includes its stream synchronisation
     hs = []
     for _ in range(max(2, steps // 2)):
         torch.cuda.synchronize()
@@ -193,9 +210,11 @@ def run_wal(steps, warmup, n_records=10_000_000):
     t_h = float(np.median(hs))
     t_w = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
     t_v = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
-    rec_bytes = int(w.rec_lengths.astype(np.int64).sum()) + 7 * len(w.rec_offsets)
+    payload = int(w.rec_lengths.astype(np.int64).sum())
+    rec_bytes = payload + 7 * len(w.rec_offsets)
     alg_v = w.total + 9 * nb
     alg_w = rec_bytes + 16 * len(w.rec_offsets)
+    alg_h = payload + 16 * len(w.rec_offsets)
     out = {"desc": f"{n_records} records log-uniform 32..32768 B, "
                    f"{w.total / GIB:.1f} GiB log, {len(w.rec_offsets)} physical records",
            "verify_GiBps": round(w.total / t_v / GIB, 1),
@@ -204,18 +223,38 @@ def run_wal(steps, warmup, n_records=10_000_000):
            "writer_crc_GiBps": round(rec_bytes / t_w / GIB, 1),
            "writer_crc_ms": round(t_w * 1e3, 3),
            "writer_roofline_frac": round(alg_w / t_w / 1e9 / HBM_PEAK_GBS, 4),
-           "record_xxh3_GiBps": round(rec_bytes / t_h / GIB, 1),
-           "record_xxh3_ms": round(t_h * 1e3, 3)}
+           "record_xxh3_GiBps": round(payload / t_h / GIB, 1),
+           "record_xxh3_ms": round(t_h * 1e3, 3),
+           "record_xxh3_roofline_frac": round(alg_h / t_h / 1e9 / HBM_PEAK_GBS, 4)}
     del w
     return out
 
 
+def cpu_threads():
+    """(threads to use, how the count was found): every CPU this process may
+    run on (sched_getaffinity), capped by a cgroup CPU quota when one is set;
+    os.cpu_count() is reported beside it."""
+    n = len(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else os.cpu_count()
+    how = "sched_getaffinity"
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, p = f.read().split()
+        if q != "max":
+            cap = max(1, int(int(q) // int(p)))
+            if cap < n:
+                n, how = cap, "cgroup cpu.max quota"
+    except (OSError, ValueError):
+        pass
+    return max(1, n or 1), how
+
+
 def cpu_baseline(b, ctype, budget_s=12.0):
     """Time the oracle (our CPU restatement, compiled -O3 -march=x86-64-v3 with
-    SSE4.2 crc32 3-way + AVX2 XXH3) on a bounded sample of the same blocks."""
+    SSE4.2 crc32 3-way + AVX2 XXH3) on a bounded sample of the same blocks,
+    on every CPU this process may use, and on one thread."""
     from oracle import oracle as O
 
-    nthreads = min(16, os.cpu_count() or 1)
+    nthreads, how = cpu_threads()
     ns = min(b.n, 1 << 18)  # up to 256 K blocks (~1 GiB of 4 KiB blocks)
     offs = b.offsets[:ns].cpu().numpy()
     sizes = b.sizes[:ns].cpu().numpy().astype(np.uint32)
@@ -234,7 +273,7 @@ def cpu_baseline(b, ctype, budget_s=12.0):
         return dt
 
     res = {}
-    for nt in (nthreads, 1):
+    for nt in sorted({nthreads, 1}, reverse=True):
         one_pass(nt)  # warm
         best, spent, reps = 1e30, 0.0, 0
         while reps < 5 and spent < budget_s / 2:
@@ -242,9 +281,11 @@ def cpu_baseline(b, ctype, budget_s=12.0):
             best, spent, reps = min(best, dt), spent + dt, reps + 1
         res[nt] = 2 * sample_bytes / best / GIB
     return {"value": round(res[nthreads], 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
+            "cores_from": how, "host_os_cpu_count": os.cpu_count(),
             "sample": f"first {ns} blocks of the same batch ({sample_bytes / GIB:.2f} GiB "
                       f"checksummed per pass), compute+verify, best of <=5, "
-                      f"oracle/oracle.c -O3 x86-64-v3 (SSE4.2 crc32 3-way, AVX2 XXH3)",
+                      f"oracle/oracle.c -O3 x86-64-v3 (SSE4.2 crc32 3-way, AVX2 XXH3), "
+                      f"one std::thread per core over contiguous block ranges",
             "single_thread_GiBps": round(res[1], 3)}
 
 
@@ -271,14 +312,13 @@ def end_to_end_pcie(b, ctype, chunk_blocks=1 << 16):
     doffs = [torch.empty(chunk_blocks, dtype=torch.int64, device="cuda") for _ in streams]
     oks = torch.empty(n, dtype=torch.uint8).pin_memory()
     dok = [torch.empty(chunk_blocks, dtype=torch.uint8, device="cuda") for _ in streams]
-    rel = (b.offsets - 0)  # device copy reused per chunk
     torch.cuda.synchronize()
     t0 = time.perf_counter()
     for k, (c0, c1, lo, hi) in enumerate(chunks):
         s = streams[k & 1]
         with torch.cuda.stream(s):
             dbufs[k & 1][:hi - lo].copy_(host[lo:hi], non_blocking=True)
-            doffs[k & 1][:c1 - c0].copy_(rel[c0:c1] - lo)
+            doffs[k & 1][:c1 - c0].copy_(b.offsets[c0:c1] - lo)
             engine.block_verify_batch(ctype, dbufs[k & 1][:hi - lo], doffs[k & 1][:c1 - c0],
                                       b.sizes[c0:c1], computed=None, stored=None,
                                       ok=dok[k & 1][:c1 - c0], stream=s)
@@ -289,25 +329,74 @@ def end_to_end_pcie(b, ctype, chunk_blocks=1 << 16):
     return b.checksummed_bytes / dt / GIB
 
 
-def load_traffic(kernel_name, config):
-    """HBM traffic per launch from the committed rocprofv3 PMC summary
-    (profiles/*pmc*.json written by profiles/collect_pmc.py), or None."""
-    parts = kernel_name.split("+")  # a pass of several kernels: sum of their traffic
-    best = None
-    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", "*pmc*.json"))):
+def _norm_kernel(name):
+    """rocprof / engine kernel names -> one form: 'crc32c_rows_kernel<verify>'"""
+    import re
+    modes = {"0": "compute", "1": "trailer", "2": "verify", "3": "raw"}
+    n = name.replace("forst::(anonymous namespace)::", "").replace("void ", "")
+    n = n.split("(forst::")[0].split("(unsigned")[0].strip()
+    return re.sub(r"<(\d)>", lambda m: "<" + modes[m.group(1)] + ">", n)
+
+
+def load_profile(kernel_name, config):
+    """(kernel-trace average ns, HBM bytes per launch) of the dominant kernel
+    from the newest committed rocprofv3 summary of this config
+    (profiles/pmc_<tag>_<config>.json, written by profiles/summarize.py from
+    a --kernel-trace --stats pass and separate FETCH_SIZE / WRITE_SIZE
+    passes), or (None, None)."""
+    parts = [_norm_kernel(p) for p in kernel_name.split("+")]
+    best = (None, None, None)
+    for f in sorted(glob.glob(os.path.join(ROOT, "profiles", f"pmc_*_{config}.json"))):
         try:
             with open(f) as fh:
                 d = json.load(fh)
-        except Exception:
+        except (OSError, ValueError):
             continue
-        got = {}
-        for row in d.get("kernels", []):
-            for p in parts:
-                if row.get("config") == config and row.get("kernel", "").startswith(p):
-                    got[p] = row.get("hbm_bytes_per_launch")
-        if len(got) == len(parts) and all(v is not None for v in got.values()):
-            best = sum(got.values())
+        rows = {_norm_kernel(r.get("kernel", "")): r for r in d.get("kernels", [])}
+        if all(p in rows for p in parts):
+            traffic = sum(rows[p].get("hbm_bytes_per_launch") or 0 for p in parts)
+            ns = sum(rows[p].get("avg_duration_ns_kernel_trace") or 0 for p in parts)
+            best = (ns or None, traffic or None, os.path.basename(f))
     return best
+
+
+def spawn_ranks(args):
+    """Start one process per GPU under torch.distributed.run (a child process,
+    started before any GPU call) and return its exit code."""
+    with socket.socket() as s:
+        s.bind(("127.0.0.1", 0))
+        port = s.getsockname()[1]
+    cmd = [sys.executable, "-m", "torch.distributed.run", "--nnodes=1",
+           f"--nproc-per-node={args.gpus}", "--master-addr", "127.0.0.1",
+           f"--master-port={port}", os.path.abspath(__file__)] + sys.argv[1:]
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    return subprocess.call(cmd, env=env)
+
+
+def dry_run(args, world, rank):
+    """the sharding of the described batch, on the CPU (gloo): every block
+    exactly once, byte-balanced"""
+    sizes_all, ctype, desc, seed = describe(args.config, world)
+    lo, hi, start = shard.rank_slice(sizes_all, rank, world)
+    got = [None] * world
+    if world > 1:
+        dist.all_gather_object(got, (lo, hi, start, int(sizes_all[lo:hi].astype(np.int64).sum())))
+    else:
+        got = [(lo, hi, start, int(sizes_all.astype(np.int64).sum()))]
+    if rank == 0:
+        cover = np.zeros(len(sizes_all), np.int32)
+        for lo_, hi_, _, _ in got:
+            cover[lo_:hi_] += 1
+        offs = np.concatenate([[0], np.cumsum(sizes_all.astype(np.int64) + 5)])
+        print(json.dumps({"dry_run": True, "config": args.config, "n_gpus": world,
+                          "blocks_total": len(sizes_all),
+                          "every_block_once": bool((cover == 1).all()),
+                          "starts_match": all(int(offs[lo_]) == st for lo_, _, st, _ in got),
+                          "shards": [{"lo": g[0], "hi": g[1], "bytes": g[3]} for g in got]}),
+              flush=True)
+    if world > 1:
+        dist.destroy_process_group()
 
 
 def main():
@@ -318,10 +407,20 @@ def main():
     ap.add_argument("--config", default="C2", choices=sorted(CONFIGS))
     ap.add_argument("--no-cpu-baseline", action="store_true")
     ap.add_argument("--no-extras", action="store_true",
-                    help="skip north-star and end-to-end extras")
+                    help="skip north-star, C3/C4, C5 and end-to-end extras")
+    ap.add_argument("--dry-run", action="store_true",
+                    help="shard the described batch on the CPU (gloo) without a GPU")
     args = ap.parse_args()
 
-    world, rank, local = dist_setup()
+    if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
+        sys.exit(spawn_ranks(args))
+    world, rank, local = shard.setup(cpu_only=args.dry_run)
+    if "WORLD_SIZE" in os.environ:
+        assert world == args.gpus, f"--gpus {args.gpus} but WORLD_SIZE={world}"
+    if world > 1:
+        assert dist.get_world_size() == world
+    if args.dry_run:
+        return dry_run(args, world, rank)
     from forst_amd import engine
 
     engine.init_device()
@@ -343,15 +442,17 @@ def main():
             r = run_config(nm, max(3, args.steps // 2), 1, rank, world)
             r.pop("batch")
             torch.cuda.empty_cache()
+            kv, kt = r["kernels"]["verify"], r["kernels"]["trailer"]
+            ns, _, _ = load_profile(kv["name"], nm)
             extras[nm] = {
                 "desc": r["desc"], "GiBps": round(r["gibs_total"], 1),
-                "verify_kernel_GiBps": round(r["kernels"]["verify"]["gibs_checksummed"], 1),
-                "verify_roofline_frac": round(r["kernels"]["verify"]["frac"], 4),
-                "trailer_kernel_GiBps": round(r["kernels"]["trailer"]["gibs_checksummed"], 1),
-                "trailer_roofline_frac": round(r["kernels"]["trailer"]["frac"], 4),
-                "verify_kernel": r["kernels"]["verify"]["name"],
-                "trailer_kernel": r["kernels"]["trailer"]["name"]}
-    if world == 1 and not args.no_extras and args.config == "C2":
+                "verify_kernel_GiBps": round(kv["gibs_checksummed"], 1),
+                "verify_roofline_frac": round(kv["frac"], 4),
+                "verify_roofline_frac_kernel_trace": (
+                    round(kv["alg_bytes"] / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if ns else None),
+                "trailer_kernel_GiBps": round(kt["gibs_checksummed"], 1),
+                "trailer_roofline_frac": round(kt["frac"], 4),
+                "verify_kernel": kv["name"], "trailer_kernel": kt["name"]}
         extras["C5_wal"] = run_wal(max(3, args.steps // 2), 1)
         torch.cuda.empty_cache()
     if rank != 0:
@@ -361,7 +462,7 @@ def main():
     kv = main_res["kernels"]["verify"]
     kt = main_res["kernels"]["trailer"]
     dom = kv if kv["avg_s"] >= kt["avg_s"] else kt
-    traffic = load_traffic(dom["name"], args.config)
+    ns, traffic, prof = load_profile(dom["name"], args.config)
     line = {
         "metric": METRIC,
         "value": round(main_res["gibs_total"], 2),
@@ -378,12 +479,20 @@ def main():
                 "written by the write-side kernel)",
         "config": {"workload": f"{args.config}: {main_res['desc']}",
                    "blocks_per_gpu": main_res["n"],
+                   "blocks_total": main_res["n_total"],
                    "checksum": {1: "kCRC32c", 4: "kXXH3"}[main_res["ctype"]],
                    "step": "trailer pass (write side) + verify pass (read side)",
-                   "parallelism": f"block shard per GPU x{world}, no collective"},
+                   "parallelism": f"byte-balanced block shards of one batch x{world}, "
+                                  "no data-path collective"},
         "roofline": {"bound": "hbm", "kernel": dom["name"],
                      "achieved": round(dom["achieved_gbs"], 1), "peak": HBM_PEAK_GBS,
-                     "unit": "GB/s", "frac": round(dom["frac"], 4), "traffic": traffic},
+                     "unit": "GB/s", "frac": round(dom["frac"], 4), "traffic": traffic,
+                     "alg_bytes_per_launch": dom["alg_bytes"],
+                     "avg_ms_hip_events": round(dom["avg_s"] * 1e3, 4),
+                     "avg_ms_kernel_trace": round(ns / 1e6, 4) if ns else None,
+                     "frac_kernel_trace": (round(dom["alg_bytes"] / (ns * 1e-9) / 1e9
+                                                 / HBM_PEAK_GBS, 4) if ns else None),
+                     "profile": prof},
         "cpu_baseline": cpu,
         "kernels": {k: {"name": v["name"], "avg_ms": round(v["avg_s"] * 1e3, 4),
                         "alg_bytes": v["alg_bytes"],

@@ -85,20 +85,31 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
 
 hipError_t scratch_free(void* p, hipStream_t stream) { return p ? hipFreeAsync(p, stream) : hipSuccess; }
 
+#ifdef FORST_DIAG
+const char* diag_env(const char* name) {
+  const char* v = std::getenv(name);
+  return v ? v : "";
+}
+#endif
+
 hipError_t feed_setup(BlockArgs& a, uint64_t nw, hipStream_t stream) {
   // half the descriptors as equal static shares (no claims while the
   // machine fills), the rest in claimed 64-descriptor chunks that absorb
   // the byte imbalance of mixed block sizes
-  const char* f = std::getenv("FORST_FEED");
-  const std::string mode = f ? f : "";
   a.ticket = nullptr;
+#ifdef FORST_DIAG
+  const std::string mode = diag_env("FORST_FEED");
   if (mode == "static") {  // one contiguous share per wave (A/B reference)
     a.share1 = (a.n + 64 * nw - 1) / (64 * nw) * 64;
     if (a.share1 * nw > a.n) a.share1 = a.n / (64 * nw) * 64;
     return hipSuccess;
   }
+  if (mode == "rr") {  // round-robin chunks, no counter (A/B reference)
+    a.share1 = a.n / (2 * 64 * nw) * 64;
+    return hipSuccess;
+  }
+#endif
   a.share1 = a.n / (2 * 64 * nw) * 64;
-  if (mode == "rr") return hipSuccess;
   void* p = nullptr;
   hipError_t e = scratch_alloc(&p, 64 * sizeof(unsigned long long), stream);
   if (e != hipSuccess) return e;
@@ -165,9 +176,13 @@ int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
   // cost 16 % of the pass (C2), split off 8 % (tools/gpu_trailer_ab.sh; a
   // read-merge-write of the covering dwords in the scatter kernel measured
   // the same).
-  // FORST_TRAILER=fused keeps them in the streaming kernel (A/B reference).
-  const char* tv = std::getenv("FORST_TRAILER");
-  if (mode == kModeTrailer && !(tv && std::string(tv) == "fused") && a.n) {
+  // (diagnostics build: FORST_TRAILER=fused keeps them in the streaming
+  // kernel, the A/B reference)
+  bool split = true;
+#ifdef FORST_DIAG
+  split = std::string(diag_env("FORST_TRAILER")) != "fused";
+#endif
+  if (mode == kModeTrailer && split && a.n) {
     BlockArgs c = a;
     void* tmp = nullptr;
     hipError_t e = hipSuccess;

@@ -207,8 +207,9 @@ __device__ __forceinline__ void fill_tables(uint32_t* L) {
   __syncthreads();
 }
 
+#ifdef FORST_DIAG
 // ---------------------------------------------------------------------------
-// Streaming block kernel.
+// Streaming block kernel v1 (diagnostics build only: A/B reference of v2).
 //
 // Each wave owns a contiguous share [kbeg, kend) of the descriptors and walks
 // it as a stream of (block, round) steps.  At the top of every step it issues
@@ -516,6 +517,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream_kernel(BlockArgs a) {
   while (step(X, Y) && step(Y, X)) {
   }
 }
+#endif  // FORST_DIAG
 
 // ---------------------------------------------------------------------------
 // Streaming block kernel v2: two independent CRC chains per lane.
@@ -640,7 +642,7 @@ struct Blk2 {
   uint64_t off;
   uint64_t we;  // window end: last dword boundary <= message end
   uint32_t size, mod, extra, R, S0;
-  uint32_t pk;  // cA:1 | lA:6 | jA:3 | q:3 | nt:2 | valid:1 | slow:1 | m:2
+  uint32_t pk;  // cA:1 | lA:6 | jA:3 | q:3 | nt:2 | valid:1 | slow:1 | m:2 | xtra:1
   __device__ __forceinline__ uint32_t cA() const { return pk & 1u; }
   __device__ __forceinline__ uint32_t lA() const { return (pk >> 1) & 63u; }
   __device__ __forceinline__ uint32_t jA() const { return (pk >> 7) & 7u; }
@@ -648,12 +650,27 @@ struct Blk2 {
   __device__ __forceinline__ uint32_t nt() const { return (pk >> 13) & 3u; }
   __device__ __forceinline__ bool valid() const { return (pk >> 15) & 1u; }
   __device__ __forceinline__ bool slow() const { return (pk >> 16) & 1u; }
-  __device__ __forceinline__ uint32_t bm() const { return 0xffffffffu << (8 * (pk >> 17)); }
+  __device__ __forceinline__ uint32_t bm() const { return 0xffffffffu << (8 * ((pk >> 17) & 3u)); }
+  __device__ __forceinline__ bool xtra() const { return (pk >> 19) & 1u; }
+  // end of the round windows: the message's last dword boundary, one dword
+  // earlier for an xtra block
+  __device__ __forceinline__ uint64_t wend() const { return we - (xtra() ? 4u : 0u); }
   // round-0 window start (may be < 0)
   __device__ __forceinline__ int64_t w0() const {
-    return static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRB2;
+    return static_cast<int64_t>(wend()) - static_cast<int64_t>(R) * kRB2;
   }
 };
+
+// Rounds of a window of d4 bytes (a dword multiple).  A window exactly one
+// dword longer than whole rounds -- a quarter of back-to-back 4 KiB blocks:
+// 4097 checksummed bytes starting at 3 mod 4 -- ends one dword early ("xtra");
+// that dword is one slicing step in the finish instead of an almost empty
+// round.  (Block modes only: raw messages of arbitrary lengths rarely hit it.)
+template <int MODE, uint32_t RB>
+__device__ __forceinline__ void window_rounds(uint64_t d4, uint32_t& R, bool& xtra) {
+  xtra = MODE != kModeRaw && (d4 & (RB - 1)) == 4 && d4 > RB;
+  R = static_cast<uint32_t>(xtra ? d4 / RB : (d4 + RB - 1) / RB);
+}
 
 template <int MODE>
 __device__ __forceinline__ bool mem_last_byte(const BlockArgs& a) {
@@ -677,7 +694,9 @@ __device__ __forceinline__ Blk2 blk2_setup_scalar(const BlockArgs& a, uint64_t k
   const uint64_t ws = b.off & ~3ull;
   b.we = E & ~3ull;
   const uint64_t d4 = b.we - ws;
-  b.R = static_cast<uint32_t>((d4 + kRB2 - 1) / kRB2);
+  bool xtra;
+  window_rounds<MODE, kRB2>(d4, b.R, xtra);
+  b.pk = xtra ? 1u << 19 : 0u;  // w0() below needs the flag
   const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - b.w0());
   const uint32_t cA = hA >> 11, lA = (hA >> 5) & 63u, jA = (hA >> 2) & 7u;
   // head segment starting in front of the buffer (only blocks at offset < 28):
@@ -694,7 +713,7 @@ __device__ __forceinline__ Blk2 blk2_setup_scalar(const BlockArgs& a, uint64_t k
     b.pk = (nt << 13) | (valid ? 1u << 15 : 0u) | (1u << 16) | (m << 17);
   } else {
     b.pk = cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
-           (m << 17);
+           (m << 17) | (xtra ? 1u << 19 : 0u);
   }
   return b;
 }
@@ -717,8 +736,10 @@ __device__ __forceinline__ Derived2 derive2(const BlockArgs& a, const DescBatch&
   const uint64_t ws = off & ~3ull;
   const uint64_t we = E & ~3ull;
   const uint64_t d4 = we - ws;
-  const uint32_t R = static_cast<uint32_t>((d4 + kRB2 - 1) / kRB2);
-  const int64_t w0 = static_cast<int64_t>(we) - static_cast<int64_t>(R) * kRB2;
+  uint32_t R;
+  bool xtra;
+  window_rounds<MODE, kRB2>(d4, R, xtra);
+  const int64_t w0 = static_cast<int64_t>(we) - (xtra ? 4 : 0) - static_cast<int64_t>(R) * kRB2;
   const uint32_t hA = static_cast<uint32_t>(static_cast<int64_t>(ws) - w0);
   const uint32_t cA = hA >> 11, lA = (hA >> 5) & 63u, jA = (hA >> 2) & 7u;
   const int64_t seg_head = static_cast<int64_t>(ws) - 4 * static_cast<int64_t>(jA);
@@ -729,7 +750,7 @@ __device__ __forceinline__ Derived2 derive2(const BlockArgs& a, const DescBatch&
   d.R = slow ? 1u : R;
   d.pk = slow ? ((nt << 13) | (valid ? 1u << 15 : 0u) | (1u << 16) | (m << 17))
               : (cA | (lA << 1) | (jA << 7) | (q << 10) | (nt << 13) | (valid ? 1u << 15 : 0u) |
-                 (m << 17));
+                 (m << 17) | (xtra ? 1u << 19 : 0u));
   d.S0 = MODE == kModeRaw ? (a.init_crcs ? unstep_m(~cb.extra, m) : kCrcS0[m]) : 0u;
   return d;
 }
@@ -747,14 +768,14 @@ __device__ __forceinline__ Blk2 blk2_setup(const BlockArgs& a, uint64_t k, uint6
   b.extra = readlane32(cb.extra, sl);
   b.pk = readlane32(cd.pk, sl);
   b.R = readlane32(cd.R, sl);
-  b.S0 = MODE == kModeRaw ? readlane32(cd.S0, sl) : kCrcS0[b.pk >> 17];
+  b.S0 = MODE == kModeRaw ? readlane32(cd.S0, sl) : kCrcS0[(b.pk >> 17) & 3u];
   b.we = b.slow() ? kRB2 : ((b.off + b.size + (mem_last_byte<MODE>(a) ? 1u : 0u)) & ~3ull);
   return b;
 }
 
 struct StepBuf2 {
   uint32_t w[2][8];
-  uint32_t t0, t1;
+  uint32_t t0, t1, t2;  // t2: the xtra dword
 };
 
 template <int MODE>
@@ -787,6 +808,7 @@ __device__ __forceinline__ void issue_step2(const uint8_t* __restrict__ base, ui
   const uint64_t t0 = b.slow() ? 0 : (nt > 0 || MODE == kModeVerify) ? b.we : b.we - 4;
   buf.t0 = ld4v(base + t0);
   buf.t1 = MODE == kModeVerify ? ld4v(base + (b.slow() || nt == 0 ? t0 : t0 + 4)) : 0u;
+  buf.t2 = MODE != kModeRaw ? ld4v(base + (b.xtra() ? b.we - 4 : t0)) : 0u;
 }
 
 __device__ __forceinline__ uint32_t xor3(uint32_t a, uint32_t b, uint32_t c) {
@@ -890,10 +912,11 @@ __device__ __forceinline__ uint32_t row_ror_xor(uint32_t v) {
 
 // join the 2 x 64 chain states, fold in the tail bytes and the extra byte;
 // returns ~state (the crc32c::Extend value), wave-uniform
+template <int MODE>
 __device__ __forceinline__ uint32_t stream_finish2(const uint8_t* __restrict__ Lb,
                                                    const Lanes2& K, uint32_t lane, const Blk2& b,
                                                    const uint32_t (&s)[2], uint32_t t0,
-                                                   bool has_extra) {
+                                                   uint32_t t2, bool has_extra) {
   // chain c of lane l ends 2048 (1 - c) + 32 (63 - l) bytes before the round end
   const bool lo0 = (lane & 15) == 15;
   const uint32_t abase = kOffA2 + 4096 * (14 - (lane & 15));  // A[lo], lo = 15 - (lane & 15)
@@ -915,8 +938,8 @@ __device__ __forceinline__ uint32_t stream_finish2(const uint8_t* __restrict__ L
     const uint32_t v1 = rho == 3 ? a1 : shift_at(Lb, kOffB2 + 4096 * (2 - rho), a1);
     v = v0 ^ v1;
   }
-  const uint32_t st = readlane32(v, 15) ^ readlane32(v, 31) ^ readlane32(v, 47) ^
-                      readlane32(v, 63);
+  uint32_t st = readlane32(v, 15) ^ readlane32(v, 31) ^ readlane32(v, 47) ^ readlane32(v, 63);
+  if (MODE != kModeRaw && b.xtra()) st = step_k(Lb, K, st, t2, 4);
   const uint32_t nt = b.nt();
   uint32_t y = nt ? (t0 & (0xffffffffu >> (32 - 8 * nt))) : 0u;
   uint32_t k = nt;
@@ -948,11 +971,12 @@ __device__ __forceinline__ uint32_t small_crc2(const uint8_t* __restrict__ Lb, c
   return ~s;
 }
 
-// PROBE = 1 (diagnostics only, FORST_CRC_VARIANT=probe_load): the same loads
-// and control flow, but every data word is only XOR-folded (no table lookups)
-// and every block reports ok -- the memory-side ceiling of this access pattern.
-template <int MODE, int PROBE = 0>
-__global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
+// PROBE = 1 (diagnostics build only, FORST_CRC_VARIANT=probe_load): the same
+// loads and control flow, but every data word is only XOR-folded (no table
+// lookups) and every block reports ok -- the memory-side ceiling of this
+// access pattern; 2 = no finish, 3 = no head handling.
+template <int MODE, int PROBE>
+__device__ __forceinline__ void crc32c_stream2_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds2Bytes / 4];
   fill_tables2(L);
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -1037,7 +1061,8 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
     if (last) {
       uint32_t crc = 0, stored = 0;
       if (PROBE == 2 || PROBE == 3) {  // rounds only / no head: finish cost still in 3
-        const uint32_t f = PROBE == 3 ? stream_finish2(Lb, K, lane, C, s, cu.t0, has_extra)
+        const uint32_t f = PROBE == 3
+                               ? stream_finish2<MODE>(Lb, K, lane, C, s, cu.t0, cu.t2, has_extra)
                                       : s[0] ^ s[1];
         stored = crc_mask(0) + C.mod;
         crc = __ballot(f == 0x9e3779b9u) ? 1u : 0u;
@@ -1048,7 +1073,7 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
         crc = __ballot(f == 0x9e3779b9u) ? 1u : 0u;
         s[0] = s[1] = 0;
       } else if (!C.slow()) {
-        crc = stream_finish2(Lb, K, lane, C, s, cu.t0, has_extra);
+        crc = stream_finish2<MODE>(Lb, K, lane, C, s, cu.t0, cu.t2, has_extra);
         if (MODE == kModeVerify)
           stored = C.nt() ? __builtin_amdgcn_alignbyte(cu.t1, cu.t0, C.nt()) : cu.t0;
       } else if (C.valid()) {
@@ -1100,6 +1125,18 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
   while (step(X, Z) && step(Y, X) && step(Z, Y)) {
   }
 }
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) crc32c_stream2_kernel(BlockArgs a) {
+  crc32c_stream2_body<MODE, 0>(a);
+}
+
+#ifdef FORST_DIAG
+template <int PROBE>
+__global__ void __launch_bounds__(kThreads) crc32c_stream2_probe_kernel(BlockArgs a) {
+  crc32c_stream2_body<kModeVerify, PROBE>(a);
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // CRC32C rows kernel (v3): one block per 16-lane row.
@@ -1248,14 +1285,13 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
                              : (a.last_bytes ? a.last_bytes[idx] : 0u);
 }
 
-// PROBE (diagnostics, never default): 1 = same loads and row bookkeeping,
-// no table work and no finish; 2 = no per-block finish.
-// DEPTH 2: two steps of loads in flight per wave (three step buffers,
-// 12-wave workgroups at 3 waves/SIMD) instead of one.
+// PROBE (diagnostics build only): 1 = same loads and row bookkeeping, no
+// table work and no finish; 2 = no per-block finish.
+// DEPTH 2 (diagnostics build only): two steps of loads in flight per wave
+// (three step buffers, 12-wave workgroups at 3 waves/SIMD) instead of one.
 constexpr uint32_t kRowsD2Waves = 12;
-template <int MODE, int PROBE = 0, int DEPTH = 1>
-__global__ void __launch_bounds__(DEPTH == 2 ? 64 * kRowsD2Waves : kThreads)
-    crc32c_rows_kernel(BlockArgs a) {
+template <int MODE, int PROBE, int DEPTH>
+__device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
   fill_tables3(L);
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
@@ -1488,6 +1524,24 @@ __global__ void __launch_bounds__(DEPTH == 2 ? 64 * kRowsD2Waves : kThreads)
 }
 
 template <int MODE>
+__global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
+  crc32c_rows_body<MODE, 0, 1>(a);
+}
+
+#ifdef FORST_DIAG
+template <int PROBE>
+__global__ void __launch_bounds__(kThreads) crc32c_rows_probe_kernel(BlockArgs a) {
+  crc32c_rows_body<kModeVerify, PROBE, 1>(a);
+}
+template <int MODE>
+__global__ void __launch_bounds__(64 * kRowsD2Waves) crc32c_rows_d2_kernel(BlockArgs a) {
+  crc32c_rows_body<MODE, 0, 2>(a);
+}
+#endif
+
+// One wave per block, no streaming: serves buffers shorter than one 4 KiB
+// round (the streaming kernels' dummy loads need that much).
+template <int MODE>
 __global__ void __launch_bounds__(kThreads)
     crc32c_block_kernel_simple(BlockArgs a) {
   __shared__ uint32_t L[kLdsDwords];
@@ -1554,12 +1608,117 @@ __global__ void __launch_bounds__(kThreads)
 
 }  // namespace
 
-hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
-                                hipStream_t stream, const char** name) {
+namespace {
+
+enum class CrcKernel {
+  kSimple,  // one wave per block: buffers shorter than one 4 KiB round
+  kRows,    // one block per 16-lane row (crc32c_rows_kernel)
+  kV2,      // one block per wave, two chains per lane (crc32c_stream2_kernel)
+#ifdef FORST_DIAG
+  kV1, kRowsD2, kRowsProbeLoad, kRowsProbeNoFin, kV2ProbeLoad, kV2ProbeRounds, kV2ProbeNoHead,
+#endif
+};
+
+hipError_t launch_kernel(void (*k)(BlockArgs), uint32_t grid, uint32_t threads, BlockArgs a,
+                         hipStream_t s) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 0, s, a);
+  return hipGetLastError();
+}
+
+// a rows-kernel launch with its work-feed counter (stream_common.h)
+hipError_t launch_fed(void (*k)(BlockArgs), uint32_t grid, uint32_t waves, BlockArgs b,
+                      hipStream_t s) {
+  hipError_t e = feed_setup(b, uint64_t(grid) * waves, s);
+  if (e != hipSuccess) return e;
+  e = launch_kernel(k, grid, 64 * waves, b, s);
+  const hipError_t f = scratch_free(b.ticket, s);
+  return e != hipSuccess ? e : f;
+}
+
+const char* crc_kernel_name(CrcKernel k, int mode) {
+  static const char* const kNames[][4] = {
+      {"crc32c_block_kernel_simple<compute>", "crc32c_block_kernel_simple<trailer>",
+       "crc32c_block_kernel_simple<verify>", "crc32c_block_kernel_simple<raw>"},
+      {"crc32c_rows_kernel<compute>", "crc32c_rows_kernel<trailer>", "crc32c_rows_kernel<verify>",
+       "crc32c_rows_kernel<raw>"},
+      {"crc32c_stream2_kernel<compute>", "crc32c_stream2_kernel<trailer>",
+       "crc32c_stream2_kernel<verify>", "crc32c_stream2_kernel<raw>"},
+#ifdef FORST_DIAG
+      {"crc32c_stream_kernel<compute>", "crc32c_stream_kernel<trailer>",
+       "crc32c_stream_kernel<verify>", "crc32c_stream_kernel<raw>"},
+      {"crc32c_rows_d2_kernel<compute>", "crc32c_rows_d2_kernel<trailer>",
+       "crc32c_rows_d2_kernel<verify>", "crc32c_rows_d2_kernel<raw>"},
+#endif
+  };
+#ifdef FORST_DIAG
+  switch (k) {
+    case CrcKernel::kRowsProbeLoad: return "crc32c_rows_probe_kernel<1>";
+    case CrcKernel::kRowsProbeNoFin: return "crc32c_rows_probe_kernel<2>";
+    case CrcKernel::kV2ProbeLoad: return "crc32c_stream2_probe_kernel<1>";
+    case CrcKernel::kV2ProbeRounds: return "crc32c_stream2_probe_kernel<2>";
+    case CrcKernel::kV2ProbeNoHead: return "crc32c_stream2_probe_kernel<3>";
+    default: break;
+  }
+#endif
+  return kNames[static_cast<int>(k)][mode & 3];
+}
+
+template <int M>
+hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipStream_t s) {
+  switch (k) {
+    case CrcKernel::kSimple:
+      return launch_kernel(crc32c_block_kernel_simple<M>, grid, kThreads, a, s);
+    case CrcKernel::kRows:
+      return launch_fed(crc32c_rows_kernel<M>, grid, kWaves, a, s);
+    case CrcKernel::kV2:
+      return launch_kernel(crc32c_stream2_kernel<M>, grid, kThreads, a, s);
+#ifdef FORST_DIAG
+    case CrcKernel::kV1:
+      return launch_kernel(crc32c_stream_kernel<M>, grid, kThreads, a, s);
+    case CrcKernel::kRowsD2:
+      return launch_fed(crc32c_rows_d2_kernel<M>, grid, kRowsD2Waves, a, s);
+    case CrcKernel::kRowsProbeLoad:
+      return launch_fed(crc32c_rows_probe_kernel<1>, grid, kWaves, a, s);
+    case CrcKernel::kRowsProbeNoFin:
+      return launch_fed(crc32c_rows_probe_kernel<2>, grid, kWaves, a, s);
+    case CrcKernel::kV2ProbeLoad:
+      return launch_kernel(crc32c_stream2_probe_kernel<1>, grid, kThreads, a, s);
+    case CrcKernel::kV2ProbeRounds:
+      return launch_kernel(crc32c_stream2_probe_kernel<2>, grid, kThreads, a, s);
+    case CrcKernel::kV2ProbeNoHead:
+      return launch_kernel(crc32c_stream2_probe_kernel<3>, grid, kThreads, a, s);
+#endif
+  }
+  return hipErrorInvalidValue;
+}
+
+#ifdef FORST_DIAG
+// diagnostics build: FORST_CRC_VARIANT overrides the kernel choice (probe
+// variants only replace verify launches; their results are not checksums)
+CrcKernel diag_crc_kernel(CrcKernel k, int mode) {
+  const std::string v = diag_env("FORST_CRC_VARIANT");
+  const bool vf = mode == kModeVerify;
+  if (v == "simple") return CrcKernel::kSimple;
+  if (v == "rows") return CrcKernel::kRows;
+  if (v == "v2") return CrcKernel::kV2;
+  if (v == "v1") return CrcKernel::kV1;
+  if (v == "rows_d2") return CrcKernel::kRowsD2;
+  if (v == "rows_probe_load" && vf) return CrcKernel::kRowsProbeLoad;
+  if (v == "rows_probe_nofin" && vf) return CrcKernel::kRowsProbeNoFin;
+  if (v == "probe_load" && vf) return CrcKernel::kV2ProbeLoad;
+  if (v == "probe_rounds" && vf) return CrcKernel::kV2ProbeRounds;
+  if (v == "probe_nohead" && vf) return CrcKernel::kV2ProbeNoHead;
+  return k;
+}
+#endif
+
+}  // namespace
+
+hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream,
+                                const char** name) {
   const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
-  uint32_t grid = static_cast<uint32_t>(
-      std::min<uint64_t>((a.n + kWaves - 1) / kWaves, di.num_cus));
+  uint32_t grid = static_cast<uint32_t>(std::min<uint64_t>((a.n + kWaves - 1) / kWaves, di.num_cus));
   if (grid == 0) grid = 1;
 #ifdef FORST_DEBUG_BOUNDS
   {
@@ -1571,113 +1730,46 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
     if (e != hipSuccess) return e;
   }
 #endif
-  // FORST_CRC_VARIANT=simple selects the per-block kernel (A/B reference); it
-  // also serves buffers too small for the stream kernel's dummy loads.
-  // FORST_CRC_VARIANT=v1 selects the one-chain stream kernel (A/B reference).
-  const char* variant = std::getenv("FORST_CRC_VARIANT");
-  const bool simple = (variant && std::string(variant) == "simple") || a.base_len < kRB;
-  const bool v1 = variant && std::string(variant) == "v1";
-  // default: the rows kernel (one block per 16-lane row) up to 20 KiB mean
-  // block size, the v2 kernel (two 4 KiB steps in flight per wave) above.
+  // The rows kernel (one block per 16-lane row) up to 20 KiB mean block
+  // size, the v2 kernel (two 4 KiB steps in flight per wave) above
   // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2 %; v2 wins on
   // the 4/16/64 KiB mix by 4 % and at 64 KiB by 45 %, where the rows of a
-  // wave stream addresses 64 KiB apart)
-  // ... and only with at least four 64-block chunks per wave: the rows
-  // kernel's work feed deals 64-block chunks, so with fewer the last chunk is
-  // a large part of a wave's work (C4, 512 K x 16 KiB: rows 0.645, v2 0.714)
+  // wave stream addresses 64 KiB apart) ... and only with at least four
+  // 64-block chunks per wave: the rows kernel's work feed deals 64-block
+  // chunks, so with fewer the last chunk is a large part of a wave's work
+  // (C4, 512 K x 16 KiB: rows 0.645, v2 0.714).  The rows kernel indexes
+  // descriptors with 32 bits.  Buffers shorter than one 4 KiB round take the
+  // simple kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
   const uint64_t mean = a.base_len / a.n;
   const bool small_blocks =
       mean <= 20480 && (mean <= 8192 || a.n >= uint64_t(4) * kBatch * kWaves * grid);
-  // (the rows kernel indexes descriptors with 32 bits)
-  const bool rows = a.n < 0xffffffffull && ((variant && std::string(variant) == "rows") ||
-                                            ((!variant || !*variant) &&
-                                             (a.kernel_hint ? a.kernel_hint == 1 : small_blocks)));
-  const int rows_probe = !variant ? 0
-                         : std::string(variant) == "rows_probe_load"   ? 1
-                         : std::string(variant) == "rows_probe_nofin" ? 2
-                                                                       : 0;
-  const bool rows_d2 = variant && std::string(variant) == "rows_d2";
-  // diagnostics: probe_load (loads only), probe_rounds (no finish),
-  // probe_nohead (no round-0 head handling); results are not checksums
-  const int probe = !variant ? 0
-                    : std::string(variant) == "probe_load"   ? 1
-                    : std::string(variant) == "probe_rounds" ? 2
-                    : std::string(variant) == "probe_nohead" ? 3
-                                                             : 0;
-#define FORST_LAUNCH_CRC(M, TAG)                                                          \
-  do {                                                                                    \
-    if (simple) {                                                                         \
-      *name = "crc32c_block_kernel_simple<" TAG ">";                                      \
-      hipLaunchKernelGGL(crc32c_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,    \
-                         stream, a);                                                      \
-    } else if (rows || rows_d2 || (rows_probe && M == kModeVerify)) {                     \
-      *name = "crc32c_rows_kernel<" TAG ">";                                              \
-      BlockArgs b = a;                                                                    \
-      hipError_t fe = feed_setup(b, uint64_t(grid) * kWaves, stream);                     \
-      if (fe != hipSuccess) return fe;                                                    \
-      if (rows_d2) {                                                                      \
-        BlockArgs b2 = b;                                                                 \
-        (void)scratch_free(b.ticket, stream);                                             \
-        fe = feed_setup(b2, uint64_t(grid) * kRowsD2Waves, stream);                       \
-        if (fe != hipSuccess) return fe;                                                  \
-        hipLaunchKernelGGL((crc32c_rows_kernel<M, 0, 2>), dim3(grid),                     \
-                           dim3(64 * kRowsD2Waves), 0, stream, b2);                       \
-        fe = hipGetLastError();                                                           \
-        const hipError_t ff2 = scratch_free(b2.ticket, stream);                           \
-        return fe != hipSuccess ? fe : ff2;                                               \
-      }                                                                                   \
-      if (rows_probe == 1)                                                                \
-        hipLaunchKernelGGL((crc32c_rows_kernel<kModeVerify, 1>), dim3(grid), dim3(kThreads), \
-                           0, stream, b);                                                 \
-      else if (rows_probe == 2)                                                           \
-        hipLaunchKernelGGL((crc32c_rows_kernel<kModeVerify, 2>), dim3(grid), dim3(kThreads), \
-                           0, stream, b);                                                 \
-      else                                                                                \
-        hipLaunchKernelGGL(crc32c_rows_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, b); \
-      fe = hipGetLastError();                                                             \
-      const hipError_t ff = scratch_free(b.ticket, stream);                               \
-      return fe != hipSuccess ? fe : ff;                                                  \
-    } else if (v1) {                                                                      \
-      *name = "crc32c_stream_kernel<" TAG ">";                                            \
-      hipLaunchKernelGGL(crc32c_stream_kernel<M>, dim3(grid), dim3(kThreads), 0, stream,  \
-                         a);                                                              \
-    } else if (probe && M == kModeVerify) {                                               \
-      *name = "crc32c_stream2_kernel<probe>";                                             \
-      if (probe == 1)                                                                     \
-        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 1>), dim3(grid),           \
-                           dim3(kThreads), 0, stream, a);                                 \
-      else if (probe == 2)                                                                \
-        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 2>), dim3(grid),           \
-                           dim3(kThreads), 0, stream, a);                                 \
-      else                                                                                \
-        hipLaunchKernelGGL((crc32c_stream2_kernel<kModeVerify, 3>), dim3(grid),           \
-                           dim3(kThreads), 0, stream, a);                                 \
-    } else {                                                                              \
-      *name = "crc32c_stream2_kernel<" TAG ">";                                           \
-      hipLaunchKernelGGL(crc32c_stream2_kernel<M>, dim3(grid), dim3(kThreads), 0, stream, \
-                         a);                                                              \
-    }                                                                                     \
-  } while (0)
+  CrcKernel k = a.base_len < kRB ? CrcKernel::kSimple
+                : (a.n < 0xffffffffull && (a.kernel_hint ? a.kernel_hint == 1 : small_blocks))
+                    ? CrcKernel::kRows
+                    : CrcKernel::kV2;
+#ifdef FORST_DIAG
+  if (a.base_len >= kRB) k = diag_crc_kernel(k, mode);
+  if (k == CrcKernel::kRows || k == CrcKernel::kRowsD2) {
+    if (a.n >= 0xffffffffull) k = CrcKernel::kV2;
+  }
+#endif
+  *name = crc_kernel_name(k, mode);
   switch (mode) {
     case kModeCompute:
-      FORST_LAUNCH_CRC(kModeCompute, "compute");
-      break;
+      return launch_crc_mode<kModeCompute>(k, a, grid, stream);
     case kModeTrailer:
-      FORST_LAUNCH_CRC(kModeTrailer, "trailer");
-      break;
+      return launch_crc_mode<kModeTrailer>(k, a, grid, stream);
     case kModeVerify:
-      FORST_LAUNCH_CRC(kModeVerify, "verify");
-      break;
+      return launch_crc_mode<kModeVerify>(k, a, grid, stream);
     default:
-      FORST_LAUNCH_CRC(kModeRaw, "raw");
-      break;
+      return launch_crc_mode<kModeRaw>(k, a, grid, stream);
   }
-#undef FORST_LAUNCH_CRC
-  return hipGetLastError();
 }
 
+#ifdef FORST_DIAG
 // ---------------------------------------------------------------------------
-// WAL (db/log_reader.cc:450-531, db/log_writer.cc:228-263)
+// WAL, one wave per log block / record (diagnostics build only: A/B reference
+// of the wal.hip pipeline; db/log_reader.cc:450-531, db/log_writer.cc:228-263)
 // ---------------------------------------------------------------------------
 namespace {
 
@@ -1802,6 +1894,8 @@ hipError_t launch_wal_record_crc_wave(const WalArgs& a, hipStream_t stream,
                      stream, a);
   return hipGetLastError();
 }
+
+#endif  // FORST_DIAG
 
 }  // namespace forst
 

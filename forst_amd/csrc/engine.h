@@ -90,12 +90,21 @@ struct DeviceInfo {
 };
 const DeviceInfo& device_info();  // current device (lazily initialised)
 
+#ifdef FORST_DIAG
+// Diagnostics build only (make diag -> lib/libforst_checksum_diag.so): kernel
+// variants for A/B runs (tools/ab_bench.py) are selected by environment
+// variables read here.  The product library compiles none of the variants and
+// reads no environment variable.  Returns "" when unset.
+const char* diag_env(const char* name);
+#endif
+
 // stream-ordered scratch from a per-device pool that keeps freed memory
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream);
 hipError_t scratch_free(void* p, hipStream_t stream);
 // work feed of a rows-kernel launch over nw waves (stream_common.h): sets
-// share1 and, unless FORST_FEED=static|rr, a zeroed ticket counter that the
-// caller releases with scratch_free(a.ticket) after the launch
+// share1 and a zeroed ticket counter that the caller releases with
+// scratch_free(a.ticket) after the launch (diagnostics build:
+// FORST_FEED=static|rr for the A/B references without a counter)
 hipError_t feed_setup(BlockArgs& a, uint64_t nw, hipStream_t stream);
 
 // Launchers (return hipError_t). `kernel_name` receives a static string.

@@ -38,8 +38,10 @@
 
 namespace forst {
 
+#ifdef FORST_DIAG
 hipError_t launch_wal_verify_wave(const WalArgs& a, hipStream_t stream, const char** name);
 hipError_t launch_wal_record_crc_wave(const WalArgs& a, hipStream_t stream, const char** name);
+#endif
 
 namespace {
 
@@ -478,6 +480,7 @@ __global__ void __launch_bounds__(kTile) rec_select_kernel(uint64_t n_logical, c
   if (out_first) out_first[j] = first_phys[j];
 }
 
+#ifdef FORST_DIAG
 // ---- raw CRC of a record list split by size (A/B variant) -------------------
 // WAL records span 7 B .. 32 KiB: with FORST_WAL_SPLIT=1 small ones go to the
 // rows kernel (one record per 16-lane row), large ones to the v2 kernel (one
@@ -514,12 +517,15 @@ __global__ void __launch_bounds__(kTile) split_scatter_kernel(uint64_t n, const 
   if (i < n) out[i] = flag[i] ? s_out[pos[i]] : b_out[i - pos[i]];
 }
 
+#endif  // FORST_DIAG
+
 size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
-bool wave_variant() {
-  const char* v = std::getenv("FORST_WAL_VARIANT");
-  return v && std::string(v) == "wave";
-}
+#ifdef FORST_DIAG
+// diagnostics build: FORST_WAL_VARIANT=wave selects the one-wave-per-log-block
+// kernels (crc32c.hip), the A/B reference of this pipeline
+bool wave_variant() { return std::string(diag_env("FORST_WAL_VARIANT")) == "wave"; }
+#endif
 
 }  // namespace
 
@@ -539,8 +545,11 @@ hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* o
   b.n = n;
   // default: one launch (the rows kernel for this size mix); the split is an
   // A/B variant (C5: 0.499 one launch vs 0.478 split, tools/wal_ab.py)
-  const char* sv = std::getenv("FORST_WAL_SPLIT");
-  if (!(sv && std::string(sv) == "1")) return launch_crc32c_blocks(kModeRaw, b, stream, name);
+#ifndef FORST_DIAG
+  return launch_crc32c_blocks(kModeRaw, b, stream, name);
+#else
+  if (std::string(diag_env("FORST_WAL_SPLIT")) != "1")
+    return launch_crc32c_blocks(kModeRaw, b, stream, name);
   const uint64_t nt = (n + kTile - 1) / kTile;
   const dim3 grid(static_cast<uint32_t>(nt));
   const size_t s8 = up256(8 * n), s4 = up256(4 * n), st = up256(8 * (nt + 1));
@@ -594,13 +603,16 @@ hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* o
   }
   const hipError_t f = scratch_free(scratch, stream);
   return e != hipSuccess ? e : f;
+#endif  // FORST_DIAG
 }
 
 }  // namespace
 
 hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream, const char** name) {
   if (a.n_blocks == 0) return hipSuccess;
+#ifdef FORST_DIAG
   if (wave_variant()) return launch_wal_verify_wave(a, stream, name);
+#endif
   const uint64_t n_tiles = (a.n_blocks + kTile - 1) / kTile;
   const size_t nb = a.n_blocks;
   const size_t sz_cnt = up256(4 * nb), sz_stop = up256(4 * nb), sz_base = up256(8 * nb),
@@ -646,7 +658,9 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream, const char** 
 
 hipError_t launch_wal_record_crc(const WalArgs& a, hipStream_t stream, const char** name) {
   if (a.n_records == 0) return hipSuccess;
+#ifdef FORST_DIAG
   if (wave_variant()) return launch_wal_record_crc_wave(a, stream, name);
+#endif
   const size_t n = a.n_records;
   const size_t sz_off = up256(8 * n), sz_len = up256(4 * n);
   void* scratch = nullptr;

@@ -365,10 +365,10 @@ __device__ __forceinline__ void xx_step_round(const XBlk& b, uint32_t r, uint32_
   }
 }
 
-// PROBE = 1 (diagnostics only, FORST_XXH3_VARIANT=probe_load): same loads and
-// control flow, data only XOR-folded, every block reported ok.
-template <int MODE, int PROBE = 0>
-__global__ void __launch_bounds__(kThreads) xxh3_stream_kernel(BlockArgs a) {
+// PROBE = 1 (diagnostics build only, FORST_XXH3_VARIANT=probe_load): same
+// loads and control flow, data only XOR-folded, every block reported ok.
+template <int MODE, int PROBE>
+__device__ __forceinline__ void xxh3_stream_body(const BlockArgs& a) {
   __shared__ uint64_t cold[4 * kColdN];
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   __syncthreads();
@@ -511,6 +511,17 @@ __global__ void __launch_bounds__(kThreads) xxh3_stream_kernel(BlockArgs a) {
   while (step(X, Y) && step(Y, X)) {
   }
 }
+
+template <int MODE>
+__global__ void __launch_bounds__(kThreads) xxh3_stream_kernel(BlockArgs a) {
+  xxh3_stream_body<MODE, 0>(a);
+}
+
+#ifdef FORST_DIAG
+__global__ void __launch_bounds__(kThreads) xxh3_stream_probe_kernel(BlockArgs a) {
+  xxh3_stream_body<kModeVerify, 1>(a);
+}
+#endif
 
 // ---------------------------------------------------------------------------
 // XXH3 v2 ("rows"): four messages per wave, one per 16-lane row.
@@ -906,72 +917,104 @@ uint32_t rows_occupancy() {
 
 }  // namespace
 
+namespace {
+
+enum class XxKernel {
+  kSimple,  // one wave per block: buffers shorter than 4 KiB
+  kRows,    // one message per 16-lane row (xxh3_rows_kernel)
+  kV1,      // one message per wave (xxh3_stream_kernel)
+#ifdef FORST_DIAG
+  kProbeLoad,
+#endif
+};
+
+hipError_t launch_kernel(void (*k)(BlockArgs), uint32_t grid, BlockArgs a, hipStream_t s) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), 0, s, a);
+  return hipGetLastError();
+}
+
+template <int M>
+hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const char** name) {
+  static const char* const kNames[][4] = {
+      {"xxh3_block_kernel_simple<compute>", "xxh3_block_kernel_simple<trailer>",
+       "xxh3_block_kernel_simple<verify>", "xxh3_block_kernel_simple<raw>"},
+      {"xxh3_rows_kernel<compute>", "xxh3_rows_kernel<trailer>", "xxh3_rows_kernel<verify>",
+       "xxh3_rows_kernel<raw>"},
+      {"xxh3_stream_kernel<compute>", "xxh3_stream_kernel<trailer>", "xxh3_stream_kernel<verify>",
+       "xxh3_stream_kernel<raw>"},
+  };
+  const DeviceInfo& di = device_info();
+  const uint64_t want = (a.n + kWaves - 1) / kWaves;
+  switch (k) {
+    case XxKernel::kSimple: {
+      *name = kNames[0][M];
+      const uint32_t grid = static_cast<uint32_t>(
+          std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
+      return launch_kernel(xxh3_block_kernel_simple<M>, grid, a, s);
+    }
+    case XxKernel::kRows: {
+      *name = kNames[1][M];
+      const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
+          1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),
+                                uint64_t(di.num_cus) * rows_occupancy<M>())));
+      BlockArgs b = a;
+      hipError_t e = feed_setup(b, uint64_t(grid) * kWaves, s);
+      if (e != hipSuccess) return e;
+      e = launch_kernel(xxh3_rows_kernel<M>, grid, b, s);
+      const hipError_t f = scratch_free(b.ticket, s);
+      return e != hipSuccess ? e : f;
+    }
+    case XxKernel::kV1: {
+      *name = kNames[2][M];
+      const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
+          1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));
+      return launch_kernel(xxh3_stream_kernel<M>, grid, a, s);
+    }
+#ifdef FORST_DIAG
+    case XxKernel::kProbeLoad: {
+      *name = "xxh3_stream_probe_kernel";
+      const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
+          1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));
+      return launch_kernel(xxh3_stream_probe_kernel, grid, a, s);
+    }
+#endif
+  }
+  return hipErrorInvalidValue;
+}
+
+}  // namespace
+
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
                               const char** name) {
-  const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
-  const uint64_t want = (a.n + kWaves - 1) / kWaves;
-  const uint32_t grid = static_cast<uint32_t>(
-      std::max<uint64_t>(1, std::min<uint64_t>(want, uint64_t(di.num_cus) * 8)));
-  // FORST_XXH3_VARIANT=simple selects the per-block kernel (A/B reference);
-  // it also serves buffers too small for the stream kernel's dummy loads.
-  const char* variant = std::getenv("FORST_XXH3_VARIANT");
-  const bool simple = (variant && std::string(variant) == "simple") || a.base_len < 4096;
-  const bool probe = variant && std::string(variant) == "probe_load" && mode == kModeVerify;
   // the rows kernel indexes descriptors with 32 bits; uniform >= 48 KiB blocks
   // go to v1 (rows of a wave streaming addresses 64 KiB apart camp on the
   // same HBM channels: X64 rows 0.49 vs v1 0.62 of the peak; C3's 4/16/64 KiB
-  // mix stays on rows, 0.67 vs 0.53)
+  // mix stays on rows, 0.67 vs 0.53).  Buffers shorter than 4 KiB take the
+  // simple kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
   const bool big = a.base_len / a.n >= 49152;
-  const bool v1 = (variant && std::string(variant) == "v1") || a.n >= 0xffffffffull ||
-                  ((!variant || !*variant) && big);
-#define FORST_LAUNCH_XXH3(M, TAG)                                                          \
-  do {                                                                                     \
-    if (simple) {                                                                          \
-      *name = "xxh3_block_kernel_simple<" TAG ">";                                         \
-      hipLaunchKernelGGL(xxh3_block_kernel_simple<M>, dim3(grid), dim3(kThreads), 0,       \
-                         stream, a);                                                       \
-    } else if (probe) {                                                                    \
-      *name = "xxh3_stream_kernel<probe_load>";                                            \
-      const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
-          1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));     \
-      hipLaunchKernelGGL((xxh3_stream_kernel<kModeVerify, 1>), dim3(sg), dim3(kThreads), 0, \
-                         stream, a);                                                       \
-    } else if (v1) {                                                                       \
-      *name = "xxh3_stream_kernel<" TAG ">";                                               \
-      const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
-          1, std::min<uint64_t>(want, uint64_t(di.num_cus) * stream_occupancy<M>())));     \
-      hipLaunchKernelGGL(xxh3_stream_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, a);   \
-    } else {                                                                               \
-      *name = "xxh3_rows_kernel<" TAG ">";                                                 \
-      const uint32_t sg = static_cast<uint32_t>(std::max<uint64_t>(                        \
-          1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),                     \
-                                uint64_t(di.num_cus) * rows_occupancy<M>())));             \
-      BlockArgs b = a;                                                                     \
-      hipError_t fe = feed_setup(b, uint64_t(sg) * kWaves, stream);                        \
-      if (fe != hipSuccess) return fe;                                                     \
-      hipLaunchKernelGGL(xxh3_rows_kernel<M>, dim3(sg), dim3(kThreads), 0, stream, b);     \
-      fe = hipGetLastError();                                                              \
-      const hipError_t ff = scratch_free(b.ticket, stream);                                \
-      return fe != hipSuccess ? fe : ff;                                                   \
-    }                                                                                      \
-  } while (0)
+  XxKernel k = a.base_len < 4096                     ? XxKernel::kSimple
+               : (a.n >= 0xffffffffull || big) ? XxKernel::kV1
+                                                     : XxKernel::kRows;
+#ifdef FORST_DIAG
+  if (a.base_len >= 4096) {
+    const std::string v = diag_env("FORST_XXH3_VARIANT");
+    if (v == "simple") k = XxKernel::kSimple;
+    if (v == "v1") k = XxKernel::kV1;
+    if (v == "rows" && a.n < 0xffffffffull) k = XxKernel::kRows;
+    if (v == "probe_load" && mode == kModeVerify) k = XxKernel::kProbeLoad;
+  }
+#endif
   switch (mode) {
     case kModeCompute:
-      FORST_LAUNCH_XXH3(kModeCompute, "compute");
-      break;
+      return launch_xxh3_mode<kModeCompute>(k, a, stream, name);
     case kModeTrailer:
-      FORST_LAUNCH_XXH3(kModeTrailer, "trailer");
-      break;
+      return launch_xxh3_mode<kModeTrailer>(k, a, stream, name);
     case kModeVerify:
-      FORST_LAUNCH_XXH3(kModeVerify, "verify");
-      break;
+      return launch_xxh3_mode<kModeVerify>(k, a, stream, name);
     default:
-      FORST_LAUNCH_XXH3(kModeRaw, "raw");
-      break;
+      return launch_xxh3_mode<kModeRaw>(k, a, stream, name);
   }
-#undef FORST_LAUNCH_XXH3
-  return hipGetLastError();
 }
 
 hipError_t launch_noop_blocks(int mode, const BlockArgs& a, hipStream_t stream,

@@ -12,16 +12,18 @@ import torch
 import torch.distributed as dist
 
 
-def setup():
+def setup(cpu_only=False):
     """(world, rank, local_rank) from the torch.distributed.run environment;
-    initialises the process group when world > 1."""
+    initialises the process group when world > 1 (RCCL with a GPU, gloo on
+    the CPU or when cpu_only: then no GPU call is made at all)."""
     world = int(os.environ.get("WORLD_SIZE", "1"))
     rank = int(os.environ.get("RANK", "0"))
     local = int(os.environ.get("LOCAL_RANK", "0"))
-    if torch.cuda.is_available():
+    gpu = not cpu_only and torch.cuda.is_available()
+    if gpu:
         torch.cuda.set_device(local)
     if world > 1 and not dist.is_initialized():
-        dist.init_process_group(backend="nccl" if torch.cuda.is_available() else "gloo")
+        dist.init_process_group(backend="nccl" if gpu else "gloo")
     return world, rank, local
 
 
@@ -68,6 +70,15 @@ def byte_ranges(sizes, world):
     cuts.append(n)
     cuts = np.maximum.accumulate(np.minimum(np.asarray(cuts), n))
     return [(int(cuts[r]), int(cuts[r + 1])) for r in range(world)]
+
+
+def rank_slice(sizes, rank, world, trailer=5):
+    """This rank's part of one described SST batch (blocks packed back to back,
+    payload n_i + `trailer` bytes each): (lo, hi, first byte offset)."""
+    sizes = np.asarray(sizes, dtype=np.int64)
+    lo, hi = byte_ranges(sizes, world)[rank]
+    start = int(sizes[:lo].sum()) + trailer * lo
+    return lo, hi, start
 
 
 def local_shard(offsets, sizes, rank, world):

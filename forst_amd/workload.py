@@ -74,17 +74,21 @@ class SstBatch:
 
 
 def make_sst_batch(n, spec, seed, ctype=engine.ChecksumType.kCRC32c, device="cuda",
-                   write_trailers=True, modifiers=None, sizes=None):
+                   write_trailers=True, modifiers=None, sizes=None, stream_start=0):
+    """n SST-packed blocks on the device.  stream_start = byte offset of the
+    first block in a larger described batch (a rank's shard, shard.rank_slice):
+    the payload bytes are then exactly that batch's bytes."""
     if sizes is None:
         sizes = block_sizes(n, spec, seed)
     sizes = np.asarray(sizes, dtype=np.uint32)
+    n = len(sizes)
     offs = np.zeros(n, dtype=np.int64)
     if n > 1:
         offs[1:] = np.cumsum(sizes[:-1].astype(np.int64) + TRAILER)
     total = int(offs[-1]) + int(sizes[-1]) + TRAILER if n else 0
     alloc = max(16, (total + 255) // 256 * 256)
     base = torch.empty(alloc, dtype=torch.uint8, device=device)
-    engine.fill_stream(base, 0, seed)
+    engine.fill_stream(base, stream_start, seed)
     base = base[:total] if total else base[:0]
     d_offs = torch.from_numpy(offs).to(device)
     d_sizes = torch.from_numpy(sizes.astype(np.int32)).to(device)

@@ -69,3 +69,23 @@ def test_two_rank_gloo_shards(tmp_path):
     world = 2
     mp.spawn(_worker, args=(world, _free_port(), str(tmp_path)), nprocs=world, join=True)
     assert np.load(tmp_path / "result.npy").tolist() == [1, 1, 1]
+
+
+def test_bench_gpus2_dry_run_covers_every_block_once():
+    """bench.py --gpus 2 starts two ranks itself (torch.distributed.run,
+    gloo on the CPU with --dry-run) and the byte-balanced shards of the
+    described batch cover every block exactly once."""
+    import json
+    import subprocess
+    import sys
+
+    root = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+    for cfg in ("C2", "C3"):
+        out = subprocess.run([sys.executable, os.path.join(root, "bench.py"), "--gpus", "2",
+                              "--dry-run", "--config", cfg], capture_output=True, text=True,
+                             timeout=300, cwd=root)
+        assert out.returncode == 0, out.stderr[-2000:]
+        line = json.loads([x for x in out.stdout.splitlines() if x.startswith("{")][-1])
+        assert line["n_gpus"] == 2 and line["every_block_once"] and line["starts_match"]
+        a, b = line["shards"]
+        assert a["hi"] == b["lo"] and abs(a["bytes"] - b["bytes"]) <= 2 * 65536

@@ -1,7 +1,9 @@
 #!/usr/bin/env python3
 """tools/ab_bench.py -- interleaved A/B of kernel variants in ONE process
 (cdna_hip_programming.md §5.4 rule 24).  Variants are selected through
-environment variables read by the launchers at each call.
+environment variables read by the launchers of the DIAGNOSTICS build
+(lib/libforst_checksum_diag.so) at each call; the product library has no
+variants.
 
   python tools/ab_bench.py --config C2 --var FORST_CRC_VARIANT=simple --var FORST_CRC_VARIANT=
 """
@@ -12,6 +14,10 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
+
+# kernel variants live only in the diagnostics build (make -C forst_amd/csrc diag)
+os.environ.setdefault("FORST_LIB_PATH", os.path.join(ROOT, "forst_amd", "lib",
+                                                     "libforst_checksum_diag.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402

@@ -9,6 +9,9 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 variants = sys.argv[1:] or ["FORST_WAL_VARIANT=", "FORST_WAL_VARIANT=wave"]
 for v in variants:
     env = dict(os.environ)
+    # variants exist only in the diagnostics build (make -C forst_amd/csrc diag)
+    env.setdefault("FORST_LIB_PATH", os.path.join(ROOT, "forst_amd", "lib",
+                                                  "libforst_checksum_diag.so"))
     k, _, val = v.partition("=")
     env[k] = val
     code = ("import sys, json; sys.path.insert(0, %r); import bench; "

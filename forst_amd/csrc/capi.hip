@@ -1,8 +1,12 @@
 // forst_amd/csrc/capi.hip -- the C ABI (include/forst_checksum.h).
 //
 // Argument validation, per-device info cache and dispatch to the kernel
-// launchers.  No entry point allocates, copies or synchronises, so callers
-// may capture them into hipGraphs (cdna_hip_programming.md Guideline 9).
+// launchers.  Scratch comes from a stream-ordered per-device pool
+// (hipMallocFromPoolAsync / hipFreeAsync).  The block, raw-hash, combine, KV
+// and WAL-writer entry points never copy to the host or synchronise, so they
+// can be captured into hipGraphs (cdna_hip_programming.md Guideline 9);
+// forst_wal_verify_batch, forst_wal_record_xxh3_batch and forst_wal_recover_batch
+// read a record count back (one stream synchronisation each) and cannot be.
 #include <hip/hip_runtime.h>
 
 #include <cstdio>

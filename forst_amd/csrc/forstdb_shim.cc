@@ -4,6 +4,7 @@
 
 #include <hip/hip_runtime.h>
 
+#include <chrono>
 #include <string>
 #include <vector>
 
@@ -111,6 +112,16 @@ Status BlockChecksumEngine::VerifyBlocks(ChecksumType type, uint32_t base_contex
   }
   if (b.n == 0) return Status::OK();
   if (file_offsets.size() != b.n) return Status::InvalidArgument("file_offsets.size() != n");
+  // PERF_TIMER_GUARD(block_checksum_time) (reader_common.cc:29), per batch
+  struct Timer {
+    uint64_t* acc;
+    std::chrono::steady_clock::time_point t0 = std::chrono::steady_clock::now();
+    ~Timer() {
+      *acc += static_cast<uint64_t>(std::chrono::duration_cast<std::chrono::nanoseconds>(
+                                        std::chrono::steady_clock::now() - t0)
+                                        .count());
+    }
+  } timer{&stats_.block_checksum_time};
   Status s = EnsureScratch(b.n);
   if (!s.ok()) return s;
   hipStream_t st = static_cast<hipStream_t>(stream_);

@@ -49,6 +49,13 @@ int unsupported(const std::string& m) {
   g_sst_err = m;
   return FORST_EUNSUPPORTED;
 }
+// ReadFooterFromFile's own message ends in ": <file>" rather than the " in
+// <file>" that CopyAppendMessage adds to DecodeFrom's errors (format.cc:491-495)
+constexpr int kTooShort = -100;
+int too_short(const std::string& m) {
+  g_sst_err = m;
+  return kTooShort;
+}
 
 uint32_t fixed32(const uint8_t* p) {
   return uint32_t(p[0]) | (uint32_t(p[1]) << 8) | (uint32_t(p[2]) << 16) | (uint32_t(p[3]) << 24);
@@ -201,6 +208,8 @@ int properties(const uint8_t* blk, uint64_t size, forst_sst_properties* pr) {
           if (varint64(q, vlim, &x)) pr->format_version = x;
         } else if (k == "rocksdb.data.size") {
           if (varint64(q, vlim, &x)) pr->data_size = x;
+        } else if (k == "rocksdb.external_sst_file.global_seqno") {  // sst_file_writer_collectors.h
+          pr->global_seqno_value_offset = static_cast<uint64_t>(v - blk);
         }
         return static_cast<uint64_t>(vlim - v);
       });
@@ -214,15 +223,25 @@ __attribute__((visibility("default"))) const char* forst_sst_last_error(void) {
   return g_sst_err.c_str();
 }
 
+static int footer_decode(const uint8_t* tail, uint64_t tail_len, uint64_t file_size,
+                         forst_sst_footer* f);
+
 // Footer::DecodeFrom (format.cc:355-463) on the last <= 53 bytes of a file.
 __attribute__((visibility("default"))) int forst_sst_footer_decode(const uint8_t* tail,
                                                                   uint64_t tail_len,
                                                                   uint64_t file_size,
                                                                   forst_sst_footer* f) {
+  const int rc = footer_decode(tail, tail_len, file_size, f);
+  return rc == kTooShort ? FORST_ECORRUPT : rc;
+}
+
+static int footer_decode(const uint8_t* tail, uint64_t tail_len, uint64_t file_size,
+                         forst_sst_footer* f) {
   if (!tail || !f) return FORST_EINVAL;
   std::memset(f, 0, sizeof(*f));
-  if (file_size < kVersion0Len || tail_len < kVersion0Len)  // format.cc:490-496
-    return corrupt("file is too short (" + std::to_string(file_size) + " bytes) to be an sstable");
+  if (file_size < kVersion0Len || tail_len < kVersion0Len)  // format.cc:490-496 (+ ": <file>")
+    return too_short("file is too short (" + std::to_string(file_size) +
+                     " bytes) to be an sstable: ");
   if (tail_len > file_size) return FORST_EINVAL;
   const uint64_t input_offset = file_size - tail_len;
   const uint8_t* magic_ptr = tail + tail_len - 8;
@@ -276,8 +295,8 @@ __attribute__((visibility("default"))) int forst_sst_footer_decode(const uint8_t
     f->metaindex_offset = metaindex_end - metaindex_size;
     f->metaindex_size = metaindex_size;
     f->index_offset = f->index_size = 0;  // in the metaindex ("rocksdb.index")
-    if (fixed64(in + 32) != 0)            // format.cc:440-448
-      return unsupported("File uses a future feature not supported in this version");
+    // format.cc:440-448: checked after the footer checksum (by the caller)
+    f->future_feature = fixed64(in + 32) != 0 ? 1u : 0u;
     f->footer_checksum_modifier =
         forstdb::ChecksumModifierForContext(f->base_context_checksum, f->footer_offset);
   } else {
@@ -324,9 +343,12 @@ __attribute__((visibility("default"))) int forst_sst_properties_decode(const uin
 namespace forstdb {
 namespace {
 
+// Status::CopyAppendMessage(s, " in ", file) of ReadFooterFromFile and the
+// block readers (format.cc:548-551)
 Status from_sst_rc(int rc, const std::string& file) {
+  if (rc == kTooShort) return Status::Corruption(g_sst_err + file);
   if (rc == FORST_ECORRUPT) return Status::Corruption(g_sst_err + " in " + file);
-  if (rc == FORST_EUNSUPPORTED) return Status::NotSupported(g_sst_err);
+  if (rc == FORST_EUNSUPPORTED) return Status::NotSupported(g_sst_err + " in " + file);
   return Status::InvalidArgument("forst_sst: " + std::to_string(rc));
 }
 
@@ -350,7 +372,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   // 1. footer (ReadFooterFromFile, format.cc:486-553)
   forst_sst_footer f;
   const uint64_t tail = file_size < kNewVersionsLen ? file_size : kNewVersionsLen;
-  int rc = forst_sst_footer_decode(host_file + file_size - tail, tail, file_size, &f);
+  int rc = footer_decode(host_file + file_size - tail, tail, file_size, &f);
   if (rc) return from_sst_rc(rc, file_name);
   rep.format_version = f.format_version;
   rep.checksum_type = f.checksum_type;
@@ -389,6 +411,9 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       return Status::Corruption("Footer at " + std::to_string(f.footer_offset) +
                                 " checksum mismatch in " + file_name);
   }
+  if (f.future_feature)  // format.cc:440-448, after the checksum compare
+    return Status::NotSupported("File uses a future feature not supported in this version in " +
+                                file_name);
   // device descriptors for block batches
   auto verify = [&](const std::vector<Handle>& hs, std::vector<uint64_t>* failed) -> Status {
     if (hs.empty()) return Status::OK();
@@ -423,6 +448,36 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
     (void)hipFree(d);
     return s;
   };
+  // VerifyBlockChecksum over a host copy of block h (+ trailer) whose 8 bytes
+  // at `zero_at` are zeroed (meta_blocks.cc:407-414), checksummed on the GPU
+  auto verify_patched = [&](const Handle& h, uint64_t zero_at) -> Status {
+    const uint64_t len = h.size + kBlockTrailer;
+    std::vector<uint8_t> tmp(host_file + h.off, host_file + h.off + len);
+    std::memset(tmp.data() + zero_at, 0, 8);
+    void* d = nullptr;
+    Status s2 = hip_status(hipMalloc(&d, len + 256), "hipMalloc");
+    if (!s2.ok()) return s2;
+    uint8_t* dblk = static_cast<uint8_t*>(d);
+    uint64_t* doff = reinterpret_cast<uint64_t*>(dblk + ((len + 15) & ~uint64_t(15)));
+    uint32_t* dsz = reinterpret_cast<uint32_t*>(doff + 1);
+    const uint64_t zero = 0;
+    const uint32_t sz = static_cast<uint32_t>(h.size);
+    s2 = hip_status(hipMemcpyAsync(dblk, tmp.data(), len, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    if (s2.ok()) s2 = hip_status(hipMemcpyAsync(doff, &zero, 8, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    if (s2.ok()) s2 = hip_status(hipMemcpyAsync(dsz, &sz, 4, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+    if (s2.ok()) {
+      DeviceBlockBatch b;
+      b.base = dblk;
+      b.base_len = len;
+      b.offsets = doff;
+      b.sizes = dsz;
+      b.n = 1;
+      s2 = eng.VerifyBlocks(type, bcc, b, file_name, {h.off}, nullptr);
+    }
+    (void)hipStreamSynchronize(st);
+    (void)hipFree(d);
+    return s2;
+  };
   auto host_block = [&](const Handle& h, const char* what) -> Status {
     if (h.off > file_size || h.size > file_size - h.off || file_size - h.off - h.size < kBlockTrailer)
       return Status::Corruption(std::string(what) + " block handle past end of file in " + file_name);
@@ -450,12 +505,18 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   std::vector<Handle> meta_blocks;  // VerifyChecksumInMetaBlocks order
   for (const MetaEntry& e : meta) {
     if (e.name == "rocksdb.properties" || e.name == "rocksdb.stats") {
-      s = verify({e.h}, nullptr);
-      if (!s.ok()) return s;
+      // ReadTablePropertiesHelper (meta_blocks.cc:250-417): decode, then the
+      // checksum -- retried with an ingested file's global seqno zeroed
       s = host_block(e.h, "properties");
       if (!s.ok()) return s;
       rc = properties(host_file + e.h.off, e.h.size, &props);
       if (rc) return from_sst_rc(rc, file_name);
+      s = verify({e.h}, nullptr);
+      if (s.IsCorruption() && props.global_seqno_value_offset != 0 &&
+          props.global_seqno_value_offset + 8 <= e.h.size) {
+        s = verify_patched(e.h, props.global_seqno_value_offset);
+      }
+      if (!s.ok()) return s;
     } else if (e.name == "rocksdb.index") {
       ix = e.h;
       have_index = true;
@@ -542,6 +603,11 @@ std::vector<Status> VerifySstFilesChecksums(BlockChecksumEngine& eng,
     const SstFileRef& r = files[f];
     if (r.dev_offset > arena_len || r.file_size > arena_len - r.dev_offset) {
       out[f] = Status::InvalidArgument("file " + r.file_name + " outside the device arena");
+      continue;
+    }
+    if ((reinterpret_cast<uintptr_t>(dev_arena) + r.dev_offset) & 3) {
+      out[f] = Status::InvalidArgument("file " + r.file_name +
+                                       ": device offset must be 4-byte aligned");
       continue;
     }
     std::vector<Handle> bulk;

@@ -33,9 +33,6 @@ class WalStatus(enum.IntEnum):
     OLD_RECORD = 4
 
 
-GPU_CHECKSUM_TYPES = (ChecksumType.kNoChecksum, ChecksumType.kCRC32c, ChecksumType.kXXH3)
-
-
 def _p(t):
     return None if t is None else t.data_ptr()
 

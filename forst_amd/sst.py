@@ -19,7 +19,7 @@ class Footer(ctypes.Structure):
                 ("stored_footer_checksum", ctypes.c_uint32),
                 ("footer_checksum_modifier", ctypes.c_uint32),
                 ("block_trailer_size", ctypes.c_uint32), ("footer_len", ctypes.c_uint32),
-                ("footer_zeroed", ctypes.c_uint8 * 53)]
+                ("footer_zeroed", ctypes.c_uint8 * 53), ("future_feature", ctypes.c_uint32)]
 
 
 class Properties(ctypes.Structure):
@@ -27,7 +27,7 @@ class Properties(ctypes.Structure):
                 ("index_value_is_delta_encoded", ctypes.c_uint64),
                 ("index_key_is_user_key", ctypes.c_uint64), ("num_data_blocks", ctypes.c_uint64),
                 ("index_partitions", ctypes.c_uint64), ("format_version", ctypes.c_uint64),
-                ("data_size", ctypes.c_uint64)]
+                ("data_size", ctypes.c_uint64), ("global_seqno_value_offset", ctypes.c_uint64)]
 
 
 class VerifyResult(ctypes.Structure):

@@ -90,6 +90,11 @@ std::string BlockChecksumMismatchMessage(ChecksumType type, uint32_t stored, uin
 struct ChecksumStats {
   uint64_t block_checksum_compute_count = 0;   // BLOCK_CHECKSUM_COMPUTE_COUNT
   uint64_t block_checksum_mismatch_count = 0;  // BLOCK_CHECKSUM_MISMATCH_COUNT
+  // PerfContext::block_checksum_time (include/rocksdb/perf_context.h:97):
+  // nanoseconds spent verifying block checksums -- the reference times each
+  // VerifyBlockChecksum call (PERF_TIMER_GUARD, reader_common.cc:29); here
+  // the wall time of each VerifyBlocks batch (launch + wait for its result)
+  uint64_t block_checksum_time = 0;
 };
 
 // A batch of blocks resident in device memory.  Block i occupies

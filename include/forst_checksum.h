@@ -52,8 +52,10 @@
  *    asynchronous and stream-ordered.  Scratch (work-feed counters, WAL
  *    record descriptors, chunk CRCs) comes from an engine-owned per-device
  *    memory pool with stream-ordered alloc/free and is zeroed with
- *    hipMemsetAsync; no call copies to the host or synchronises except
- *    forst_wal_verify_batch, which reads the record total back once.
+ *    hipMemsetAsync.  No call copies to the host or synchronises except
+ *    forst_wal_verify_batch, forst_wal_record_xxh3_batch and
+ *    forst_wal_recover_batch (each reads a record count back once) and the
+ *    explicitly synchronous host-memory / SST-file entry points below.
  *  - `base` must be 4-byte aligned; blocks live at base + offsets[i] and may
  *    start at any byte (SST blocks are packed back-to-back with 5-byte
  *    trailers, so starts are unaligned).  base_len bounds every access: a
@@ -168,7 +170,10 @@ int forst_xxh3_64_batch(const uint8_t* base, uint64_t base_len,
                         uint64_t* out, uint64_t n_buffers, void* stream);
 
 /* WAL replay (a13): log blocks [first_block, first_block + n_blocks) of the
- * log image `log` (log_len bytes; the last block may be short).  One entry
+ * log image `log` (log_len bytes; the last block may be short).  Checks
+ * physical records only (ReadPhysicalRecord: header chain, length, old
+ * record, zero type, CRC); fragment order and record types are the caller's
+ * (or forst_wal_recover_batch's).  One entry
  * per log block: status_out (FORST_WAL_*), nrec_out = physical records whose
  * CRC verified before the first failure, fail_off_out = byte offset in the
  * block of the failing header (or of the end of parsing).  Any out may be
@@ -198,8 +203,10 @@ int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
  * (recyclable types alike), hashed as the concatenation of its payloads.
  * hashes[j] / first_phys[j] (device, capacity n_phys; first_phys nullable)
  * for j < *n_logical (host).  Synchronises the stream once.  Defined for the
- * fragment sequences log::Writer emits; malformed sequences are the reader's
- * corruption path (forst_wal_verify_batch). */
+ * fragment sequences log::Writer emits.  Fragment-order and record-type
+ * validation (ReadRecord's "missing start of fragmented record", "unknown
+ * record type" ...) is NOT done here: forst_wal_recover_batch does the whole
+ * reader. */
 int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
                                 const uint64_t* header_offsets, uint64_t n_phys,
                                 uint64_t* hashes, uint64_t* first_phys, uint64_t* n_logical,
@@ -284,6 +291,11 @@ typedef struct forst_sst_footer {
   uint32_t block_trailer_size;
   uint32_t footer_len;
   uint8_t footer_zeroed[53];
+  /* fv >= 6: the 8 checked reserved bytes are non-zero.  The reference
+   * (format.cc:440-448) reports NotSupported("File uses a future feature not
+   * supported in this version") only AFTER the footer checksum matched, so
+   * this is a flag, not an error of forst_sst_footer_decode. */
+  uint32_t future_feature;
 } forst_sst_footer;
 
 /* Table properties the checksum walk needs (table/meta_blocks.cc:81-140,
@@ -297,6 +309,11 @@ typedef struct forst_sst_properties {
   uint64_t index_partitions;
   uint64_t format_version;
   uint64_t data_size;
+  /* offset of the 8-byte "rocksdb.external_sst_file.global_seqno" value
+   * inside the properties block, 0 when absent (meta_blocks.cc:346-348):
+   * ingestion may rewrite it after the block checksum was taken, so the
+   * properties checksum is retried with it zeroed (meta_blocks.cc:401-417) */
+  uint64_t global_seqno_value_offset;
 } forst_sst_properties;
 
 typedef struct forst_sst_verify_result {
@@ -333,7 +350,9 @@ int forst_sst_verify_file(const uint8_t* host_file, uint64_t file_size, const ui
 
 /* DB::VerifyChecksum (db/db_impl/db_impl.cc:6254 -> convenience.cc:57 per
  * file) over n_files SST files: file i is host_files[i] (file_sizes[i] bytes)
- * in host memory and dev_arena[dev_offsets[i] ..] in device memory.  Each
+ * in host memory and dev_arena[dev_offsets[i] ..] in device memory (each
+ * dev_offsets[i] 4-byte aligned, as device buffers are: a file at an
+ * unaligned offset gets InvalidArgument in out[i]).  Each
  * file's structural blocks are checked as in forst_sst_verify_file; the meta
  * and data blocks of ALL files are then verified in one launch per checksum
  * type.  out[i] = exactly what forst_sst_verify_file returns for file i.

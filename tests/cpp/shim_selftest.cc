@@ -2,12 +2,17 @@
 // (include/forst/checksum_engine.h) the way a ForSt call site would.
 //   shim_selftest pure   host-only helpers (no GPU)
 //   shim_selftest gpu    BlockChecksumEngine write/verify on a real MI355X
+//   shim_selftest threads  4 host threads, one HIP stream each, interleaving
+//                        write-side, verify, WAL and raw-hash calls against
+//                        the engine's shared per-device scratch pool
 // Prints PASS or FAIL lines; exit code 0 iff all passed.
 #include <hip/hip_runtime.h>
 
+#include <atomic>
 #include <cstdio>
 #include <cstring>
 #include <string>
+#include <thread>
 #include <vector>
 
 #include "forst/checksum_engine.h"
@@ -137,10 +142,156 @@ static void gpu() {
   (void)hipFree(d_types);
 }
 
+// One thread's private inputs: an SST-packed batch and a WAL image.
+struct Work {
+  int n = 0;
+  uint64_t total = 0;
+  std::vector<uint64_t> offs;
+  std::vector<uint32_t> sizes;
+  uint8_t *d_base = nullptr, *d_types = nullptr, *d_log = nullptr;
+  uint64_t *d_offs = nullptr, *d_hoffs = nullptr, *d_h64 = nullptr;
+  uint32_t *d_sizes = nullptr, *d_out = nullptr, *d_comp = nullptr, *d_crc = nullptr;
+  uint8_t *d_ok = nullptr, *d_st = nullptr;
+  uint32_t *d_nrec = nullptr, *d_fail = nullptr;
+  unsigned long long* d_bad = nullptr;
+  uint64_t log_len = 0, n_phys = 0, n_lblocks = 0;
+  // expected results (single-threaded pass)
+  std::vector<uint32_t> want_out, want_crc;
+  std::vector<uint64_t> want_h64;
+};
+
+static bool setup_work(Work& w, int seed) {
+  bool ok = true;
+  w.n = 3000;
+  w.offs.resize(w.n);
+  w.sizes.resize(w.n);
+  for (int i = 0; i < w.n; ++i) {
+    w.sizes[i] = ((i + seed) * 2654435761u) % 20000;
+    w.offs[i] = w.total;
+    w.total += w.sizes[i] + 5;
+  }
+  ok &= hipMalloc(&w.d_base, w.total + 256) == hipSuccess;
+  ok &= hipMalloc(&w.d_offs, w.n * 8) == hipSuccess;
+  ok &= hipMalloc(&w.d_sizes, w.n * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_types, w.n) == hipSuccess;
+  ok &= hipMalloc(&w.d_out, w.n * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_comp, w.n * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_ok, w.n) == hipSuccess;
+  ok &= hipMalloc(&w.d_h64, w.n * 8) == hipSuccess;
+  ok &= hipMemcpy(w.d_offs, w.offs.data(), w.n * 8, hipMemcpyHostToDevice) == hipSuccess;
+  ok &= hipMemcpy(w.d_sizes, w.sizes.data(), w.n * 4, hipMemcpyHostToDevice) == hipSuccess;
+  ok &= hipMemset(w.d_types, 1, w.n) == hipSuccess;
+  ok &= forst_fill_stream(w.d_base, 0, w.total, 1000 + seed, nullptr) == FORST_OK;
+  // WAL image (db/log_writer.cc layout from forst_wal_layout, payload from
+  // the splitmix stream, zero-filled block tails, CRCs by the writer kernel)
+  std::vector<uint32_t> lens(2000);
+  for (size_t i = 0; i < lens.size(); ++i) lens[i] = ((i + seed) * 40503u) % 40000;
+  uint64_t np = 0, npad = 0, tot = 0;
+  ok &= forst_wal_layout(lens.data(), lens.size(), 0, nullptr, nullptr, nullptr, 0, nullptr,
+                         nullptr, 0, &np, &npad, &tot) == FORST_OK;
+  std::vector<uint64_t> ho(np), po(npad + 1);
+  std::vector<uint32_t> hl(np), pl(npad + 1);
+  std::vector<uint8_t> ht(np);
+  ok &= forst_wal_layout(lens.data(), lens.size(), 0, ho.data(), hl.data(), ht.data(), np,
+                         po.data(), pl.data(), npad, &np, &npad, &tot) == FORST_OK;
+  w.log_len = tot;
+  w.n_phys = np;
+  w.n_lblocks = (tot + 32767) / 32768;
+  ok &= hipMalloc(&w.d_log, tot + 256) == hipSuccess;
+  ok &= forst_fill_stream(w.d_log, 0, tot, 2000 + seed, nullptr) == FORST_OK;
+  std::vector<uint8_t> img(tot);
+  ok &= hipMemcpy(img.data(), w.d_log, tot, hipMemcpyDeviceToHost) == hipSuccess;
+  for (uint64_t i = 0; i < np; ++i) {
+    img[ho[i] + 4] = static_cast<uint8_t>(hl[i]);
+    img[ho[i] + 5] = static_cast<uint8_t>(hl[i] >> 8);
+    img[ho[i] + 6] = ht[i];
+  }
+  for (uint64_t i = 0; i < npad; ++i) std::memset(img.data() + po[i], 0, pl[i]);
+  ok &= hipMemcpy(w.d_log, img.data(), tot, hipMemcpyHostToDevice) == hipSuccess;
+  ok &= hipMalloc(&w.d_hoffs, np * 8) == hipSuccess;
+  ok &= hipMemcpy(w.d_hoffs, ho.data(), np * 8, hipMemcpyHostToDevice) == hipSuccess;
+  ok &= hipMalloc(&w.d_crc, np * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_st, w.n_lblocks) == hipSuccess;
+  ok &= hipMalloc(&w.d_nrec, w.n_lblocks * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_fail, w.n_lblocks * 4) == hipSuccess;
+  ok &= hipMalloc(&w.d_bad, 8) == hipSuccess;
+  return ok;
+}
+
+// one round of every kind of call on `stream`; results compared with the
+// expected ones when `check`, recorded as expected otherwise
+static bool round_of_calls(Work& w, void* stream, bool check) {
+  hipStream_t st = static_cast<hipStream_t>(stream);
+  bool ok = true;
+  ok &= forst_block_trailer_batch(kCRC32c, w.d_base, w.total, w.d_offs, w.d_sizes, w.d_types,
+                                  nullptr, w.d_out, w.n, stream) == FORST_OK;
+  ok &= hipMemsetAsync(w.d_bad, 0, 8, st) == hipSuccess;
+  ok &= forst_block_verify_batch(kCRC32c, w.d_base, w.total, w.d_offs, w.d_sizes, nullptr,
+                                 w.d_comp, nullptr, w.d_ok, w.d_bad, w.n, stream) == FORST_OK;
+  ok &= forst_wal_record_crc_batch(w.d_log, w.log_len, w.d_hoffs, w.n_phys, 1, w.d_crc,
+                                   stream) == FORST_OK;
+  unsigned long long bad_blocks = 0;
+  ok &= hipMemsetAsync(w.d_bad, 0, 8, st) == hipSuccess;
+  ok &= forst_xxh3_64_batch(w.d_base, w.total, w.d_offs, w.d_sizes, w.d_h64, w.n, stream) ==
+        FORST_OK;
+  // (synchronises its stream once: the record total sizes the descriptors)
+  ok &= forst_wal_verify_batch(w.d_log, w.log_len, 0, w.n_lblocks, 0, w.d_st, w.d_nrec,
+                               w.d_fail, w.d_bad, stream) == FORST_OK;
+  std::vector<uint32_t> out(w.n), comp(w.n), crc(w.n_phys), nrec(w.n_lblocks);
+  std::vector<uint64_t> h64(w.n);
+  std::vector<uint8_t> okv(w.n);
+  ok &= hipMemcpyAsync(out.data(), w.d_out, w.n * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipMemcpyAsync(comp.data(), w.d_comp, w.n * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipMemcpyAsync(okv.data(), w.d_ok, w.n, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipMemcpyAsync(crc.data(), w.d_crc, w.n_phys * 4, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipMemcpyAsync(h64.data(), w.d_h64, w.n * 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipMemcpyAsync(nrec.data(), w.d_nrec, w.n_lblocks * 4, hipMemcpyDeviceToHost, st) ==
+        hipSuccess;
+  ok &= hipMemcpyAsync(&bad_blocks, w.d_bad, 8, hipMemcpyDeviceToHost, st) == hipSuccess;
+  ok &= hipStreamSynchronize(st) == hipSuccess;
+  if (!ok) return false;
+  for (int i = 0; i < w.n; ++i) ok &= okv[i] == 1 && comp[i] == out[i];
+  uint64_t recs = 0;
+  for (uint32_t r : nrec) recs += r;
+  ok &= recs == w.n_phys && bad_blocks == 0;
+  if (!check) {
+    w.want_out = out;
+    w.want_crc = crc;
+    w.want_h64 = h64;
+    return ok;
+  }
+  return ok && out == w.want_out && crc == w.want_crc && h64 == w.want_h64;
+}
+
+static void threads() {
+  constexpr int kThreads = 4, kRounds = 12;
+  std::vector<Work> work(kThreads);
+  for (int t = 0; t < kThreads; ++t) CHECK(setup_work(work[t], t));
+  for (int t = 0; t < kThreads; ++t) CHECK(round_of_calls(work[t], nullptr, false));
+  std::atomic<int> failures{0};
+  std::vector<std::thread> th;
+  for (int t = 0; t < kThreads; ++t) {
+    th.emplace_back([&, t] {
+      hipStream_t s;
+      if (hipStreamCreateWithFlags(&s, hipStreamNonBlocking) != hipSuccess) {
+        ++failures;
+        return;
+      }
+      for (int r = 0; r < kRounds; ++r)
+        if (!round_of_calls(work[t], s, true)) ++failures;
+      (void)hipStreamDestroy(s);
+    });
+  }
+  for (auto& x : th) x.join();
+  CHECK(failures.load() == 0);
+  std::printf("threads: %d x %d rounds, failures %d\n", kThreads, kRounds, failures.load());
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "pure";
   pure();
   if (mode == "gpu") gpu();
+  if (mode == "threads") threads();
   std::printf(g_fail ? "FAIL (%d)\n" : "PASS\n", g_fail);
   return g_fail ? 1 : 0;
 }

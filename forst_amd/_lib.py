@@ -32,7 +32,8 @@ def exported_symbols():
     hdr = os.path.join(os.path.dirname(_HERE), "include", "forst_checksum.h")
     with open(hdr) as f:
         text = f.read()
-    return sorted(set(re.findall(r"^\s*(?:int|uint32_t|const char\*)\s+(forst_\w+)\(", text, re.M)))
+    return sorted(set(re.findall(r"^\s*(?:int|uint32_t|uint64_t|const char\*)\s+(forst_\w+)\(",
+                                 text, re.M)))
 
 
 def lib():
@@ -73,6 +74,20 @@ def lib():
                                       u64, vp]),
         "forst_wal_layout": (i, [vp, u64, i, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp]),
         "forst_fill_stream": (i, [vp, u64, u64, u64, vp]),
+        "forst_partition_bytes": (i, [vp, u64, u32, vp]),
+        "forst_block_verify_host": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp, i]),
+        "forst_block_checksum_host": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp, i]),
+        "forst_host_register": (i, [vp, u64]),
+        "forst_host_unregister": (i, [vp]),
+        "forst_host_last_error": (ctypes.c_char_p, []),
+        "forst_trailer_writer_open": (i, [i, u32, u64, u32, u64, vp, vp, vp, vp]),
+        "forst_trailer_writer_add": (i, [vp, vp, u64, ctypes.c_uint8, i, vp, vp]),
+        "forst_trailer_writer_flush": (i, [vp]),
+        "forst_trailer_writer_footer": (i, [vp, u32, u64, u64, u64, u64]),
+        "forst_trailer_writer_offset": (u64, [vp]),
+        "forst_trailer_writer_close": (i, [vp]),
+        "forst_trailer_writer_last_error": (ctypes.c_char_p, []),
+        "forst_sst_footer_build": (i, [u32, i, u64, u32, u64, u64, u64, u64, vp, vp, vp]),
     }
     for name, (res, args) in sigs.items():
         f = getattr(L, name)

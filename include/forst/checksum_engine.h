@@ -17,6 +17,7 @@
 #pragma once
 
 #include <cstdint>
+#include <functional>
 #include <string>
 #include <vector>
 
@@ -175,5 +176,57 @@ std::vector<Status> VerifySstFilesChecksums(BlockChecksumEngine& engine,
                                             const std::vector<SstFileRef>& files,
                                             const uint8_t* dev_arena, uint64_t arena_len,
                                             std::vector<SstVerifyReport>* reports = nullptr);
+
+// Write-side batching for flush and compaction:
+// BlockBasedTableBuilder::WriteMaybeCompressedBlock
+// (table/block_based/block_based_table_builder.cc:1311-1360) with the trailer
+// deferred.  AddBlock places the block at its final file offset at once
+// (handle = (offset, n), as the reference sets it) and writes the type byte;
+// the LE32 checksum -- ComputeBuiltinChecksumWithLastByte(block, type) +
+// ChecksumModifierForContext(base_context_checksum, offset) -- is filled when
+// the block's window comes back from the GPU (one batch launch per window,
+// two pinned windows alternating), and windows reach the sink
+// (WritableFileWriter::Append) in file order.  block_align pads data blocks
+// like :1385-1395; WriteFooter is FooterBuilder::Build (format.cc:231-330).
+class GpuTrailerWriter {
+ public:
+  struct Options {
+    ChecksumType checksum = kXXH3;       // BlockBasedTableOptions::checksum (table.h:257)
+    uint32_t base_context_checksum = 0;  // format_version >= 6 (builder.cc:615-623)
+    uint64_t start_offset = 0;           // file offset of the first block
+    bool block_align = false;            // BlockBasedTableOptions::block_align
+    uint64_t alignment = 4096;
+    uint64_t window_bytes = 32ull << 20;  // blocks per GPU launch (bytes)
+  };
+  using Sink = std::function<Status(const char* data, size_t n)>;
+  GpuTrailerWriter(const Options& opt, Sink sink, void* hip_stream = nullptr);
+  ~GpuTrailerWriter();
+  GpuTrailerWriter(const GpuTrailerWriter&) = delete;
+  GpuTrailerWriter& operator=(const GpuTrailerWriter&) = delete;
+
+  Status AddBlock(const char* data, size_t n, uint8_t compression_type, bool is_data_block,
+                  uint64_t* handle_offset, uint64_t* handle_size);
+  // every pending trailer computed and every byte handed to the sink
+  Status Flush();
+  // Flush + the footer for (metaindex, index) handles at the current offset
+  Status WriteFooter(uint32_t format_version, uint64_t metaindex_offset, uint64_t metaindex_size,
+                     uint64_t index_offset, uint64_t index_size);
+  uint64_t offset() const { return offset_; }  // r->get_offset()
+  const ChecksumStats& stats() const { return stats_; }
+
+ private:
+  struct Window;
+  Status Reserve(Window& w, uint64_t bytes, uint64_t blocks);
+  Status Launch(Window& w);
+  Status Retire(Window& w);
+  Options opt_;
+  Sink sink_;
+  void* stream_;
+  uint64_t offset_;
+  Window* win_[2];
+  int cur_ = 0;
+  Status status_;
+  ChecksumStats stats_;
+};
 
 }  // namespace forstdb

@@ -270,6 +270,78 @@ int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
  * call on this thread and the launch configuration used. */
 const char* forst_last_kernel(void);
 
+/* ---- Host-memory batches over the GPUs of one process ------
+ * ForSt is one process (DB::VerifyChecksum, db/db_impl/db_impl.cc:6254, walks
+ * every file in it); its blocks start in host memory (table builder buffers,
+ * FilePrefetchBuffer, mmap'd SST pages -- env/io_posix.cc:958).  These calls
+ * take HOST arrays, cut the blocks into contiguous byte-balanced ranges, one
+ * per entry of devices[] (forst_partition_bytes), and give every device its
+ * own host thread, HIP stream and pinned staging: the range streams through
+ * two 64 MiB device windows (the copy of the next window overlaps the kernel
+ * on this one) and 4-5 result bytes per block come back.  Pinned or
+ * registered host memory (forst_host_register) is copied by DMA in place;
+ * pageable memory goes through the thread's pinned staging.  No data moves
+ * between devices.  Synchronous; errors via forst_host_last_error().  A
+ * device may appear more than once (several threads/streams on one GPU). */
+
+/* cuts[0..parts]: part p = blocks [cuts[p], cuts[p+1]), part p starting at the
+ * first block whose payload-byte prefix reaches p/parts of the total. */
+int forst_partition_bytes(const uint32_t* sizes, uint64_t n, uint32_t parts, uint64_t* cuts);
+/* forst_block_verify_batch over host memory (host arrays; computed / stored /
+ * ok / mismatches may be NULL; *mismatches = failing blocks). */
+int forst_block_verify_host(int checksum_type, const uint8_t* host_base, uint64_t base_len,
+                            const uint64_t* offsets, const uint32_t* sizes,
+                            const uint32_t* modifiers, uint32_t* computed, uint32_t* stored,
+                            uint8_t* ok, uint64_t* mismatches, uint64_t n_blocks,
+                            const int* devices, int n_devices);
+/* forst_block_checksum_batch over host memory (write side: the caller's
+ * table writer appends the trailers, see forst_trailer_writer_*). */
+int forst_block_checksum_host(int checksum_type, const uint8_t* host_base, uint64_t base_len,
+                              const uint64_t* offsets, const uint32_t* sizes,
+                              const uint8_t* last_bytes, const uint32_t* modifiers, uint32_t* out,
+                              uint64_t n_blocks, const int* devices, int n_devices);
+/* hipHostRegister / hipHostUnregister of a host range (e.g. an mmap'd SST
+ * file) so the host-memory calls read it by DMA without staging. */
+int forst_host_register(void* p, uint64_t len);
+int forst_host_unregister(void* p);
+const char* forst_host_last_error(void);
+
+/* ---- Write side of flush / compaction with deferred trailers (§8f-3) --------
+ * BlockBasedTableBuilder::WriteMaybeCompressedBlock
+ * (table/block_based/block_based_table_builder.cc:1311-1360) as a batched
+ * writer: forst_trailer_writer_add places each block at its final offset
+ * (handle returned at once), the trailers of a window of blocks are computed
+ * in one GPU launch, and the finished bytes go to `sink` (WritableFileWriter::
+ * Append) in file order.  `sink` returns 0 on success.  block_align = 0 or the
+ * alignment for BlockBasedTableOptions::block_align padding of data blocks;
+ * window_bytes = 0 for the default (32 MiB). */
+typedef int (*forst_sink_fn)(void* arg, const uint8_t* data, uint64_t n);
+typedef struct forst_trailer_writer forst_trailer_writer;
+int forst_trailer_writer_open(int checksum_type, uint32_t base_context_checksum,
+                              uint64_t start_offset, uint32_t block_align, uint64_t window_bytes,
+                              forst_sink_fn sink, void* sink_arg, void* stream,
+                              forst_trailer_writer** out);
+int forst_trailer_writer_add(forst_trailer_writer* w, const uint8_t* block, uint64_t size,
+                             uint8_t compression_type, int is_data_block,
+                             uint64_t* handle_offset, uint64_t* handle_size);
+int forst_trailer_writer_flush(forst_trailer_writer* w);
+/* flush, then append the footer (forst_sst_footer_build at the current offset) */
+int forst_trailer_writer_footer(forst_trailer_writer* w, uint32_t format_version,
+                                uint64_t metaindex_offset, uint64_t metaindex_size,
+                                uint64_t index_offset, uint64_t index_size);
+uint64_t forst_trailer_writer_offset(const forst_trailer_writer* w);
+int forst_trailer_writer_close(forst_trailer_writer* w); /* flushes, frees */
+const char* forst_trailer_writer_last_error(void);
+
+/* FooterBuilder::Build (table/format.cc:231-330) of the block-based table:
+ * out (>= 53 bytes) / *out_len = 48 (fv 0) or 53.  For format_version >= 6
+ * the footer checksum is computed on the GPU (synchronises `stream`); fv < 6
+ * makes no GPU call. */
+int forst_sst_footer_build(uint32_t format_version, int checksum_type, uint64_t footer_offset,
+                           uint32_t base_context_checksum, uint64_t metaindex_offset,
+                           uint64_t metaindex_size, uint64_t index_offset, uint64_t index_size,
+                           uint8_t* out, uint32_t* out_len, void* stream);
+
 /* ---- SST files (BlockBasedTable::VerifyChecksum, ----------------------------
  * table/block_based/block_based_table_reader.cc:2457-2574) ----------------- */
 

@@ -88,11 +88,13 @@ def lib():
         "forst_trailer_writer_close": (i, [vp]),
         "forst_trailer_writer_last_error": (ctypes.c_char_p, []),
         "forst_sst_footer_build": (i, [u32, i, u64, u32, u64, u64, u64, u64, vp, vp, vp]),
+        "forst_wal_recover_batch": None,  # struct arguments: argtypes set by engine
     }
-    for name, (res, args) in sigs.items():
+    for name, sig in sigs.items():
         f = getattr(L, name)
-        f.restype = res
-        f.argtypes = args
+        if sig is None:
+            continue
+        f.restype, f.argtypes = sig
     _lib = L
     return L
 

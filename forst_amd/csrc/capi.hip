@@ -346,6 +346,29 @@ FORST_API int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
                     "wal_record_xxh3 launch");
 }
 
+FORST_API int forst_wal_recover_batch(const uint8_t* log, uint64_t log_len, uint32_t log_number,
+                                     int wal_recovery_mode, forst_wal_records records,
+                                     uint64_t record_capacity, forst_wal_reports reports,
+                                     uint64_t report_capacity, forst_wal_recover_result* result,
+                                     void* stream) {
+  if (!result) return set_error(FORST_EINVAL, "result must be non-null");
+  std::memset(result, 0, sizeof(*result));
+  if (log_len && (!log || !aligned4(log)))
+    return set_error(FORST_EINVAL, "log must be non-null, 4-byte aligned");
+  if (wal_recovery_mode < 0 || wal_recovery_mode > 3)
+    return set_error(FORST_EINVAL, "unknown WALRecoveryMode " + std::to_string(wal_recovery_mode));
+  int rc = check_device();
+  if (rc) return rc;
+  rc = hip_status(launch_wal_recover(log, log_len, log_number, wal_recovery_mode, records,
+                                     record_capacity, reports, report_capacity, result,
+                                     static_cast<hipStream_t>(stream), &g_last_kernel),
+                  "wal_recover launch");
+  if (rc == FORST_OK && result->unsupported)
+    return set_error(FORST_EUNSUPPORTED,
+                     "WAL compression / user-defined timestamp size records (types 9-11)");
+  return rc;
+}
+
 FORST_API int forst_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init, uint32_t* out,
                                   void* stream) {
   if (!out || (len && (!base || !aligned4(base))))

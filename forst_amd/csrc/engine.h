@@ -5,6 +5,8 @@
 
 #include <cstdint>
 
+#include "../../include/forst_checksum.h"
+
 namespace forst {
 
 // What a block launch does with each descriptor.
@@ -129,6 +131,10 @@ hipError_t launch_crc32c_buffer(const uint8_t* base, uint64_t len, uint32_t init
 hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out_first,
                                   uint64_t* n_logical_host, hipStream_t stream,
                                   const char** kernel_name);
+hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log_number, int mode,
+                              forst_wal_records recs, uint64_t rec_cap, forst_wal_reports reps,
+                              uint64_t rep_cap, forst_wal_recover_result* res, hipStream_t st,
+                              const char** name);
 hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_fill_stream(uint8_t* dev, uint64_t start, uint64_t n,
                               uint64_t seed, hipStream_t stream);

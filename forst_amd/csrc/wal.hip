@@ -35,6 +35,7 @@
 
 #include "device_common.h"
 #include "engine.h"
+#include "scan_common.h"
 
 namespace forst {
 
@@ -281,62 +282,6 @@ __device__ __forceinline__ FragInfo frag_info(const WalArgs& a, uint64_t i) {
     }
   }
   return f;
-}
-
-// u64 exclusive scan in three passes: tile sums, one-workgroup scan of the
-// tile sums, tile-local scans plus tile prefix
-__global__ void __launch_bounds__(kTile) scan_tiles_kernel(const uint64_t* in, uint64_t n,
-                                                           uint64_t* tile_sum) {
-  __shared__ uint64_t sh[kTile];
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
-  sh[threadIdx.x] = i < n ? in[i] : 0;
-  __syncthreads();
-  for (uint32_t d = kTile / 2; d >= 1; d >>= 1) {
-    if (threadIdx.x < d) sh[threadIdx.x] += sh[threadIdx.x + d];
-    __syncthreads();
-  }
-  if (threadIdx.x == 0) tile_sum[blockIdx.x] = sh[0];
-}
-
-__global__ void __launch_bounds__(kScanThreads) scan_top_kernel(uint64_t* tile_sum,
-                                                                uint64_t n_tiles) {
-  __shared__ uint64_t sh[kScanThreads];
-  const uint32_t t = threadIdx.x;
-  uint64_t carry = 0;
-  for (uint64_t c0 = 0; c0 < n_tiles; c0 += kScanThreads) {
-    const uint64_t i = c0 + t;
-    const uint64_t v = i < n_tiles ? tile_sum[i] : 0;
-    sh[t] = v;
-    __syncthreads();
-    for (uint32_t d = 1; d < kScanThreads; d <<= 1) {
-      const uint64_t add = t >= d ? sh[t - d] : 0;
-      __syncthreads();
-      sh[t] += add;
-      __syncthreads();
-    }
-    if (i < n_tiles) tile_sum[i] = carry + sh[t] - v;  // in place: exclusive prefix
-    carry += sh[kScanThreads - 1];
-    __syncthreads();
-  }
-  if (t == 0) tile_sum[n_tiles] = carry;
-}
-
-__global__ void __launch_bounds__(kTile) scan_apply_kernel(const uint64_t* in, uint64_t n,
-                                                           const uint64_t* tile_prefix,
-                                                           uint64_t* out) {
-  __shared__ uint64_t sh[kTile];
-  const uint32_t t = threadIdx.x;
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + t;
-  const uint64_t v = i < n ? in[i] : 0;
-  sh[t] = v;
-  __syncthreads();
-  for (uint32_t d = 1; d < kTile; d <<= 1) {
-    const uint64_t add = t >= d ? sh[t - d] : 0;
-    __syncthreads();
-    sh[t] += add;
-    __syncthreads();
-  }
-  if (i < n) out[i] = tile_prefix[blockIdx.x] + sh[t] - v;
 }
 
 // start flags (kFullType / kFirstType)

@@ -214,6 +214,83 @@ def wal_record_xxh3_batch(log, header_offsets, stream=None):
     return hashes[:nl.value], first[:nl.value]
 
 
+class WalRecords(ctypes.Structure):
+    """forst_wal_records (device array pointers)"""
+    _fields_ = [("offset", ctypes.c_void_p), ("length", ctypes.c_void_p),
+                ("hash", ctypes.c_void_p), ("n_fragments", ctypes.c_void_p)]
+
+
+class WalReports(ctypes.Structure):
+    """forst_wal_reports (device array pointers)"""
+    _fields_ = [("offset", ctypes.c_void_p), ("bytes", ctypes.c_void_p),
+                ("reason", ctypes.c_void_p), ("type", ctypes.c_void_p)]
+
+
+class WalRecoverResult(ctypes.Structure):
+    _fields_ = [("n_records", ctypes.c_uint64), ("n_reports", ctypes.c_uint64),
+                ("n_physical", ctypes.c_uint64), ("stop_offset", ctypes.c_uint64),
+                ("stop_reason", ctypes.c_uint32), ("truncated", ctypes.c_uint32),
+                ("unsupported", ctypes.c_uint32), ("reserved", ctypes.c_uint32)]
+
+
+# forst_wal_report_reason -> the reader's Reporter::Corruption text (log_reader.cc)
+WAL_REASONS = {1: "partial record without end(1)", 2: "partial record without end(2)",
+               3: "missing start of fragmented record(1)",
+               4: "missing start of fragmented record(2)", 5: "error in middle of record",
+               6: "checksum mismatch", 7: "bad record length", 8: "truncated header",
+               9: "error reading trailing data", 10: "truncated record body",
+               11: "unknown record type %u"}
+WAL_STOPS = {0: "eof", 1: "old_record", 2: "truncated_header", 3: "truncated_body",
+             4: "recycled_tail"}
+# WALRecoveryMode (include/rocksdb/options.h)
+kTolerateCorruptedTailRecords, kAbsoluteConsistency, kPointInTimeRecovery, \
+    kSkipAnyCorruptedRecords = 0, 1, 2, 3
+
+
+def _recover_sig(L):
+    f = L.forst_wal_recover_batch
+    if f.argtypes is None:
+        vp, u64 = ctypes.c_void_p, ctypes.c_uint64
+        f.restype = ctypes.c_int
+        f.argtypes = [vp, u64, ctypes.c_uint32, ctypes.c_int, WalRecords, u64, WalReports, u64,
+                      vp, vp]
+
+
+def wal_recover_batch(log, log_number=0, mode=kPointInTimeRecovery, record_capacity=None,
+                      report_capacity=1024, stream=None):
+    """log::Reader::ReadRecord over a whole device log image (log_reader.cc:69-320):
+    returns (records dict of device tensors offset/length/hash/n_fragments,
+    reports dict of device tensors offset/bytes/reason/type, result)."""
+    _dev_u8(log)
+    _recover_sig(lib())
+    if record_capacity is None:
+        record_capacity = max(1024, log.numel() // 1024)
+    while True:
+        dev = log.device
+        rec = {"offset": torch.empty(record_capacity, dtype=torch.int64, device=dev),
+               "length": torch.empty(record_capacity, dtype=torch.int64, device=dev),
+               "hash": torch.empty(record_capacity, dtype=torch.int64, device=dev),
+               "n_fragments": torch.empty(record_capacity, dtype=torch.int32, device=dev)}
+        rep = {"offset": torch.empty(report_capacity, dtype=torch.int64, device=dev),
+               "bytes": torch.empty(report_capacity, dtype=torch.int64, device=dev),
+               "reason": torch.empty(report_capacity, dtype=torch.int32, device=dev),
+               "type": torch.empty(report_capacity, dtype=torch.int32, device=dev)}
+        res = WalRecoverResult()
+        check(lib().forst_wal_recover_batch(
+            log.data_ptr(), log.numel(), log_number, mode,
+            WalRecords(*[rec[k].data_ptr() for k in ("offset", "length", "hash", "n_fragments")]),
+            record_capacity,
+            WalReports(*[rep[k].data_ptr() for k in ("offset", "bytes", "reason", "type")]),
+            report_capacity, ctypes.byref(res), _stream(stream)))
+        if not res.truncated:
+            break
+        record_capacity = max(record_capacity, res.n_records)
+        report_capacity = max(report_capacity, res.n_reports)
+    rec = {k: v[:res.n_records] for k, v in rec.items()}
+    rep = {k: v[:res.n_reports] for k, v in rep.items()}
+    return rec, rep, res
+
+
 def hash64_batch(base, offsets, lengths, seeds=None, seed=0, out=None, stream=None):
     """Hash64 / NPHash64 per buffer (util/hash.cc:81, XXPH3 0.7.2 preview)."""
     n = _desc(offsets, lengths)

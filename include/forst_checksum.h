@@ -212,6 +212,73 @@ int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
                                 uint64_t* hashes, uint64_t* first_phys, uint64_t* n_logical,
                                 void* stream);
 
+/* ---- Fused WAL recovery (§8f-2): log::Reader::ReadRecord over a whole log ---
+ * (db/log_reader.cc:69-320, ReadPhysicalRecord :450-531, ReadMore :404-448)
+ * as DBImpl::RecoverLogFiles (db/db_impl/db_impl_open.cc:1210) drives it, with
+ * every record boundary found on the device: the header walk, the CRC of
+ * every physical record, the fragment state machine and the XXH3_64bits
+ * record checksum of every logical record (:95-165), in one call, without
+ * header offsets from the host.  Output = what the reader returns, in order:
+ * the logical records (Reader::LastRecordOffset, length, XXH3, fragments) and
+ * the reporter's Corruption(bytes, reason) calls (reader position, bytes,
+ * reason, record type for "unknown record type %u").  wal_recovery_mode =
+ * WALRecoveryMode (include/rocksdb/options.h): 0 kTolerateCorruptedTailRecords,
+ * 1 kAbsoluteConsistency, 2 kPointInTimeRecovery, 3 kSkipAnyCorruptedRecords
+ * -- it decides which conditions are reported and whether old records end
+ * reading, exactly as in ReadRecord; stopping recovery on a report is the
+ * caller's (RecoverLogFiles') decision.  Output arrays are DEVICE arrays of
+ * the given capacities (any member may be NULL); *result (host) has the
+ * counts -- if a count exceeds its capacity, result->truncated is set and
+ * only the first `capacity` entries are written.  WAL compression and
+ * user-defined-timestamp-size records (types 9-11) are not handled:
+ * FORST_EUNSUPPORTED.  Synchronises the stream (record counts). */
+enum forst_wal_report_reason {
+  FORST_WAL_PARTIAL_RECORD_1 = 1,   /* "partial record without end(1)" */
+  FORST_WAL_PARTIAL_RECORD_2 = 2,   /* "partial record without end(2)" */
+  FORST_WAL_MISSING_START_1 = 3,    /* "missing start of fragmented record(1)" */
+  FORST_WAL_MISSING_START_2 = 4,    /* "missing start of fragmented record(2)" */
+  FORST_WAL_ERROR_IN_MIDDLE = 5,    /* "error in middle of record" */
+  FORST_WAL_CHECKSUM_MISMATCH = 6,  /* "checksum mismatch" */
+  FORST_WAL_BAD_RECORD_LENGTH = 7,  /* "bad record length" */
+  FORST_WAL_TRUNCATED_HEADER = 8,   /* "truncated header" */
+  FORST_WAL_TRAILING_DATA = 9,      /* "error reading trailing data" */
+  FORST_WAL_TRUNCATED_BODY = 10,    /* "truncated record body" */
+  FORST_WAL_UNKNOWN_TYPE = 11       /* "unknown record type %u" */
+};
+enum forst_wal_stop_reason {
+  FORST_WAL_STOP_EOF = 0,              /* kEof */
+  FORST_WAL_STOP_OLD_RECORD = 1,       /* kOldRecord (recycled log) */
+  FORST_WAL_STOP_TRUNCATED_HEADER = 2, /* kBadHeader at EOF */
+  FORST_WAL_STOP_TRUNCATED_BODY = 3,   /* kBadRecordLen at EOF */
+  FORST_WAL_STOP_RECYCLED_TAIL = 4     /* corrupt tail of a recycled log, tolerated */
+};
+typedef struct forst_wal_records {
+  uint64_t* offset;       /* Reader::LastRecordOffset of the record */
+  uint64_t* length;       /* logical record bytes */
+  uint64_t* hash;         /* XXH3_64bits(record) */
+  uint32_t* n_fragments;  /* physical records */
+} forst_wal_records;
+typedef struct forst_wal_reports {
+  uint64_t* offset;  /* reader position of the physical record / event */
+  uint64_t* bytes;   /* bytes dropped, as passed to Reporter::Corruption */
+  uint32_t* reason;  /* forst_wal_report_reason */
+  uint32_t* type;    /* record type (FORST_WAL_UNKNOWN_TYPE) */
+} forst_wal_reports;
+typedef struct forst_wal_recover_result {
+  uint64_t n_records, n_reports;
+  uint64_t n_physical;   /* physical records parsed by the walk */
+  uint64_t stop_offset;  /* reader position where reading ended */
+  uint32_t stop_reason;  /* forst_wal_stop_reason */
+  uint32_t truncated;    /* a count exceeded its capacity */
+  uint32_t unsupported;  /* types 9-11 present (the call returns FORST_EUNSUPPORTED) */
+  uint32_t reserved;
+} forst_wal_recover_result;
+int forst_wal_recover_batch(const uint8_t* log, uint64_t log_len, uint32_t log_number,
+                            int wal_recovery_mode, forst_wal_records records,
+                            uint64_t record_capacity, forst_wal_reports reports,
+                            uint64_t report_capacity, forst_wal_recover_result* result,
+                            void* stream);
+
 /* Host utility (no GPU call): the physical-record layout log::Writer::AddRecord
  * produces for logical records of the given lengths (db/log_writer.cc:65-160,
  * no compression): header offset, payload length and RecordType of every

@@ -198,3 +198,26 @@ def kv_verify(base, ko, ks, vo, vs, prot_bytes, chk, ops=None, seqs=None, cfs=No
                                      *[_p(a) for a in opt], prot_bytes, _p(chk), _p(comp),
                                      _p(ok), _p(bad), n, None))
     return comp, ok, int(bad[0])
+
+
+def wal_recover(log, log_number=0, mode=2, cap=None):
+    """forst_wal_recover_batch on the SIMT emulator: (records, reports, result)
+    with records = (offset, length, hash, n_fragments) arrays, reports =
+    (offset, bytes, reason, type) arrays"""
+    from forst_amd.engine import WalRecords, WalReports, WalRecoverResult, _recover_sig
+    L = lib()
+    _recover_sig(L)
+    log = _aligned(log)
+    cap = cap or max(64, log.nbytes // 7 + 2)
+    ro, rl, rh = (np.zeros(cap, np.uint64) for _ in range(3))
+    rn = np.zeros(cap, np.uint32)
+    po, pb = np.zeros(cap, np.uint64), np.zeros(cap, np.uint64)
+    pr, pt = np.zeros(cap, np.uint32), np.zeros(cap, np.uint32)
+    res = WalRecoverResult()
+    rc = L.forst_wal_recover_batch(_p(log), log.nbytes, log_number, mode,
+                                   WalRecords(_p(ro), _p(rl), _p(rh), _p(rn)), cap,
+                                   WalReports(_p(po), _p(pb), _p(pr), _p(pt)), cap,
+                                   ctypes.byref(res), None)
+    _chk(rc)
+    n, m = res.n_records, res.n_reports
+    return (ro[:n], rl[:n], rh[:n], rn[:n]), (po[:m], pb[:m], pr[:m], pt[:m]), res

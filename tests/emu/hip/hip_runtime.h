@@ -198,12 +198,20 @@ inline uint32_t atomicXor(uint32_t* p, uint32_t v) { return __atomic_fetch_xor(p
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
+inline uint32_t atomicOr(uint32_t* p, uint32_t v) { return __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
+inline unsigned long long atomicMin(unsigned long long* p, unsigned long long v) {
+  unsigned long long cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v < cur && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED)) {
+  }
+  return cur;
+}
 
 // stream-ordered allocation / copies: host memory, everything synchronous
 typedef void* hipMemPool_t;
 constexpr hipError_t hipErrorInvalidDevice = 101;
 constexpr hipError_t hipErrorInvalidValue = 1;
-enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2 };
+enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
 enum { hipMemAllocationTypePinned = 1, hipMemLocationTypeDevice = 1,
        hipMemPoolAttrReleaseThreshold = 4 };
 struct hipMemPoolProps {

@@ -208,6 +208,18 @@ def run_wal(steps, warmup, n_records=10_000_000):
         hs.append(time.perf_counter() - t0)
     assert hh.numel() == w.n_records
     t_h = float(np.median(hs))
+    # f2: the fused recovery pass (walk + CRC + fragment state machine +
+    # record XXH3, forst_wal_recover_batch), PIT recovery mode
+    rs = []
+    for _ in range(max(2, steps // 2)):
+        torch.cuda.synchronize()
+        t0 = time.perf_counter()
+        rec, rep, res = engine.wal_recover_batch(w.log, 0, engine.kPointInTimeRecovery,
+                                                 record_capacity=w.n_records + 1024)
+        torch.cuda.synchronize()
+        rs.append(time.perf_counter() - t0)
+    assert res.n_records == w.n_records and res.n_reports == 0
+    t_r = float(np.median(rs))
     t_w = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
     t_v = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
     payload = int(w.rec_lengths.astype(np.int64).sum())
@@ -225,7 +237,12 @@ def run_wal(steps, warmup, n_records=10_000_000):
            "writer_roofline_frac": round(alg_w / t_w / 1e9 / HBM_PEAK_GBS, 4),
            "record_xxh3_GiBps": round(payload / t_h / GIB, 1),
            "record_xxh3_ms": round(t_h * 1e3, 3),
-           "record_xxh3_roofline_frac": round(alg_h / t_h / 1e9 / HBM_PEAK_GBS, 4)}
+           "record_xxh3_roofline_frac": round(alg_h / t_h / 1e9 / HBM_PEAK_GBS, 4),
+           "recover_ms": round(t_r * 1e3, 3),
+           "recover_GiBps": round(w.total / t_r / GIB, 1),
+           "recover_desc": "forst_wal_recover_batch: header walk + every physical CRC + "
+                           "fragment state machine + XXH3 of every logical record, "
+                           "kPointInTimeRecovery, incl. its 3 stream synchronisations"}
     del w
     return out
 
@@ -327,6 +344,58 @@ def end_to_end_pcie(b, ctype, chunk_blocks=1 << 16):
     dt = time.perf_counter() - t0
     assert bool(oks.all())
     return b.checksummed_bytes / dt / GIB
+
+
+def host_paths(b, ctype, sample_blocks=1 << 18):
+    """Blocks starting in HOST memory through the in-process multi-device entry
+    (forst_block_verify_host: per device a host thread + stream + pinned
+    staging, 64 MiB windows double-buffered): pageable input (memcpy into
+    pinned staging), pinned input (DMA in place), and an SST-shaped file
+    mmap'd read-only and hipHostRegister'd (env/io_posix.cc:958).  PCIe-bound;
+    recorded in DESIGN.md, never the headline value."""
+    import tempfile
+    from forst_amd import hostpath
+
+    ns = min(b.n, sample_blocks)
+    offs = b.offsets[:ns].cpu().numpy().astype(np.uint64)
+    sizes = b.sizes[:ns].cpu().numpy().astype(np.uint32)
+    end = int(offs[-1]) + int(sizes[-1]) + 5
+    pageable = b.base[:end].cpu().numpy().copy()
+    nbytes = int(sizes.astype(np.int64).sum()) + ns
+    ndev = torch.cuda.device_count()
+    out = {"sample": f"first {ns} blocks ({nbytes / GIB:.2f} GiB checksummed)",
+           "devices": list(range(ndev))}
+
+    def rate(base, devices):
+        best = 1e30
+        for _ in range(3):
+            t0 = time.perf_counter()
+            _, _, ok, bad = hostpath.block_verify_host(ctype, base, offs, sizes, devices=devices)
+            best = min(best, time.perf_counter() - t0)
+            assert bad == 0
+        return round(nbytes / best / GIB, 2)
+
+    out["pageable_GiBps"] = rate(pageable, list(range(ndev)))
+    out["pageable_2streams_per_gpu_GiBps"] = rate(pageable, [d for d in range(ndev) for _ in (0, 1)])
+    pinned = torch.from_numpy(pageable).pin_memory()
+    out["pinned_GiBps"] = rate(pinned.numpy(), list(range(ndev)))
+    del pinned
+    d = os.environ.get("TMPDIR", tempfile.gettempdir())
+    path = os.path.join(d, f"forst_bench_{os.getpid()}.sst")
+    try:
+        pageable.tofile(path)
+        m = hostpath.MappedFile(path, register=True)
+        out["mmap_registered"] = m.registered
+        if not m.registered:
+            out["mmap_register_error"] = m.register_error
+        out["mmap_GiBps"] = rate(m, list(range(ndev)))
+        m.close()
+    except OSError as e:  # pragma: no cover
+        out["mmap_error"] = str(e)
+    finally:
+        if os.path.exists(path):
+            os.unlink(path)
+    return out
 
 
 def _norm_kernel(name):
@@ -435,6 +504,10 @@ def main():
             extras["end_to_end_pcie_GiBps"] = round(end_to_end_pcie(b, main_res["ctype"]), 2)
         except Exception as e:  # pragma: no cover
             extras["end_to_end_pcie_error"] = str(e)
+        try:
+            extras["host_memory_verify"] = host_paths(b, main_res["ctype"])
+        except Exception as e:  # pragma: no cover
+            extras["host_memory_verify_error"] = str(e)
     del b
     torch.cuda.empty_cache()
     if world == 1 and not args.no_extras and args.config == "C2":

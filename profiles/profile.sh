@@ -1,23 +1,29 @@
 #!/bin/bash
-# profiles/profile.sh -- rocprofv3 evidence for bench.py (run on the GPU box):
-#   1. --kernel-trace --stats          per-kernel durations (must agree with bench.py's HIP events)
-#   2. --pmc FETCH_SIZE                 HBM read traffic   (separate pass, guide §HBM)
-#   3. --pmc WRITE_SIZE                 HBM write traffic  (separate pass)
-# Usage: bash profiles/profile.sh <tag> [bench args...]
-# Writes raw output under gpurun_out/prof_<tag>/; summarise with
-#   python profiles/summarize.py <tag>
+# profiles/profile.sh -- rocprofv3 evidence for one bench.py config (GPU box):
+#   1. --kernel-trace --stats   per-kernel durations (compared with bench.py's HIP events)
+#   2. --pmc FETCH_SIZE         HBM read traffic   (separate pass, MI355X_MICROARCH.md §HBM)
+#   3. --pmc WRITE_SIZE         HBM write traffic  (separate pass)
+# Usage: bash profiles/profile.sh <tag> <config> [program args...]
+#   config = C2 | NS16 | NS16X | C3 | C4 (bench.py --config) or C5 (tools/prof_wal.py)
+# Raw output under gpurun_out/prof_<tag>_<config>/; summarise with
+#   python profiles/summarize.py <tag> <config>
 set -euo pipefail
-cd /tmp && export TMPDIR=/tmp
+export TMPDIR=/tmp
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
-TAG=${1:-r01}
-shift || true
-ARGS=${*:---steps 5 --warmup 2 --no-cpu-baseline --no-extras}
-OUT=gpurun_out/prof_${TAG}
+TAG=${1:-r02}
+CFG=${2:-C2}
+shift 2 || true
+if [ "$CFG" = "C5" ]; then
+  PROG="tools/prof_wal.py ${*:-}"
+else
+  PROG="bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-extras ${*:-}"
+fi
+OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p "$OUT"
 timeout -k 10 300 rocprofv3 --kernel-trace --stats -d "$OUT/trace" -o trace --output-format csv \
-  -- python3 bench.py $ARGS > "$OUT/trace.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \
-  -- python3 bench.py $ARGS > "$OUT/fetch.log" 2>&1
-timeout -k 10 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv \
-  -- python3 bench.py $ARGS > "$OUT/write.log" 2>&1
-echo "profile $TAG done"
+  -- python3 $PROG > "$OUT/trace.log" 2>&1
+timeout -s KILL 300 rocprofv3 --pmc FETCH_SIZE -d "$OUT/fetch" -o fetch --output-format csv \
+  -- python3 $PROG > "$OUT/fetch.log" 2>&1
+timeout -s KILL 300 rocprofv3 --pmc WRITE_SIZE -d "$OUT/write" -o write --output-format csv \
+  -- python3 $PROG > "$OUT/write.log" 2>&1
+echo "profile $TAG $CFG done"

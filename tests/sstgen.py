@@ -125,7 +125,8 @@ class SstWriter:
             builder.add(sep, full, delta)
             prev = (off, n)
 
-    def build(self, n_data=40, filter_block=True, partition_size=8, compress_type_bytes=None):
+    def build(self, n_data=40, filter_block=True, partition_size=8, compress_type_bytes=None,
+              external=False):
         entries = []
         k = 0
         for i in range(n_data):
@@ -171,6 +172,9 @@ class SstWriter:
         }
         if self.index_type == 2:
             props[b"rocksdb.index.partitions"] = varint(len(parts))
+        if external:  # SstFileWriter's collector (sst_file_writer_collectors.h): version 2, seqno 0
+            props[b"rocksdb.external_sst_file.version"] = struct.pack("<I", 2)
+            props[b"rocksdb.external_sst_file.global_seqno"] = struct.pack("<Q", 0)
         pbld = BlockBuilder(2**31 - 1)
         for name in sorted(props):
             pbld.add(name, props[name])

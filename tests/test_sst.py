@@ -273,3 +273,54 @@ def test_verify_files_many():
     rs = sst.verify_files(files)
     assert all(r.status == 0 for r in rs), [r.message for r in rs if r.status]
     assert all(r.data_blocks == 300 for r in rs)
+
+
+@pytest.mark.gpu
+def test_ingested_global_seqno_rewrite_still_verifies():
+    """IngestExternalFile(write_global_seqno=true) rewrites the 8-byte
+    global_seqno property value after the properties block checksum was taken;
+    the reference retries that checksum with the value zeroed
+    (ReadTablePropertiesHelper, meta_blocks.cc:401-417)"""
+    name = "/db/000099.sst"
+    for fv, ct in ((5, 1), (6, 4)):
+        w, f = make(fv, ct, 0, 1, external=True)
+        po, pn = blocks_of(w, "properties")[0]
+        props = sst.properties(f[po:po + pn])
+        at = po + props.global_seqno_value_offset
+        assert props.global_seqno_value_offset > 0
+        b = bytearray(f)
+        b[at:at + 8] = struct.pack("<Q", 123456789)  # the ingested file's global seqno
+        r = sst.verify_file(bytes(b), file_name=name)
+        assert r.status == 0, r.message
+        b[po + 2] ^= 0x40  # any other byte of the block still fails
+        r = sst.verify_file(bytes(b), file_name=name)
+        assert r.status == 2 and b"block checksum mismatch" in r.message
+
+
+@pytest.mark.gpu
+def test_footer_checked_reserved_bytes_after_checksum():
+    """fv6: the footer checksum is compared before the 8 checked reserved
+    bytes (format.cc:421-448): a flip there is a checksum mismatch; non-zero
+    reserved bytes under a valid checksum are NotSupported"""
+    name = "x.sst"
+    w, f = make(6, 1, 0, 1)
+    b = bytearray(f)
+    b[-20] ^= 1
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.message.decode() == f"Corruption: Footer at {w.footer_offset} checksum mismatch in {name}"
+    ft = bytearray(b[-53:])
+    ft[5:9] = bytes(4)
+    c = O.compute_builtin_checksum(1, bytes(ft))
+    c = (c + O.checksum_modifier_for_context(w.bcc, w.footer_offset)) & 0xFFFFFFFF
+    b[-48:-44] = struct.pack("<I", c)
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.status == 3
+    assert r.message.decode() == ("Not implemented: File uses a future feature not supported "
+                                  f"in this version in {name}")
+
+
+@pytest.mark.gpu
+def test_short_file_message():
+    r = sst.verify_file(bytes(10), file_name="/db/000001.sst")
+    assert r.message.decode() == ("Corruption: file is too short (10 bytes) to be an sstable: "
+                                  "/db/000001.sst")

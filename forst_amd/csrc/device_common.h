@@ -1,5 +1,10 @@
 // forst_amd/csrc/device_common.h -- gfx950 device helpers shared by the kernels.
 #pragma once
+// register budget of a kernel as resident waves per SIMD (the SIMT emulator,
+// tests/emu, defines it away)
+#ifndef FORST_WAVES_PER_EU
+#define FORST_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
 #include <hip/hip_runtime.h>
 
 #include <cstdint>

@@ -114,6 +114,10 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a,
                                 hipStream_t stream, const char** kernel_name);
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
+// XXH3_64bits of WAL logical records read in place across their fragments
+// (xxh3.hip xxh3_frag_kernel): offsets = first payload byte, sizes = record
+// length, init_crcs = frag_info (hs | j_last << 8); needs base_len >= 4096
+hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_noop_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
 // kxxHash (x64 = false, XXH32) / kxxHash64 (x64 = true, Lower32 of XXH64)

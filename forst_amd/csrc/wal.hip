@@ -36,6 +36,7 @@
 #include "device_common.h"
 #include "engine.h"
 #include "scan_common.h"
+#include "wal_hash.h"
 
 namespace forst {
 
@@ -253,9 +254,9 @@ __global__ void __launch_bounds__(kTile) wal_rec_finish_kernel(WalArgs a, const 
 // ---- a14: XXH3 of logical records (log_reader.cc:95-165) --------------------
 // A logical record is a kFullType fragment, or kFirstType + kMiddleType* +
 // kLastType; the reader hashes it with XXH3_64bits (full) or the streaming API
-// over the fragments (= XXH3_64bits of their concatenation).  Full records are
-// hashed in place; the fragments of multi-fragment records are gathered into
-// one contiguous scratch run per record first.
+// over the fragments (= XXH3_64bits of their concatenation).  wal_hash.h hashes
+// them in place across the fragment headers (a writer's layout) or from a
+// gathered copy (anything else).
 
 __device__ __forceinline__ uint32_t norm_type(uint32_t t) {  // recyclable -> legacy
   return (t >= 5 && t <= 8) ? t - 4 : t;
@@ -292,137 +293,40 @@ __global__ void __launch_bounds__(kTile) rec_start_kernel(WalArgs a, uint64_t* s
   start[i] = f.ok && (f.type == 1 || f.type == 2) ? 1 : 0;
 }
 
-// per logical record: first fragment and kind; per fragment: gathered length
-// (payload bytes of fragments owned by a kFirstType record, else 0)
+// per logical record: first fragment and kind
 __global__ void __launch_bounds__(kTile) rec_owner_kernel(WalArgs a, const uint64_t* start,
                                                           const uint64_t* lid_excl,
-                                                          uint64_t* first_phys, uint8_t* kind,
-                                                          uint64_t* glen) {
+                                                          uint64_t* first_phys, uint8_t* kind) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   if (i >= a.n_records) return;
-  const FragInfo f = frag_info(a, i);
   if (start[i]) {
     first_phys[lid_excl[i]] = i;
-    kind[lid_excl[i]] = static_cast<uint8_t>(f.type);
-  }
-  // the owner is the last start at or before i (lid_excl + start - 1)
-  const uint64_t owned = lid_excl[i] + start[i];
-  // provisional: every non-full fragment with an owner; rec_orphan_kernel
-  // clears the ones whose owner turns out to be a kFullType record
-  glen[i] = owned > 0 && f.ok && f.type != 1 ? f.len : 0;
-}
-
-// orphans after a kFullType owner are not gathered
-__global__ void __launch_bounds__(kTile) rec_orphan_kernel(WalArgs a, const uint64_t* start,
-                                                           const uint64_t* lid_excl,
-                                                           const uint8_t* kind, uint64_t* glen) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
-  if (i >= a.n_records) return;
-  const uint64_t owned = lid_excl[i] + start[i];
-  if (owned == 0 || kind[owned - 1] != 2) glen[i] = 0;
-}
-
-// gather fragment payloads: one workgroup per fragment, one destination-
-// aligned dword per lane (source realigned from two aligned dwords with
-// v_alignbyte); the partial dwords at either end are byte stores, since the
-// neighbouring fragments' bytes are written by other workgroups
-__device__ __forceinline__ uint32_t ld_any4(const uint8_t* p, const uint8_t* lo,
-                                            const uint8_t* hi) {
-  const uint64_t pa = reinterpret_cast<uint64_t>(p);
-  const uint8_t* q = reinterpret_cast<const uint8_t*>(pa & ~3ull);
-  const uint32_t m = static_cast<uint32_t>(pa & 3);
-  if (q < lo || q + 8 > hi) {  // near the log edges: byte loads
-    uint32_t v = 0;
-    for (uint32_t k = 0; k < 4; ++k)
-      if (p + k >= lo && p + k < hi) v |= static_cast<uint32_t>(p[k]) << (8 * k);
-    return v;
-  }
-  const uint32_t w0 = *reinterpret_cast<const uint32_t*>(q);
-  const uint32_t w1 = *reinterpret_cast<const uint32_t*>(q + 4);
-  return m ? __builtin_amdgcn_alignbyte(w1, w0, m) : w0;
-}
-
-// 16 source bytes at any alignment: a dword-aligned 16-byte load plus one
-// dword, realigned with v_alignbyte
-__device__ __forceinline__ u32x4a4 ld_any16(const uint8_t* p, const uint8_t* lo, const uint8_t* hi) {
-  const uint64_t pa = reinterpret_cast<uint64_t>(p);
-  const uint8_t* q = reinterpret_cast<const uint8_t*>(pa & ~3ull);
-  const uint32_t m = static_cast<uint32_t>(pa & 3);
-  u32x4a4 r;
-  if (q < lo || q + 20 > hi) {
-    r.x = ld_any4(p, lo, hi);
-    r.y = ld_any4(p + 4, lo, hi);
-    r.z = ld_any4(p + 8, lo, hi);
-    r.w = ld_any4(p + 12, lo, hi);
-    return r;
-  }
-  const u32x4a4 v = *reinterpret_cast<const u32x4a4*>(q);
-  const uint32_t e = *reinterpret_cast<const uint32_t*>(q + 16);
-  if (m == 0) return v;
-  r.x = __builtin_amdgcn_alignbyte(v.y, v.x, m);
-  r.y = __builtin_amdgcn_alignbyte(v.z, v.y, m);
-  r.z = __builtin_amdgcn_alignbyte(v.w, v.z, m);
-  r.w = __builtin_amdgcn_alignbyte(e, v.w, m);
-  return r;
-}
-
-__global__ void __launch_bounds__(kTile) rec_gather_kernel(WalArgs a, const uint64_t* glen,
-                                                           const uint64_t* goff, uint8_t* dst) {
-  const uint8_t* lo = a.log;
-  const uint8_t* hi = a.log + a.log_len;
-  for (uint64_t i = blockIdx.x; i < a.n_records; i += gridDim.x) {
-    const uint64_t n = glen[i];
-    if (n == 0) continue;
-    const FragInfo f = frag_info(a, i);
-    const uint8_t* src = a.log + f.off;
-    uint8_t* d = dst + goff[i];
-    const uint64_t da = reinterpret_cast<uint64_t>(d);
-    const uint32_t head = static_cast<uint32_t>((16 - (da & 15)) & 15);  // to 16 B alignment
-    const uint64_t h = head < n ? head : n;
-    if (threadIdx.x < h) d[threadIdx.x] = src[threadIdx.x];
-    const uint64_t body = (n - h) & ~15ull;
-    u32x4a4* d16 = reinterpret_cast<u32x4a4*>(d + h);
-    for (uint64_t k = threadIdx.x; k < body / 16; k += kTile)
-      d16[k] = ld_any16(src + h + 16 * k, lo, hi);
-    const uint64_t tail = n - h - body;
-    if (threadIdx.x < tail) d[h + body + threadIdx.x] = src[h + body + threadIdx.x];
+    kind[lid_excl[i]] = static_cast<uint8_t>(frag_info(a, i).type);
   }
 }
 
-// descriptors per logical record: full records in place (batch A, base =
-// log), gathered records in scratch (batch B); the other batch gets length 0
-__global__ void __launch_bounds__(kTile) rec_desc_kernel(WalArgs a, uint64_t n_logical,
-                                                         const uint64_t* first_phys,
-                                                         const uint8_t* kind,
-                                                         const uint64_t* goff, uint64_t gtotal,
-                                                         uint64_t* a_off, uint32_t* a_len,
-                                                         uint64_t* b_off, uint32_t* b_len) {
+// the fragments of logical record j (wal_hash.h accessor): a kFullType
+// record is its start fragment; a kFirstType record owns every valid
+// fragment up to the next start
+struct A14Frags {
+  WalArgs a;
+  const uint64_t* first;
+  const uint8_t* kind;
+  uint64_t n_logical;
+  __device__ uint64_t begin(uint64_t j) const { return first[j]; }
+  __device__ uint64_t end(uint64_t j) const {
+    if (kind[j] == 1) return first[j] + 1;
+    return j + 1 < n_logical ? first[j + 1] : a.n_records;
+  }
+  __device__ uint64_t header(uint64_t q) const { return a.header_offsets[q]; }
+  __device__ bool use(uint64_t q) const { return frag_info(a, q).ok; }
+};
+
+__global__ void __launch_bounds__(kTile) rec_first_kernel(uint64_t n_logical,
+                                                          const uint64_t* first_phys,
+                                                          uint64_t* out_first) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
-  if (j >= n_logical) return;
-  const uint64_t i = first_phys[j];
-  const FragInfo f = frag_info(a, i);
-  a_off[j] = 0;
-  a_len[j] = 0;
-  b_off[j] = 0;
-  b_len[j] = 0;
-  if (kind[j] == 1) {
-    a_off[j] = f.off;
-    a_len[j] = f.len;
-  } else {
-    const uint64_t end = j + 1 < n_logical ? goff[first_phys[j + 1]] : gtotal;
-    b_off[j] = goff[i];
-    b_len[j] = static_cast<uint32_t>(end - goff[i]);
-  }
-}
-
-__global__ void __launch_bounds__(kTile) rec_select_kernel(uint64_t n_logical, const uint8_t* kind,
-                                                           const uint64_t* ha, const uint64_t* hb,
-                                                           const uint64_t* first_phys,
-                                                           uint64_t* out, uint64_t* out_first) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
-  if (j >= n_logical) return;
-  out[j] = kind[j] == 1 ? ha[j] : hb[j];
-  if (out_first) out_first[j] = first_phys[j];
+  if (j < n_logical) out_first[j] = first_phys[j];
 }
 
 #ifdef FORST_DIAG
@@ -634,83 +538,39 @@ hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out
   if (a.n_records == 0) return hipSuccess;
   const uint64_t n = a.n_records, nt = (n + kTile - 1) / kTile;
   const dim3 grid(static_cast<uint32_t>(nt));
-  // scratch: start, lid, glen, goff (u64 x n), first_phys (u64 x n), kind (u8 x n),
-  // tile sums (u64 x nt + 1), hashes A/B (u64 x n), descriptors (12 B x n x 2)
-  const size_t s8 = up256(8 * n), s1 = up256(n), st = up256(8 * (nt + 1)), s4 = up256(4 * n);
+  // scratch: start, lid, first_phys (u64 x n), kind (u8 x n), tile sums
+  const size_t s8 = up256(8 * n), s1 = up256(n), st = up256(8 * (nt + 2));
   void* scratch = nullptr;
-  hipError_t e = scratch_alloc(&scratch, 7 * s8 + s1 + st + 2 * s8 + 2 * s4, stream);
+  hipError_t e = scratch_alloc(&scratch, 3 * s8 + s1 + st, stream);
   if (e != hipSuccess) return e;
   uint8_t* p = static_cast<uint8_t*>(scratch);
   uint64_t* start = reinterpret_cast<uint64_t*>(p);
   uint64_t* lid = reinterpret_cast<uint64_t*>(p + s8);
-  uint64_t* glen = reinterpret_cast<uint64_t*>(p + 2 * s8);
-  uint64_t* goff = reinterpret_cast<uint64_t*>(p + 3 * s8);
-  uint64_t* first = reinterpret_cast<uint64_t*>(p + 4 * s8);
-  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 5 * s8);
-  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 6 * s8);
-  uint8_t* kind = p + 7 * s8;
-  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 7 * s8 + s1);
-  uint64_t* a_off = reinterpret_cast<uint64_t*>(p + 7 * s8 + s1 + st);
-  uint64_t* b_off = reinterpret_cast<uint64_t*>(p + 8 * s8 + s1 + st);
-  uint32_t* a_len = reinterpret_cast<uint32_t*>(p + 9 * s8 + s1 + st);
-  uint32_t* b_len = reinterpret_cast<uint32_t*>(p + 9 * s8 + s1 + st + s4);
-  auto scan = [&](const uint64_t* in, uint64_t* outx) {
-    hipLaunchKernelGGL(scan_tiles_kernel, grid, dim3(kTile), 0, stream, in, n, tiles);
-    hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanThreads), 0, stream, tiles, nt);
-    hipLaunchKernelGGL(scan_apply_kernel, grid, dim3(kTile), 0, stream, in, n, tiles, outx);
-  };
+  uint64_t* first = reinterpret_cast<uint64_t*>(p + 2 * s8);
+  uint8_t* kind = p + 3 * s8;
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 3 * s8 + s1);
   hipLaunchKernelGGL(rec_start_kernel, grid, dim3(kTile), 0, stream, a, start);
-  scan(start, lid);
-  uint64_t n_logical = 0, gtotal = 0;
-  if ((e = hipMemcpyAsync(&n_logical, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess) {
-    (void)scratch_free(scratch, stream);
-    return e;
-  }
-  hipLaunchKernelGGL(rec_owner_kernel, grid, dim3(kTile), 0, stream, a, start, lid, first, kind,
-                     glen);
-  hipLaunchKernelGGL(rec_orphan_kernel, grid, dim3(kTile), 0, stream, a, start, lid, kind, glen);
-  scan(glen, goff);
-  if ((e = hipMemcpyAsync(&gtotal, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+  scan_u64(start, n, tiles, lid, stream);
+  hipLaunchKernelGGL(rec_owner_kernel, grid, dim3(kTile), 0, stream, a, start, lid, first, kind);
+  uint64_t n_logical = 0;
+  if ((e = hipMemcpyAsync(&n_logical, tiles + (n + kScanTile - 1) / kScanTile, 8,
+                          hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess) {
     (void)scratch_free(scratch, stream);
     return e;
   }
-  void* gbuf = nullptr;
-  if ((e = scratch_alloc(&gbuf, up256(gtotal + 256), stream)) != hipSuccess) {
-    (void)scratch_free(scratch, stream);
-    return e;
-  }
-  uint8_t* g = static_cast<uint8_t*>(gbuf);
-  const uint32_t ggrid = static_cast<uint32_t>(n < 65536 ? n : 65536);
-  hipLaunchKernelGGL(rec_gather_kernel, dim3(ggrid), dim3(kTile), 0, stream, a, glen, goff, g);
-  const dim3 lgrid(static_cast<uint32_t>((n_logical + kTile - 1) / kTile));
   if (n_logical) {
-    hipLaunchKernelGGL(rec_desc_kernel, lgrid, dim3(kTile), 0, stream, a, n_logical, first, kind,
-                       goff, gtotal, a_off, a_len, b_off, b_len);
-    BlockArgs ba{};
-    ba.base = a.log;
-    ba.base_len = a.log_len;
-    ba.offsets = a_off;
-    ba.sizes = a_len;
-    ba.out64 = ha;
-    ba.n = n_logical;
-    e = launch_xxh3_blocks(kModeRaw, ba, stream, name);
-    if (e == hipSuccess) {
-      BlockArgs bb = ba;
-      bb.base = g;
-      bb.base_len = up256(gtotal + 256);
-      bb.offsets = b_off;
-      bb.sizes = b_len;
-      bb.out64 = hb;
-      e = launch_xxh3_blocks(kModeRaw, bb, stream, name);
+    const A14Frags f{a, first, kind, n_logical};
+    e = hash_logical_records(a.log, a.log_len, f, n_logical, out, stream, name);
+    if (e == hipSuccess && out_first) {
+      hipLaunchKernelGGL(rec_first_kernel, dim3(static_cast<uint32_t>((n_logical + kTile - 1) / kTile)),
+                         dim3(kTile), 0, stream, n_logical, first, out_first);
+      e = hipGetLastError();
     }
-    hipLaunchKernelGGL(rec_select_kernel, lgrid, dim3(kTile), 0, stream, n_logical, kind, ha, hb,
-                       first, out, out_first);
   }
-  if (e == hipSuccess) e = hipGetLastError();
   *n_logical_host = n_logical;
-  const hipError_t f1 = scratch_free(gbuf, stream), f2 = scratch_free(scratch, stream);
-  return e != hipSuccess ? e : f1 != hipSuccess ? f1 : f2;
+  const hipError_t f1 = scratch_free(scratch, stream);
+  return e != hipSuccess ? e : f1;
 }
 
 }  // namespace forst

@@ -1,0 +1,200 @@
+// forst_amd/csrc/wal_hash.h -- XXH3_64bits of WAL logical records
+// (log::Reader::ReadRecord's record checksum, db/log_reader.cc:95-165), shared
+// by forst_wal_record_xxh3_batch (wal.hip) and forst_wal_recover_batch
+// (wal_recover.hip).
+//
+// A logical record is a run of physical records (fragments).  Records laid
+// out the way log::Writer::AddRecord writes them (db/log_writer.cc:65-160:
+// every fragment but the last fills its log block, the next one starts right
+// after the next block's header) are hashed IN PLACE by xxh3_frag_kernel
+// (xxh3.hip), which reads across the header holes; only the rest -- records
+// of <= 240 bytes that span a block boundary, records whose last fragment is
+// under 64 bytes (the last stripe would straddle), fragment runs a writer
+// never produces -- are gathered into scratch (one workgroup per record) and
+// hashed there.  The accessor F describes a pipeline's fragments:
+//   F::begin(j), F::end(j)   fragment range of logical record j
+//   F::header(q)             log offset of fragment q's header
+//   F::use(q)                false: fragment q is not part of the record (the
+//                            record is then gathered without it)
+#pragma once
+#include <hip/hip_runtime.h>
+
+#include <cstdint>
+
+#include "device_common.h"
+#include "engine.h"
+#include "scan_common.h"
+
+namespace forst {
+namespace {
+
+constexpr uint32_t kWhBlock = 32768;  // db/log_format.h:45
+constexpr uint32_t kWhLanes = 256;
+
+__device__ __forceinline__ uint32_t wh_hs(const uint8_t* log, uint64_t hdr) {
+  const uint32_t t = log[hdr + 6];  // recyclable types: db/log_format.h:20-41
+  return ((t >= 5 && t <= 8) || t == 11) ? 11u : 7u;
+}
+__device__ __forceinline__ uint32_t wh_len(const uint8_t* log, uint64_t hdr) {
+  return static_cast<uint32_t>(log[hdr + 4]) | (static_cast<uint32_t>(log[hdr + 5]) << 8);
+}
+
+// per logical record: in-place descriptor (p0, len, info = hs | j_last << 8)
+// for the frag kernel, or glen = len when it must be gathered (its frag
+// descriptor then has length 0)
+template <class F>
+__global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F f, uint64_t n,
+                                                           uint64_t* p0, uint32_t* len,
+                                                           uint32_t* info, uint64_t* glen) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t b = f.begin(j), e = f.end(j);
+  uint64_t total = 0;
+  bool regular = true;
+  uint64_t start = 0;   // payload offset of the first non-empty fragment
+  uint32_t hs0 = 0, nz = 0, last_len = 0;
+  uint64_t prev_end = 0;
+  for (uint64_t q = b; q < e; ++q) {
+    if (!f.use(q)) {
+      regular = false;
+      continue;
+    }
+    const uint64_t h = f.header(q);
+    const uint32_t hs = wh_hs(log, h), l = wh_len(log, h);
+    if (q > b && (h != prev_end || (h & (kWhBlock - 1)) != 0)) regular = false;
+    if (q + 1 < e && ((h + hs + l) & (kWhBlock - 1)) != 0) regular = false;  // fills its block
+    if (q == b) hs0 = hs;
+    if (hs != hs0) regular = false;
+    if (l && !nz++) start = h + hs;
+    total += l;
+    last_len = l;
+    prev_end = h + hs + l;
+  }
+  const bool multi = nz > 1;
+  if (multi && (total <= 240 || last_len < 64)) regular = false;
+  if (total > 0xffffffffull) regular = false;
+  if (nz == 0) start = e > b && f.use(b) ? f.header(b) + wh_hs(log, f.header(b)) : 0;
+  p0[j] = start;
+  len[j] = regular ? static_cast<uint32_t>(total) : 0u;
+  info[j] = multi ? (hs0 | ((nz - 1) << 8)) : 0u;
+  glen[j] = regular ? 0 : total;
+}
+
+// one workgroup per gathered record: its fragments back to back at dst + goff[j]
+template <class F>
+__global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log, F f, uint64_t n,
+                                                             const uint64_t* glen,
+                                                             const uint64_t* goff, uint8_t* dst) {
+  for (uint64_t j = blockIdx.x; j < n; j += gridDim.x) {
+    if (glen[j] == 0) continue;
+    uint8_t* d = dst + goff[j];
+    for (uint64_t q = f.begin(j); q < f.end(j); ++q) {
+      if (!f.use(q)) continue;
+      const uint64_t h = f.header(q);
+      const uint8_t* src = log + h + wh_hs(log, h);
+      const uint32_t l = wh_len(log, h);
+      for (uint32_t x = threadIdx.x; x < l; x += kWhLanes) d[x] = src[x];
+      d += l;
+    }
+  }
+}
+
+__global__ void __launch_bounds__(kWhLanes) wh_gdesc_kernel(const uint64_t* glen,
+                                                            const uint64_t* goff, uint64_t n,
+                                                            uint64_t* off, uint32_t* len) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (j >= n) return;
+  off[j] = goff[j];
+  len[j] = static_cast<uint32_t>(glen[j]);
+}
+
+__global__ void __launch_bounds__(kWhLanes) wh_select_kernel(const uint64_t* glen,
+                                                             const uint64_t* ha,
+                                                             const uint64_t* hb, uint64_t n,
+                                                             uint64_t* out) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (j >= n) return;
+  out[j] = glen[j] ? hb[j] : ha[j];
+}
+
+inline size_t wh_up256(size_t b) { return (b + 255) & ~size_t(255); }
+inline dim3 wh_grid(uint64_t n) {
+  const uint64_t g = (n + kWhLanes - 1) / kWhLanes;
+  return dim3(static_cast<uint32_t>(g ? g : 1));
+}
+
+// out[j] = XXH3_64bits of logical record j (device array).  Synchronises the
+// stream once (the gathered byte total sizes the scratch).
+template <class F>
+hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f, uint64_t n,
+                                uint64_t* out, hipStream_t st, const char** name) {
+  if (n == 0) return hipSuccess;
+  const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * (n / kScanTile + 2));
+  void* scratch = nullptr;
+  hipError_t e = scratch_alloc(&scratch, 7 * s8 + 3 * s4 + st8, st);
+  if (e != hipSuccess) return e;
+  uint8_t* p = static_cast<uint8_t*>(scratch);
+  uint64_t* p0 = reinterpret_cast<uint64_t*>(p);
+  uint64_t* glen = reinterpret_cast<uint64_t*>(p + s8);
+  uint64_t* goff = reinterpret_cast<uint64_t*>(p + 2 * s8);
+  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 3 * s8);
+  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 4 * s8);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(p + 5 * s8);
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 7 * s8 + 3 * s4);
+  uint32_t* len = reinterpret_cast<uint32_t*>(p + 7 * s8);
+  uint32_t* info = reinterpret_cast<uint32_t*>(p + 7 * s8 + s4);
+  uint32_t* blen = reinterpret_cast<uint32_t*>(p + 7 * s8 + 2 * s4);
+  hipLaunchKernelGGL(wh_prep_kernel<F>, wh_grid(n), dim3(kWhLanes), 0, st, log, f, n, p0, len,
+                     info, glen);
+  scan_u64(glen, n, tiles, goff, st);
+  uint64_t gtotal = 0;
+  if ((e = hipMemcpyAsync(&gtotal, tiles + (n + kScanTile - 1) / kScanTile, 8,
+                          hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (e = hipStreamSynchronize(st)) != hipSuccess) {
+    (void)scratch_free(scratch, st);
+    return e;
+  }
+  // in place across the fragments (every record; gathered ones have length 0)
+  BlockArgs fa{};
+  fa.base = log;
+  fa.base_len = log_len;
+  fa.offsets = p0;
+  fa.sizes = len;
+  fa.init_crcs = info;
+  fa.out64 = ha;
+  fa.n = n;
+  e = log_len >= 4096 ? launch_xxh3_frag(fa, st, name) : launch_xxh3_blocks(kModeRaw, fa, st, name);
+  void* gbuf = nullptr;
+  if (e == hipSuccess && gtotal) {
+    e = scratch_alloc(&gbuf, wh_up256(gtotal + 4096), st);
+    if (e == hipSuccess) {
+      const uint32_t gg = static_cast<uint32_t>(n < 65536 ? n : 65536);
+      hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, st, log, f, n, glen,
+                         goff, static_cast<uint8_t*>(gbuf));
+      hipLaunchKernelGGL(wh_gdesc_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, goff, n, boff,
+                         blen);
+      BlockArgs ga = fa;
+      ga.base = static_cast<uint8_t*>(gbuf);
+      ga.base_len = wh_up256(gtotal + 4096);
+      ga.offsets = boff;
+      ga.sizes = blen;
+      ga.init_crcs = nullptr;
+      ga.out64 = hb;
+      const char* gname = nullptr;
+      e = launch_xxh3_blocks(kModeRaw, ga, st, &gname);
+    }
+  }
+  if (e == hipSuccess) {
+    if (gtotal) {
+      hipLaunchKernelGGL(wh_select_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, ha, hb, n, out);
+      e = hipGetLastError();
+    } else {
+      e = hipMemcpyAsync(out, ha, 8 * n, hipMemcpyDeviceToDevice, st);
+    }
+  }
+  const hipError_t f1 = scratch_free(gbuf, st), f2 = scratch_free(scratch, st);
+  return e != hipSuccess ? e : f1 != hipSuccess ? f1 : f2;
+}
+
+}  // namespace
+}  // namespace forst

@@ -32,8 +32,9 @@
 //            unfinished First segment reports what the reader reports there
 //   emit     logical records (first fragment = segment head) and reports in
 //            reader order                               (one sync: counts)
-//   hash     XXH3_64bits of every logical record: single fragments in place,
-//            multi-fragment records gathered into scratch (wal.hip's gather)
+//   hash     XXH3_64bits of every logical record (wal_hash.h): in place
+//            across the fragment headers when laid out as a writer lays them
+//            out, else from a gathered copy             (one sync: gathered bytes)
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
@@ -43,6 +44,7 @@
 #include "device_common.h"
 #include "engine.h"
 #include "scan_common.h"
+#include "wal_hash.h"
 
 namespace forst {
 namespace {
@@ -462,69 +464,17 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
   }
 }
 
-// ---- hashing: single fragments in place, multi-fragment records gathered ----
-__device__ __forceinline__ uint64_t payload_off(const uint8_t* log, uint64_t hdr) {
-  return hdr + (recyclable_type(log[hdr + 6]) ? kLogRHdr : kLogHdr);
-}
-
-// per logical record: in-place descriptor (single fragment) or gathered size
-__global__ void __launch_bounds__(kLanes) rw_hash_desc_kernel(
-    RecoverArgs a, Tokens t, const uint64_t* it_off, const uint64_t* head_tok,
-    const uint32_t* n_frag, const uint64_t* length, uint64_t n_rec, uint64_t* a_off,
-    uint32_t* a_len, uint64_t* glen) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (j >= n_rec) return;
-  const uint64_t h = head_tok[j];
-  if (n_frag[j] == 1) {
-    a_off[j] = payload_off(a.log, it_off[t.item[h]]);
-    a_len[j] = static_cast<uint32_t>(length[j]);
-    glen[j] = 0;
-  } else {
-    a_off[j] = 0;
-    a_len[j] = 0;
-    glen[j] = length[j];
-  }
-}
-
-// one workgroup per multi-fragment record: its fragments copied back to back
-// into g + goff[j] (byte-granular ends, dword body)
-__global__ void __launch_bounds__(kLanes) rw_gather_kernel(RecoverArgs a, Tokens t,
-                                                           const uint64_t* it_off,
-                                                           const uint64_t* head_tok,
-                                                           const uint32_t* n_frag,
-                                                           const uint64_t* glen,
-                                                           const uint64_t* goff, uint64_t n_rec,
-                                                           uint8_t* g) {
-  for (uint64_t j = blockIdx.x; j < n_rec; j += gridDim.x) {
-    if (glen[j] == 0) continue;
-    uint8_t* d = g + goff[j];
-    const uint64_t h = head_tok[j];
-    for (uint32_t q = 0; q < n_frag[j]; ++q) {
-      const uint64_t ti = h + q;
-      const uint8_t* src = a.log + payload_off(a.log, it_off[t.item[ti]]);
-      const uint32_t len = t.len[ti];
-      for (uint32_t x = threadIdx.x; x < len; x += kLanes) d[x] = src[x];
-      d += len;
-    }
-  }
-}
-
-__global__ void __launch_bounds__(kLanes) rw_gdesc_kernel(const uint64_t* glen,
-                                                          const uint64_t* goff, uint64_t n_rec,
-                                                          uint64_t* b_off, uint32_t* b_len) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (j >= n_rec) return;
-  b_off[j] = goff[j];
-  b_len[j] = static_cast<uint32_t>(glen[j]);
-}
-
-__global__ void __launch_bounds__(kLanes) rw_select_kernel(const uint32_t* n_frag,
-                                                           const uint64_t* ha, const uint64_t* hb,
-                                                           uint64_t n_rec, uint64_t* out) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (j >= n_rec) return;
-  out[j] = n_frag[j] == 1 ? ha[j] : hb[j];
-}
+// ---- hashing (wal_hash.h): record j = tokens head_tok[j] .. + n_frag[j] - 1 --
+struct RecFrags {
+  const uint64_t* head_tok;
+  const uint32_t* n_frag;
+  const uint64_t* item;
+  const uint64_t* it_off;
+  __device__ uint64_t begin(uint64_t j) const { return head_tok[j]; }
+  __device__ uint64_t end(uint64_t j) const { return head_tok[j] + n_frag[j]; }
+  __device__ uint64_t header(uint64_t q) const { return it_off[item[q]]; }
+  __device__ bool use(uint64_t) const { return true; }
+};
 
 __global__ void rw_recycled_kernel(RecoverArgs a, uint32_t* flag) {
   // Reader::recycled_: the first header of the file has a recyclable type
@@ -710,32 +660,13 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   res->stop_offset = last_pos;
   res->truncated = (n_rec > rec_cap || n_rp > rep_cap) ? 1u : 0u;
   // records + reports at their positions, then the hashes
-  void* s3 = nullptr;
   const uint64_t nr = n_rec;
-  const size_t p3 = up256(8 * nr) + up256(8 * nr) * 6 + up256(4 * nr) * 2 + up256(8 * (nr / kScanTile + 2)) + 4096;
-  if ((e = scratch_alloc(&s3, p3, st)) != hipSuccess) {
-    (void)scratch_free(s2, st);
-    (void)scratch_free(s1, st);
-    return e;
-  }
-  Arena A3{static_cast<uint8_t*>(s3), 0};
-  uint64_t* head_tok = A3.take<uint64_t>(nr);
-  uint64_t* a_off = A3.take<uint64_t>(nr);
-  uint64_t* glen = A3.take<uint64_t>(nr);
-  uint64_t* goff = A3.take<uint64_t>(nr);
-  uint64_t* ha = A3.take<uint64_t>(nr);
-  uint64_t* hb = A3.take<uint64_t>(nr);
-  uint64_t* b_off = A3.take<uint64_t>(nr);
-  uint32_t* a_len = A3.take<uint32_t>(nr);
-  uint32_t* b_len = A3.take<uint32_t>(nr);
-  uint64_t* tiles3 = A3.take<uint64_t>(nr / kScanTile + 2);
   // full record list in scratch first (the caller's capacity may be short)
   forst_wal_records full{};
-  uint64_t* r_len = nullptr;
+  uint64_t* head_tok = nullptr;
   uint32_t* r_nf = nullptr;
   void* s4 = nullptr;
-  if ((e = scratch_alloc(&s4, up256(8 * nr) * 3 + up256(4 * nr), st)) != hipSuccess) {
-    (void)scratch_free(s3, st);
+  if ((e = scratch_alloc(&s4, up256(8 * nr) * 4 + up256(4 * nr), st)) != hipSuccess) {
     (void)scratch_free(s2, st);
     (void)scratch_free(s1, st);
     return e;
@@ -743,52 +674,16 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   {
     Arena A4{static_cast<uint8_t*>(s4), 0};
     full.offset = A4.take<uint64_t>(nr);
-    full.length = r_len = A4.take<uint64_t>(nr);
+    full.length = A4.take<uint64_t>(nr);
     full.hash = A4.take<uint64_t>(nr);
     full.n_fragments = r_nf = A4.take<uint32_t>(nr);
+    head_tok = A4.take<uint64_t>(nr);
   }
   hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, nullptr,
                      nullptr, emit_at, rep_at, full, nr, reps, rep_cap, head_tok);
-  uint64_t gtotal = 0;
   if (nr) {
-    const dim3 rg = grid_for(nr);
-    hipLaunchKernelGGL(rw_hash_desc_kernel, rg, dim3(kLanes), 0, st, a, t, it_off, head_tok, r_nf,
-                       r_len, nr, a_off, a_len, glen);
-    scan_u64(glen, nr, tiles3, goff, st);
-    e = hipMemcpyAsync(&gtotal, tiles3 + (nr + kScanTile - 1) / kScanTile, 8,
-                       hipMemcpyDeviceToHost, st);
-    if (e == hipSuccess) e = hipStreamSynchronize(st);
-  }
-  void* gbuf = nullptr;
-  if (e == hipSuccess && nr) e = scratch_alloc(&gbuf, up256(gtotal + 4096), st);
-  if (e == hipSuccess && nr) {
-    const uint32_t ggrid = static_cast<uint32_t>(nr < 65536 ? nr : 65536);
-    hipLaunchKernelGGL(rw_gather_kernel, dim3(ggrid), dim3(kLanes), 0, st, a, t, it_off, head_tok,
-                       r_nf, glen, goff, nr, static_cast<uint8_t*>(gbuf));
-    hipLaunchKernelGGL(rw_gdesc_kernel, grid_for(nr), dim3(kLanes), 0, st, glen, goff, nr, b_off,
-                       b_len);
-    BlockArgs ba{};
-    ba.base = log;
-    ba.base_len = log_len;
-    ba.offsets = a_off;
-    ba.sizes = a_len;
-    ba.out64 = ha;
-    ba.n = nr;
-    e = launch_xxh3_blocks(kModeRaw, ba, st, name);
-    if (e == hipSuccess) {
-      BlockArgs bb = ba;
-      bb.base = static_cast<uint8_t*>(gbuf);
-      bb.base_len = up256(gtotal + 4096);
-      bb.offsets = b_off;
-      bb.sizes = b_len;
-      bb.out64 = hb;
-      e = launch_xxh3_blocks(kModeRaw, bb, st, name);
-    }
-    if (e == hipSuccess) {
-      hipLaunchKernelGGL(rw_select_kernel, grid_for(nr), dim3(kLanes), 0, st, r_nf, ha, hb, nr,
-                         full.hash);
-      e = hipGetLastError();
-    }
+    const RecFrags rf{head_tok, r_nf, t.item, it_off};
+    e = hash_logical_records(log, log_len, rf, nr, full.hash, st, name);
   }
   // copy the (capacity-limited) record list out
   const uint64_t nc = nr < rec_cap ? nr : rec_cap;
@@ -803,11 +698,10 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   }
   if (e == hipSuccess) e = hipGetLastError();
   *name = "wal_recover";
-  const hipError_t f0 = scratch_free(gbuf, st), f4 = scratch_free(s4, st),
-                   f3 = scratch_free(s3, st), f2 = scratch_free(s2, st),
+  const hipError_t f4 = scratch_free(s4, st), f2 = scratch_free(s2, st),
                    f1 = scratch_free(s1, st);
   if (e != hipSuccess) return e;
-  for (hipError_t x : {f0, f4, f3, f2, f1})
+  for (hipError_t x : {f4, f2, f1})
     if (x != hipSuccess) return x;
   return hipSuccess;
 }

@@ -797,6 +797,269 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
   }
 }
 
+// ---------------------------------------------------------------------------
+// Fragment-aware XXH3 of WAL logical records (log::Reader::ReadRecord's record
+// checksum, db/log_reader.cc:95-165), read in place from the log.
+//
+// log::Writer::AddRecord (db/log_writer.cc:65-160) fills every log block: a
+// First or Middle fragment runs to the block end, the next fragment's payload
+// starts hs = 7 (11 recyclable) header bytes into the next block.  So a
+// logical record of L bytes whose first payload byte is at P0 is the log
+// bytes from P0 on with an hs-byte hole at every block start it crosses:
+// logical offset p lives at P0 + p + hs * j(p), j(p) = fragment boundaries
+// <= p, the first at l0 = 32768 - P0 % 32768, then every D = 32768 - hs bytes.
+// The rows kernel layout (one message per 16-lane row, one 1 KiB XXH3-block
+// per step) is kept; each row carries (j at the window start, the next
+// boundary), at most one boundary falls in a 1 KiB window (D > 1024), and the
+// one 16-byte lane slot that straddles it gets a second load hs bytes further
+// on, merged bytewise.  Per-message descriptors: offsets = P0, sizes = L,
+// init_crcs (reused) = frag_info = hs | j_last << 8 (hs = 0: one fragment;
+// j_last = the fragment index of the last stripe).  Records this does not
+// describe (short multi-fragment records, a last fragment under 64 bytes,
+// middles that do not fill their block) are hashed from a gathered copy by
+// the caller.
+// ---------------------------------------------------------------------------
+constexpr uint32_t kWalBlock = 32768;  // db/log_format.h:45
+constexpr uint32_t kNoBound = 0xffffffffu;
+
+struct FRow {
+  uint32_t off_lo, off_hi, size, rel, g;
+  uint32_t info;  // hs | j_last << 8
+  uint32_t jc;    // fragment of the window start
+  uint32_t bn;    // next boundary (logical offset), kNoBound
+  __device__ __forceinline__ uint64_t off() const {
+    return (static_cast<uint64_t>(off_hi) << 32) | off_lo;
+  }
+  __device__ __forceinline__ uint32_t hs() const { return info & 0xffu; }
+};
+
+struct FStep {
+  uint32_t x[4][5];
+  uint32_t l[5];
+  uint32_t alt[5];
+  uint32_t fm;  // m0..m3 (2 bits each) | has_alt:1 @8 | kk:2 @9 | cut:4 @11 | m_alt:2 @15
+};
+
+__device__ __forceinline__ void frow_start(FRow& P) {
+  P.g = 0;
+  P.jc = 0;
+  const uint32_t hs = P.hs();
+  const uint32_t l0 = kWalBlock - static_cast<uint32_t>(P.off() & (kWalBlock - 1));
+  P.bn = (hs && l0 < P.size) ? l0 : kNoBound;
+}
+
+__device__ __forceinline__ void frow_next(FRow& P) {  // window g -> g + 1
+  ++P.g;
+  if (P.bn != kNoBound && 1024u * P.g >= P.bn) {
+    ++P.jc;
+    const uint32_t nb = P.bn + (kWalBlock - P.hs());
+    P.bn = nb < P.size ? nb : kNoBound;
+  }
+}
+
+__device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, const FRow& P,
+                                           FStep& d) {
+  const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
+  const uint64_t P0 = P.off();
+  const bool valid = P.rel != kNoMsg && P0 <= a.base_len;
+  const bool lng = valid && P.size > 240;
+  const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
+  const uint32_t hs = P.hs();
+  uint32_t fm = 0;
+  uint64_t alt_phys = 0;
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
+    const uint32_t ps = 1024u * P.g + 64 * s4 + 16 * p + 256 * k;
+    const uint32_t jk = P.jc + (ps >= P.bn ? 1u : 0u);
+    const uint64_t phys = P0 + ps + static_cast<uint64_t>(hs) * jk;
+    const uint64_t o = need ? (phys & ~3ull) : 0;
+    const uint32_t m = need ? static_cast<uint32_t>(phys & 3) : 0u;
+    const u32x4a4 v = ld16_a4(a.base + o);
+    d.x[k][0] = v.x;
+    d.x[k][1] = v.y;
+    d.x[k][2] = v.z;
+    d.x[k][3] = v.w;
+    d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
+    fm |= m << (2 * k);
+    const bool straddle = need && ps < P.bn && ps + 16 > P.bn;
+    if (straddle) {
+      alt_phys = phys + hs;  // the bytes past the boundary: hs further on
+      fm |= (1u << 8) | (k << 9) | ((P.bn - ps) << 11) | (static_cast<uint32_t>(alt_phys & 3) << 15);
+    }
+  }
+  const uint64_t ao = (fm >> 8) & 1u ? (alt_phys & ~3ull) : 0;
+  const u32x4a4 av = ld16_a4(a.base + ao);
+  d.alt[0] = av.x;
+  d.alt[1] = av.y;
+  d.alt[2] = av.z;
+  d.alt[3] = av.w;
+  d.alt[4] = ld4_a4(a.base + ((fm >> 8) & 1u ? ao + 16 : ao));
+  d.fm = fm;
+  // last stripe at L - 64, inside the last fragment (fragment j_last)
+  const bool lastp = lng && P.g == nb;
+  const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+  const uint32_t ml = static_cast<uint32_t>(lq & 3);
+  const u32x4a4 lv = ld16_a4(a.base + lo);
+  d.l[0] = lv.x;
+  d.l[1] = lv.y;
+  d.l[2] = lv.z;
+  d.l[3] = lv.w;
+  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+}
+
+// WPE: waves per SIMD the register allocation targets (3: 168 VGPRs with a
+// few spills, 2: 181 VGPRs, none)
+template <int WPE>
+__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(WPE)
+xxh3_frag_kernel(BlockArgs a) {
+  // cold per-pair constants and the accumulate keys live in LDS (registers
+  // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
+  __shared__ uint64_t cold[4 * kColdN];
+  __shared__ uint64_t keys[24];
+  if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
+  if (threadIdx.x < 24) keys[threadIdx.x] = sec64(8 * threadIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
+  const uint64_t* ck = cold + kColdN * p;
+  // K0[k] = keys[s4 + 2p + 4k], K1[k] = keys[s4 + 2p + 4k + 1]
+  const uint64_t ks0 = sec64(128 + 16 * p), ks1 = sec64(136 + 16 * p);
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  BatchFeed feed;
+  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  if (cg >= a.n) return;
+  uint64_t ng = feed_next(a, nw, lane, feed);
+  DescBatch cb, nb;
+  uint64_t kbrel = 0;
+  load_batch<kModeRaw>(a, cg, a.n, lane, cb);  // extra = frag_info (init_crcs)
+  load_batch<kModeRaw>(a, ng, a.n, lane, nb);
+  auto fetch = [&](uint64_t rel, FRow& P) {
+    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
+    const int src = static_cast<int>(j & 63u);
+    const bool in_n = j >= 64;
+    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
+    const uint32_t sz_c = __shfl(cb.size, src), in_c = __shfl(cb.extra, src);
+    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
+    const uint32_t sz_n = __shfl(nb.size, src), in_nn = __shfl(nb.extra, src);
+    P.off_lo = in_n ? lo_n : lo_c;
+    P.off_hi = in_n ? hi_n : hi_c;
+    P.size = in_n ? sz_n : sz_c;
+    P.info = in_n ? in_nn : in_c;
+    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
+    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoMsg;
+    frow_start(P);
+  };
+  const uint32_t row = lane >> 4;
+  uint64_t next = 4;
+  FRow C;
+  fetch(row, C);
+  auto advance = [&](const FRow& P, FRow& I) {
+    const bool lng = P.rel != kNoMsg && P.size > 240;
+    const uint32_t nbP = (P.size - 1) >> 10;
+    const bool more = lng && P.g < nbP;
+    const bool need = P.rel != kNoMsg && !more;
+    const uint64_t rows = __ballot(need && t == 0);
+    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+    FRow F;
+    fetch(next + rank, F);
+    next += static_cast<uint64_t>(__popcll(rows));
+    I = P;
+    if (more) frow_next(I);
+    if (need) I = F;
+    if (next >= kbrel + kBatch) {
+      kbrel += kBatch;
+      cb = nb;
+      cg = ng;
+      ng = feed_next(a, nw, lane, feed);
+      load_batch<kModeRaw>(a, ng, a.n, lane, nb);
+    }
+  };
+  FRow I;
+  advance(C, I);
+  FStep X, Y;
+  frag_issue(a, lane, C, X);
+  uint64_t acc0 = 0, acc1 = 0;
+  auto step = [&](FStep& cu, FStep& nx) -> bool {
+    if (__ballot(C.rel != kNoMsg) == 0) return false;
+    frag_issue(a, lane, I, nx);
+    const bool valid = C.rel != kNoMsg && C.off() <= a.base_len;
+    const bool lng = valid && C.size > 240;
+    const uint32_t nbC = (C.size - 1) >> 10, nbSC = ((C.size - 1) & 1023) >> 6;
+    if (C.g == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
+      acc0 = ck[kColdI0];
+      acc1 = ck[kColdI1];
+    }
+    uint64_t sum0 = 0, sum1 = 0;
+    const uint32_t fm = cu.fm;
+    // re-read the keys from LDS every step (an opaque index keeps the
+    // compiler from hoisting them back into registers)
+    uint32_t kix = s4 + 2 * p;
+#ifndef FORST_HOST_EMULATION
+    asm volatile("" : "+v"(kix));
+#endif
+    const uint64_t* kq = keys + kix;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      uint64_t d0, d1;
+      xx_words(cu.x[k], (fm >> (2 * k)) & 3u, d0, d1);
+      if (((fm >> 8) & 1u) && ((fm >> 9) & 3u) == k) {  // the slot across the boundary
+        uint64_t a0, a1;
+        xx_words(cu.alt, (fm >> 15) & 3u, a0, a1);
+        const uint32_t cut = (fm >> 11) & 15u;  // bytes before the boundary
+        const uint64_t mlo = cut >= 8 ? ~0ull : ((1ull << (8 * cut)) - 1);
+        const uint64_t mhi = cut >= 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull;
+        d0 = (d0 & mlo) | (a0 & ~mlo);
+        d1 = (d1 & mhi) | (a1 & ~mhi);
+      }
+      const uint64_t c0 = mul32to64(d0 ^ kq[4 * k]) + d1;  // acc[2p] (xxhash.h:4926-4927)
+      const uint64_t c1 = d0 + mul32to64(d1 ^ kq[4 * k + 1]);  // acc[2p+1]
+      const bool use = C.g < nbC || s4 + 4 * k < nbSC;
+      sum0 += use ? c0 : 0ull;
+      sum1 += use ? c1 : 0ull;
+    }
+    sum0 += row_ror64<4>(sum0);
+    sum1 += row_ror64<4>(sum1);
+    sum0 += row_ror64<8>(sum0);
+    sum1 += row_ror64<8>(sum1);
+    acc0 += sum0;
+    acc1 += sum1;
+    const bool full = C.g < nbC;
+    if (full) {
+      acc0 = scramble(acc0, ks0);
+      acc1 = scramble(acc1, ks1);
+    }
+    const bool fin = C.rel != kNoMsg && !(lng && full);
+    if (__ballot(fin)) {
+      uint64_t h;
+      {
+        uint64_t d0, d1;
+        const uint64_t le = C.off() + C.size + static_cast<uint64_t>(C.hs()) * (C.info >> 8);
+        xx_words(cu.l, static_cast<uint32_t>(le & 3), d0, d1);
+        const uint64_t a0 = acc0 + mul32to64(d0 ^ ck[kColdL0]) + d1;
+        const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ ck[kColdL1]);
+        uint64_t tm = mul128_fold64(a0 ^ ck[kColdM0], a1 ^ ck[kColdM1]);
+        tm += shfl_xor64(tm, 1);
+        tm += shfl_xor64(tm, 2);
+        h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
+      }
+      if (fin && valid && !lng) {  // short record: one fragment, in place
+        const uint64_t hs2 = xxh3_short(a.base + C.off(), C.size);
+        h = mk64(retire(static_cast<uint32_t>(hs2)), retire(static_cast<uint32_t>(hs2 >> 32)));
+      }
+      if (fin && t == 0 && a.out64) a.out64[C.rel] = valid ? h : 0ull;
+    }
+    C = I;
+    advance(C, I);
+    return true;
+  };
+  while (step(X, Y) && step(Y, X)) {
+  }
+}
+
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) xxh3_block_kernel_simple(BlockArgs a) {
   const uint32_t lane = threadIdx.x & 63;
@@ -983,6 +1246,44 @@ hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const
 }
 
 }  // namespace
+
+template <int WPE>
+uint32_t frag_occupancy() {
+  static const uint32_t occ = [] {
+    int o = 0;
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE>, kThreads, 0) !=
+            hipSuccess ||
+        o < 1)
+      o = 1;
+    return static_cast<uint32_t>(o);
+  }();
+  return occ;
+}
+
+template <int WPE>
+hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name) {
+  const DeviceInfo& di = device_info();
+  const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
+      1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),
+                            uint64_t(di.num_cus) * frag_occupancy<WPE>())));
+  BlockArgs b = a;
+  hipError_t e = feed_setup(b, uint64_t(grid) * kWaves, stream);
+  if (e != hipSuccess) return e;
+  *name = WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
+  hipLaunchKernelGGL(xxh3_frag_kernel<WPE>, dim3(grid), dim3(kThreads), 0, stream, b);
+  e = hipGetLastError();
+  const hipError_t f = scratch_free(b.ticket, stream);
+  return e != hipSuccess ? e : f;
+}
+
+hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char** name) {
+  if (a.n == 0) return hipSuccess;
+  if (a.n >= 0xffffffffull || a.base_len < 4096 || !a.init_crcs) return hipErrorInvalidValue;
+#ifdef FORST_DIAG
+  if (std::string(diag_env("FORST_FRAG_WPE")) == "3") return launch_frag<3>(a, stream, name);
+#endif
+  return launch_frag<2>(a, stream, name);
+}
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
                               const char** name) {

@@ -27,6 +27,7 @@
 #define __constant__
 #define __forceinline__ inline
 #define __launch_bounds__(...)
+#define FORST_WAVES_PER_EU(n)
 #define __shared__ static
 
 struct dim3 {

@@ -289,6 +289,24 @@ def test_emu_wal_record_xxh3(recyclable):
         assert int(h[j]) == O.xxh3_64(payload[starts[j]:starts[j + 1]].tobytes()), j
 
 
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_emu_wal_record_xxh3_fragment_edges(recyclable):
+    """a14 across log-block boundaries at every lane-slot byte, window and
+    stripe edge, last fragments of 63-66 bytes, 241-300-byte records, empty
+    first fragments, 3-4 fragments (tests/walcases.py): the in-place
+    fragment-aware hash and the gathered fallback both equal XXH3 of the
+    payload"""
+    import walcases as W
+    buf, po, payload, lens, targets = W.frag_edge_log(recyclable, seed=5 + recyclable)
+    first = W.first_fragment_offsets(buf, po)
+    hs = 11 if recyclable else 7
+    for j, l0 in targets:  # the generator placed each case where it meant to
+        assert int(first[j]) % W.BLOCK == W.BLOCK - hs - l0, (j, l0)
+    h, f = emu.wal_record_xxh3(buf, po)
+    assert len(h) == len(lens)
+    assert (np.asarray(h).view(np.uint64) == W.expected_hashes(payload, lens)).all()
+
+
 def test_emu_rows_extra_dword_windows():
     """4096- and 1024·k-byte blocks at every start alignment: the rows kernel
     ends windows that are one dword longer than whole rounds one dword early

@@ -556,6 +556,16 @@ def test_wal_record_xxh3(recyclable):
     assert (h == want).all()
 
 
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_record_xxh3_fragment_edges(recyclable):
+    """every boundary placement of tests/walcases.py, 20 rounds (~4800
+    records): the in-place fragment-aware kernel and the gathered fallback"""
+    import walcases as W
+    buf, po, payload, lens, targets = W.frag_edge_log(recyclable, seed=40 + recyclable, repeat=20)
+    h, first = engine.wal_record_xxh3_batch(d(buf), d(po.astype(np.int64)))
+    assert (host(h).view(np.uint64) == W.expected_hashes(payload, lens)).all()
+
+
 def test_full_size_c5_record_xxh3():
     """10 M logical records of C5: count, first fragments against the writer's
     layout, 2000 sampled hashes against the oracle over the gathered bytes"""

@@ -1265,24 +1265,30 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
       d.w[c][4 * q + 3] = v.w;
     }
   }
-  // tail dword at the window end (last round of a fast block only)
-  const uint32_t nt = P.nt();
+  // the finishing step's words: tail dword at the window end (last round of a
+  // fast block), stored checksum, modifier / type byte / init -- loaded only
+  // in steps where some row of the wave finishes a block
   const bool lastr = !P.slow() && P.g + 1 >= P.R;
-  const bool xt = MODE != kModeRaw && P.xtra();
-  const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
-  const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
-  const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
-  d.t0 = ld4v(a.base + t0);
-  // t1: the word after the tail (verify: stored checksum), else the extra
-  // window dword; t2: the extra window dword in verify mode
-  const uint64_t tx = lastr && xt ? wE : t0;
-  d.t1 = MODE == kModeRaw ? 0u
-                          : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
-  d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
-  const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
-  d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
-  d.extra = MODE == kModeRaw ? (a.init_crcs ? a.init_crcs[idx] : 0u)
-                             : (a.last_bytes ? a.last_bytes[idx] : 0u);
+  const bool fin = P.rel != kNoBlk && (P.slow() || lastr);
+  d.t0 = d.t1 = d.t2 = d.mod = d.extra = 0u;
+  if (__ballot(fin)) {
+    const uint32_t nt = P.nt();
+    const bool xt = MODE != kModeRaw && P.xtra();
+    const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
+    const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
+    const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
+    d.t0 = ld4v(a.base + t0);
+    // t1: the word after the tail (verify: stored checksum), else the extra
+    // window dword; t2: the extra window dword in verify mode
+    const uint64_t tx = lastr && xt ? wE : t0;
+    d.t1 = MODE == kModeRaw ? 0u
+                            : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
+    d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
+    const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
+    d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
+    d.extra = MODE == kModeRaw ? (a.init_crcs ? a.init_crcs[idx] : 0u)
+                               : (a.last_bytes ? a.last_bytes[idx] : 0u);
+  }
 }
 
 // PROBE (diagnostics build only): 1 = same loads and row bookkeeping, no
@@ -1339,19 +1345,23 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     const bool more = P.rel != kNoBlk && !P.slow() && P.g + 1 < P.R;
     const bool need = P.rel != kNoBlk && !more;
     const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
-    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
-    CRowPos F;
-    fetch(next + rank, F);
-    next += static_cast<uint64_t>(__popcll(rows));
     I = P;
     if (more) I.g = P.g + 1;
-    if (need) I = F;
-    if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
-      kbrel += kBatch;
-      cb = nb;
-      cg = ng;
-      ng = feed_next(a, nw, lane, feed);
-      load_batch<MODE>(a, ng, a.n, lane, nb);
+    // rows in the middle of their blocks (every row, 3 steps in 4 of a batch
+    // of 4 KiB blocks): no descriptor work
+    if (rows) {
+      const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+      CRowPos F;
+      fetch(next + rank, F);
+      next += static_cast<uint64_t>(__popcll(rows));
+      if (need) I = F;
+      if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
+        kbrel += kBatch;
+        cb = nb;
+        cg = ng;
+        ng = feed_next(a, nw, lane, feed);
+        load_batch<MODE>(a, ng, a.n, lane, nb);
+      }
     }
   };
   CRowPos I, I2;

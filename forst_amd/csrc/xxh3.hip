@@ -592,31 +592,38 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
     // holds a message byte, so it never crosses into an unmapped page
     d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
   }
+  // the finishing step's words (last stripe, type byte / stored checksum,
+  // modifier): loaded only in steps where some row of the wave finishes
   const bool lastp = lng && P.g == nb;
-  const uint64_t lq = off + P.size - 64 + 16 * p;
-  const uint32_t ml = static_cast<uint32_t>(lq & 3);
-  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
-  const u32x4a4 v = ld16_a4(a.base + lo);
-  d.l[0] = v.x;
-  d.l[1] = v.y;
-  d.l[2] = v.z;
-  d.l[3] = v.w;
-  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
-  // type byte at E = off + size, stored LE32 at E + 1 (verify); for compute /
-  // trailer without last_bytes[] only the type byte
-  const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
-  const uint64_t E = off + P.size;
-  const uint64_t t0 = (lastp && mem_last) ? (E & ~3ull) : 0;
-  d.t0 = ld4v(a.base + t0);
-  d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastp ? t0 + 4 : 0)) : 0u;
-  const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
-  d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
-  d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
-                                                                              : 0u;
+  const bool fin = P.rel != kNoMsg && (!lng || P.g == nb);
+  d.l[0] = d.l[1] = d.l[2] = d.l[3] = d.l[4] = 0u;
+  d.t0 = d.t1 = d.mod = d.extra = 0u;
+  if (__ballot(fin)) {
+    const uint64_t lq = off + P.size - 64 + 16 * p;
+    const uint32_t ml = static_cast<uint32_t>(lq & 3);
+    const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+    const u32x4a4 v = ld16_a4(a.base + lo);
+    d.l[0] = v.x;
+    d.l[1] = v.y;
+    d.l[2] = v.z;
+    d.l[3] = v.w;
+    d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+    // type byte at E = off + size, stored LE32 at E + 1 (verify); for compute /
+    // trailer without last_bytes[] only the type byte
+    const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
+    const uint64_t E = off + P.size;
+    const uint64_t t0 = (lastp && mem_last) ? (E & ~3ull) : 0;
+    d.t0 = ld4v(a.base + t0);
+    d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastp ? t0 + 4 : 0)) : 0u;
+    const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
+    d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
+    d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
+                                                                                : 0u;
+  }
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
+__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kernel(BlockArgs a) {
   __shared__ uint64_t cold[4 * kColdN];
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   __syncthreads();
@@ -674,19 +681,21 @@ __global__ void __launch_bounds__(kThreads) xxh3_rows_kernel(BlockArgs a) {
     const bool more = lng && P.g < nbP;
     const bool need = P.rel != kNoMsg && !more;
     const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
-    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
-    RowPos F;
-    fetch(next + rank, F);
-    next += static_cast<uint64_t>(__popcll(rows));
     I = P;
     if (more) I.g = P.g + 1;
-    if (need) I = F;
-    if (next >= kbrel + kBatch) {  // every message of cb is assigned: slide the batches
-      kbrel += kBatch;
-      cb = nb;
-      cg = ng;
-      ng = feed_next(a, nw, lane, feed);
-      load_batch<MODE>(a, ng, a.n, lane, nb);
+    if (rows) {  // descriptor work only in steps where some row takes a message
+      const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+      RowPos F;
+      fetch(next + rank, F);
+      next += static_cast<uint64_t>(__popcll(rows));
+      if (need) I = F;
+      if (next >= kbrel + kBatch) {  // every message of cb is assigned: slide the batches
+        kbrel += kBatch;
+        cb = nb;
+        cg = ng;
+        ng = feed_next(a, nw, lane, feed);
+        load_batch<MODE>(a, ng, a.n, lane, nb);
+      }
     }
   };
 
@@ -896,21 +905,25 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   d.alt[3] = av.w;
   d.alt[4] = ld4_a4(a.base + ((fm >> 8) & 1u ? ao + 16 : ao));
   d.fm = fm;
-  // last stripe at L - 64, inside the last fragment (fragment j_last)
+  // last stripe at L - 64, inside the last fragment (fragment j_last): only
+  // in steps where some row of the wave finishes a long record
   const bool lastp = lng && P.g == nb;
-  const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
-  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
-  const uint32_t ml = static_cast<uint32_t>(lq & 3);
-  const u32x4a4 lv = ld16_a4(a.base + lo);
-  d.l[0] = lv.x;
-  d.l[1] = lv.y;
-  d.l[2] = lv.z;
-  d.l[3] = lv.w;
-  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+  d.l[0] = d.l[1] = d.l[2] = d.l[3] = d.l[4] = 0u;
+  if (__ballot(lastp)) {
+    const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+    const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+    const uint32_t ml = static_cast<uint32_t>(lq & 3);
+    const u32x4a4 lv = ld16_a4(a.base + lo);
+    d.l[0] = lv.x;
+    d.l[1] = lv.y;
+    d.l[2] = lv.z;
+    d.l[3] = lv.w;
+    d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+  }
 }
 
-// WPE: waves per SIMD the register allocation targets (3: 168 VGPRs with a
-// few spills, 2: 181 VGPRs, none)
+// WPE: waves per SIMD the register allocation targets (3, the default: 168
+// VGPRs with a few spilled dwords, C5 a14 21.5 vs 24.8 ms at 2: 181 VGPRs)
 template <int WPE>
 __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(WPE)
 xxh3_frag_kernel(BlockArgs a) {
@@ -963,19 +976,21 @@ xxh3_frag_kernel(BlockArgs a) {
     const bool more = lng && P.g < nbP;
     const bool need = P.rel != kNoMsg && !more;
     const uint64_t rows = __ballot(need && t == 0);
-    const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
-    FRow F;
-    fetch(next + rank, F);
-    next += static_cast<uint64_t>(__popcll(rows));
     I = P;
     if (more) frow_next(I);
-    if (need) I = F;
-    if (next >= kbrel + kBatch) {
-      kbrel += kBatch;
-      cb = nb;
-      cg = ng;
-      ng = feed_next(a, nw, lane, feed);
-      load_batch<kModeRaw>(a, ng, a.n, lane, nb);
+    if (rows) {  // descriptor work only in steps where some row takes a record
+      const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+      FRow F;
+      fetch(next + rank, F);
+      next += static_cast<uint64_t>(__popcll(rows));
+      if (need) I = F;
+      if (next >= kbrel + kBatch) {
+        kbrel += kBatch;
+        cb = nb;
+        cg = ng;
+        ng = feed_next(a, nw, lane, feed);
+        load_batch<kModeRaw>(a, ng, a.n, lane, nb);
+      }
     }
   };
   FRow I;
@@ -1280,9 +1295,9 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
   if (a.n == 0) return hipSuccess;
   if (a.n >= 0xffffffffull || a.base_len < 4096 || !a.init_crcs) return hipErrorInvalidValue;
 #ifdef FORST_DIAG
-  if (std::string(diag_env("FORST_FRAG_WPE")) == "3") return launch_frag<3>(a, stream, name);
+  if (std::string(diag_env("FORST_FRAG_WPE")) == "2") return launch_frag<2>(a, stream, name);
 #endif
-  return launch_frag<2>(a, stream, name);
+  return launch_frag<3>(a, stream, name);
 }
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,

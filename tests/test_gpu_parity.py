@@ -313,30 +313,46 @@ def test_sst_batches_vs_oracle(spec, ctype):
     assert (hb[:4096] == S.stream(b.seed, 0, 4096)).all() or sizes[0] < 4096
 
 
-def test_full_size_c2_properties():
-    """C2: 1 M x 4 KiB kCRC32c, compute + verify at full size.  Checked by
-    (1) round trip: trailers written by the compute kernel verify clean,
-    (2) a 4096-block random sample against the oracle,
-    (3) exact detection of injected corruptions."""
-    n = 1 << 20
-    b = workload.make_sst_batch(n, 4096, workload.SEEDS["C2"], ctype=CT.kCRC32c)
-    comp, st, ok, bad = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
+FULL_SIZE = {  # bench.py CONFIGS: (blocks, size spec, checksum type, seed)
+    "C2": (1 << 20, 4096, CT.kCRC32c, workload.SEEDS["C2"]),
+    "C3": (1 << 20, (4096, 16384, 65536), CT.kXXH3, workload.SEEDS["C3"]),
+    "C4": (1 << 19, 16384, CT.kCRC32c, workload.SEEDS["C4"]),
+    "NS16": (1 << 20, 16384, CT.kCRC32c, workload.SEEDS["C2"]),
+    "NS16X": (1 << 20, 16384, CT.kXXH3, workload.SEEDS["C2"]),
+}
+
+
+@pytest.mark.parametrize("cfg", list(FULL_SIZE))
+def test_full_size_properties(cfg):
+    """Every bench configuration at its full size (C2 1 M x 4 KiB, C3 1 M
+    mixed 4/16/64 KiB XXH3, C4 512 K x 16 KiB, NS16 / NS16X 1 M x 16 KiB
+    CRC32C / XXH3), the kernels the bench times: (1) round trip -- trailers
+    written by the trailer kernel verify clean, (2) a 4096-block random sample
+    (plus the first and last blocks) against the oracle, (3) exact detection
+    of 64 injected corruptions, at the block start, middle and last byte."""
+    n, spec, ctype, seed = FULL_SIZE[cfg]
+    b = workload.make_sst_batch(n, spec, seed, ctype=ctype)
+    comp, st, ok, bad = engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes)
     assert int(host(bad)[0]) == 0
     rng = np.random.default_rng(5)
     sample = np.unique(np.concatenate([[0, 1, n - 1], rng.integers(0, n, 4096)]))
     offs = host(b.offsets)
+    sizes = host(b.sizes).astype(np.int64)
     compd = host(comp)
+    stored = host(st)
     for i in sample:
-        o = int(offs[i])
-        blk = host(b.base[o:o + 4096 + 5])
-        assert int(compd[i]) == O.compute_builtin_checksum(1, blk[:4097])
+        o, sz = int(offs[i]), int(sizes[i])
+        blk = host(b.base[o:o + sz + 5])
+        want = O.compute_builtin_checksum(int(ctype), blk[:sz + 1])
+        assert int(compd[i]) == want and int(stored[i]) == want, (cfg, i)
     victims = rng.choice(n, 64, replace=False)
-    flip = torch.from_numpy(offs[victims] + 17).to(DEV)
-    b.base[flip] ^= 0x10
-    _, _, ok, bad = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
-    okh = host(ok)
+    pos = offs[victims].astype(np.int64) + np.where(
+        np.arange(64) % 3 == 0, 0, np.where(np.arange(64) % 3 == 1, sizes[victims] // 2,
+                                             sizes[victims] - 1))
+    b.base[torch.from_numpy(pos).to(DEV)] ^= 0x10
+    _, _, ok, bad = engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes)
     assert int(host(bad)[0]) == 64
-    assert set(np.nonzero(okh == 0)[0].tolist()) == set(victims.tolist())
+    assert set(np.nonzero(host(ok) == 0)[0].tolist()) == set(victims.tolist())
 
 
 # ---- a15: Hash64 (XXPH3) and per-KV protection (db/kv_checksum.h) ---------

@@ -1224,7 +1224,10 @@ __device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
   const uint32_t q = seg_head < 0 ? static_cast<uint32_t>(-seg_head) >> 2 : 0u;
   const uint32_t nt = static_cast<uint32_t>(E - we);
   const uint32_t m = static_cast<uint32_t>(off & 3);
-  const bool slow = !valid || d4 < 64;
+  // messages without one whole dword take the slow path (its loads are serial
+  // and unprefetched: a WAL record of 40 B through it cost a wave ~10 dependent
+  // load latencies); everything else, however short, is one prefetched round
+  const bool slow = !valid || d4 < 4;
   if (slow) {  // the slow path loads on its own; dummy round loads at [0, 1 KiB)
     R = 1;
     w0 = 0;
@@ -1241,12 +1244,29 @@ struct CRStep {
   uint32_t t0, t1, t2, mod, extra;  // t2: the extra window dword (xtra)
 };
 
-template <int MODE>
+template <int MODE, int PROBE = 0>
 __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, const CRowPos& P,
                                            uint64_t kbeg, CRStep& d) {
   const uint32_t t = lane & 15;
   const int64_t w0 = P.w0();
   const uint32_t cA = P.cA(), tA = P.tA();
+  if (PROBE == 3) {  // diagnostics: the same bytes as 16-B aligned, row-contiguous pieces
+    const int64_t rb = (w0 & ~int64_t(15)) + static_cast<int64_t>(P.g) * kRowRound + 16 * t;
+#pragma unroll
+    for (uint32_t c = 0; c < 2; ++c)
+#pragma unroll
+      for (int q = 0; q < 2; ++q) {
+        int64_t so = rb + 256 * (2 * c + q);
+        so = so < 0 ? 0 : so;
+        const u32x4a4 v = ld16_a4(a.base + so);
+        d.w[c][4 * q + 0] = v.x;
+        d.w[c][4 * q + 1] = v.y;
+        d.w[c][4 * q + 2] = v.z;
+        d.w[c][4 * q + 3] = v.w;
+      }
+    d.t0 = d.t1 = d.t2 = d.mod = d.extra = 0u;
+    return;
+  }
 #pragma unroll
   for (uint32_t c = 0; c < 2; ++c) {
     int64_t so = w0 + static_cast<int64_t>(P.g) * kRowRound + kRowChain * c + kSeg2 * t;
@@ -1286,9 +1306,11 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
     d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
     const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
     d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
-    d.extra = MODE == kModeRaw ? (a.init_crcs ? a.init_crcs[idx] : 0u)
-                               : (a.last_bytes ? a.last_bytes[idx] : 0u);
+    if (MODE != kModeRaw && a.last_bytes) d.extra = a.last_bytes[idx];
   }
+  // raw mode's per-message init: the head (round 0) and the slow path read it
+  if (MODE == kModeRaw && a.init_crcs && __ballot(P.rel != kNoBlk && (fin || P.g == 0)))
+    d.extra = a.init_crcs[kbeg + (P.rel == kNoBlk ? 0 : P.rel)];
 }
 
 // PROBE (diagnostics build only): 1 = same loads and row bookkeeping, no
@@ -1368,15 +1390,15 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   advance(C, I);
   if (DEPTH == 2) advance(I, I2);
   CRStep X, Y, Z;
-  crow_issue<MODE>(a, lane, C, kbeg, X);
-  if (DEPTH == 2) crow_issue<MODE>(a, lane, I, kbeg, Y);
+  crow_issue<MODE, PROBE>(a, lane, C, kbeg, X);
+  if (DEPTH == 2) crow_issue<MODE, PROBE>(a, lane, I, kbeg, Y);
   uint32_t s[2] = {0, 0};
 
   // cu: the current step's data (ready); nx: the buffer that receives the
   // loads issued now (the position DEPTH steps ahead)
   auto step = [&](CRStep& cu, CRStep& nx) -> bool {
     if (__ballot(C.rel != kNoBlk) == 0) return false;
-    crow_issue<MODE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
+    crow_issue<MODE, PROBE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
     const bool fast = C.rel != kNoBlk && !C.slow();
     const bool r0 = C.g == 0;
     // ---- one 1 KiB round of every row ----
@@ -1385,7 +1407,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     for (int c = 0; c < 2; ++c)
 #pragma unroll
       for (int j = 0; j < 8; ++j) w[c][j] = cu.w[c][j];
-    if (PROBE != 1 && __ballot(fast && r0)) {  // some row starts a block: its head
+    if (PROBE != 1 && PROBE != 3 && __ballot(fast && r0)) {  // some row starts a block: its head
       const uint32_t cA = C.cA(), tA = C.tA(), jA = C.jA(), q = C.q(), m = C.m();
       const uint32_t bm = 0xffffffffu << (8 * m);
       // raw mode with per-message inits: the GF(2) unstep; without (crc32c::Value,
@@ -1421,7 +1443,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         }
       }
     }
-    if (PROBE == 1) {
+    if (PROBE == 1 || PROBE == 3) {
 #pragma unroll
       for (int c = 0; c < 2; ++c) {
         uint32_t x = r0 ? 0u : s[c];
@@ -1431,7 +1453,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       }
     }
 #pragma unroll
-    for (int c = 0; c < (PROBE == 1 ? 0 : 2); ++c) {
+    for (int c = 0; c < ((PROBE == 1 || PROBE == 3) ? 0 : 2); ++c) {
       uint32_t lj[4], lg[4];
       rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);  // J3(0) = 0: a row at round 0 starts fresh
       rep_look<false>(Lb, K, w[c][0], lg);
@@ -1547,6 +1569,9 @@ template <int MODE>
 __global__ void __launch_bounds__(64 * kRowsD2Waves) crc32c_rows_d2_kernel(BlockArgs a) {
   crc32c_rows_body<MODE, 0, 2>(a);
 }
+__global__ void __launch_bounds__(64 * kRowsD2Waves) crc32c_rows_d2_probe_kernel(BlockArgs a) {
+  crc32c_rows_body<kModeVerify, 1, 2>(a);
+}
 #endif
 
 // One wave per block, no streaming: serves buffers shorter than one 4 KiB
@@ -1625,7 +1650,7 @@ enum class CrcKernel {
   kRows,    // one block per 16-lane row (crc32c_rows_kernel)
   kV2,      // one block per wave, two chains per lane (crc32c_stream2_kernel)
 #ifdef FORST_DIAG
-  kV1, kRowsD2, kRowsProbeLoad, kRowsProbeNoFin, kV2ProbeLoad, kV2ProbeRounds, kV2ProbeNoHead,
+  kV1, kRowsD2, kRowsProbeLoad, kRowsProbeNoFin, kRowsD2ProbeLoad, kRowsProbeContig, kV2ProbeLoad, kV2ProbeRounds, kV2ProbeNoHead,
 #endif
 };
 
@@ -1664,6 +1689,8 @@ const char* crc_kernel_name(CrcKernel k, int mode) {
   switch (k) {
     case CrcKernel::kRowsProbeLoad: return "crc32c_rows_probe_kernel<1>";
     case CrcKernel::kRowsProbeNoFin: return "crc32c_rows_probe_kernel<2>";
+    case CrcKernel::kRowsD2ProbeLoad: return "crc32c_rows_d2_probe_kernel";
+    case CrcKernel::kRowsProbeContig: return "crc32c_rows_probe_kernel<3>";
     case CrcKernel::kV2ProbeLoad: return "crc32c_stream2_probe_kernel<1>";
     case CrcKernel::kV2ProbeRounds: return "crc32c_stream2_probe_kernel<2>";
     case CrcKernel::kV2ProbeNoHead: return "crc32c_stream2_probe_kernel<3>";
@@ -1691,6 +1718,10 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
       return launch_fed(crc32c_rows_probe_kernel<1>, grid, kWaves, a, s);
     case CrcKernel::kRowsProbeNoFin:
       return launch_fed(crc32c_rows_probe_kernel<2>, grid, kWaves, a, s);
+    case CrcKernel::kRowsD2ProbeLoad:
+      return launch_fed(crc32c_rows_d2_probe_kernel, grid, kRowsD2Waves, a, s);
+    case CrcKernel::kRowsProbeContig:
+      return launch_fed(crc32c_rows_probe_kernel<3>, grid, kWaves, a, s);
     case CrcKernel::kV2ProbeLoad:
       return launch_kernel(crc32c_stream2_probe_kernel<1>, grid, kThreads, a, s);
     case CrcKernel::kV2ProbeRounds:
@@ -1715,6 +1746,8 @@ CrcKernel diag_crc_kernel(CrcKernel k, int mode) {
   if (v == "rows_d2") return CrcKernel::kRowsD2;
   if (v == "rows_probe_load" && vf) return CrcKernel::kRowsProbeLoad;
   if (v == "rows_probe_nofin" && vf) return CrcKernel::kRowsProbeNoFin;
+  if (v == "rows_d2_probe_load" && vf) return CrcKernel::kRowsD2ProbeLoad;
+  if (v == "rows_probe_contig" && vf) return CrcKernel::kRowsProbeContig;
   if (v == "probe_load" && vf) return CrcKernel::kV2ProbeLoad;
   if (v == "probe_rounds" && vf) return CrcKernel::kV2ProbeRounds;
   if (v == "probe_nohead" && vf) return CrcKernel::kV2ProbeNoHead;

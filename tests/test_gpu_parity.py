@@ -73,6 +73,28 @@ def test_crc32c_extend_with_init(golden):
         assert int(out[k]) == want, (r["n"], r["off"])
 
 
+@pytest.mark.parametrize("mean", [600, 5000, 40000])
+def test_crc32c_extend_multi_round_with_init(mean):
+    """crc32c::Extend(init, data, n) with a per-message init over messages of
+    1..~3 x mean bytes at every alignment, from the buffer start on: the rows
+    kernel (mean <= 20 KiB) and the v2 kernel take the init in round 0 of a
+    message, many rounds before its finish"""
+    rng = np.random.default_rng(mean)
+    n = 3000
+    sizes = rng.integers(1, 3 * mean, n).astype(np.uint32)
+    sizes[:64] = np.arange(1, 65)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + rng.integers(0, 9, n - 1).astype(np.uint64))
+    total = int(offs[-1]) + int(sizes[-1]) + 64
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = host(engine.crc32c_batch(d(base), d(offs.view(np.int64)), d(sizes.view(np.int32)),
+                                   init_crcs=d(init.view(np.int32)))).view(np.uint32)
+    for k in range(n):
+        o, s = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.crc32c_extend(int(init[k]), base[o:o + s]), (k, o, s)
+
+
 def test_xxh3_raw_golden(golden):
     v, arr, base, offs, lens = golden
     out = host(engine.xxh3_64_batch(base, offs, lens)).view(np.uint64)

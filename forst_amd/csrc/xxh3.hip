@@ -100,6 +100,105 @@ __device__ uint64_t xxh3_short(const uint8_t* in, uint32_t len) {
   return xxh3_avalanche(acc + acc_end);
 }
 
+// ---- short inputs (<= 240 B) on a 16-lane row, from prefetched chunks -----
+// Lane t of the row that owns the input loads ONE 16-byte chunk with the
+// step's other prefetched loads, chosen so that the length class's formula
+// (util/xxhash.h:3918-4139, xxh3_short above) becomes one mix16B per lane and
+// two row sums -- no dependent loads in the finish:
+//   129..240  t < len/16: [16t, +16) (t < 8: acc, else acc_end with secret
+//             16(t-8)+3); t = 15: [len-16, +16) (acc_end, secret 119)
+//   17..128   t < 4: front chunk r = t, [16r, +16), secret 32r; 4 <= t < 8:
+//             back chunk r = t-4, [len-16-16r, +16), secret 32r+16 (r <=
+//             (len-1)/32)
+//   0..16     t = 0: the 16 bytes ending at the input end (from 0 when the
+//             input ends in the buffer's first 16 bytes); the formula reads
+//             its 1-3 bytes / two dwords / two qwords out of that window
+// Unused lanes load the input's first byte's dword (never past its end).
+__device__ __forceinline__ bool short_used(uint32_t L, uint32_t t) {
+  if (L > 128) return t == 15 || t < L / 16;
+  if (L > 16) {
+    const uint32_t r = (L - 1) / 32;
+    return t < 4 ? t <= r : (t < 8 && t - 4 <= r);
+  }
+  return t == 0;
+}
+
+// address of lane t's chunk of the input [P0, P0 + L)
+__device__ __forceinline__ uint64_t short_phys(uint64_t P0, uint32_t L, uint32_t t) {
+  if (L <= 16) return t == 0 && P0 + L >= 16 ? P0 + L - 16 : (t == 0 ? 0 : P0);
+  if (!short_used(L, t)) return P0;
+  if (L > 128) return P0 + (t == 15 ? L - 16 : 16 * t);
+  return P0 + (t < 4 ? 16 * t : L - 16 - 16 * (t - 4));
+}
+
+// per-lane secret words of the two chunk classes (LDS, 4 x u64 per row lane):
+// [0..1] 129..240, [2..3] 17..128
+__device__ __forceinline__ void short_secrets_fill(uint64_t* sk, uint32_t tid) {
+  if (tid < 16) {
+    const uint32_t t = tid;
+    const uint32_t sa = t < 8 ? 16 * t : (t == 15 ? 136 - 17 : 16 * (t - 8) + 3);
+    const uint32_t sb = t < 4 ? 32 * t : (t < 8 ? 32 * (t - 4) + 16 : 0);
+    sk[4 * t + 0] = sec64(sa);
+    sk[4 * t + 1] = sec64(sa + 8);
+    sk[4 * t + 2] = sec64(sb);
+    sk[4 * t + 3] = sec64(sb + 8);
+  }
+}
+
+// 8 / 4 / 1 bytes at byte position pos of the 16-byte window (d0 | d1 << 64)
+__device__ __forceinline__ uint64_t win8(uint64_t d0, uint64_t d1, uint32_t pos) {
+  if (pos == 0) return d0;
+  if (pos >= 8) return d1 >> (8 * (pos - 8));
+  return (d0 >> (8 * pos)) | (d1 << (64 - 8 * pos));
+}
+__device__ __forceinline__ uint32_t win1(uint64_t d0, uint64_t d1, uint32_t pos) {
+  return static_cast<uint32_t>((pos < 8 ? d0 >> (8 * pos) : d1 >> (8 * (pos - 8))) & 0xffu);
+}
+
+// XXH3_64bits of the row's short input of L bytes; (d0, d1) = the lane's
+// chunk, pb = the input's first byte in lane 0's window (L <= 16).  Every
+// lane of the wave must call it (DPP row sums); the row's lanes agree on the
+// result for L > 16, lane 0 holds it for L <= 16.
+__device__ __forceinline__ uint64_t xxh3_short_row(uint64_t d0, uint64_t d1, uint32_t L,
+                                                   uint32_t t, uint32_t pb,
+                                                   const uint64_t* __restrict__ sk) {
+  const bool big = L > 128;
+  const bool used = L > 16 && short_used(L, t);
+  const uint64_t k0 = big ? sk[4 * t + 0] : sk[4 * t + 2];
+  const uint64_t k1 = big ? sk[4 * t + 1] : sk[4 * t + 3];
+  const uint64_t mx = used ? mul128_fold64(d0 ^ k0, d1 ^ k1) : 0ull;
+  uint64_t sa = t < 8 ? mx : 0ull, sb = t < 8 ? 0ull : mx;
+  sa += row_ror64<1>(sa);
+  sb += row_ror64<1>(sb);
+  sa += row_ror64<2>(sa);
+  sb += row_ror64<2>(sb);
+  sa += row_ror64<4>(sa);
+  sb += row_ror64<4>(sb);
+  sa += row_ror64<8>(sa);
+  sb += row_ror64<8>(sb);
+  const uint64_t acc = static_cast<uint64_t>(L) * P64_1 + sa;
+  if (L > 128) return xxh3_avalanche(xxh3_avalanche(acc) + sb);
+  if (L > 16) return xxh3_avalanche(acc);
+  if (L > 8) {
+    const uint64_t lo = win8(d0, d1, pb) ^ (sec64(24) ^ sec64(32));
+    const uint64_t hi = win8(d0, d1, pb + L - 8) ^ (sec64(40) ^ sec64(48));
+    return xxh3_avalanche(L + __builtin_bswap64(lo) + hi + mul128_fold64(lo, hi));
+  }
+  if (L >= 4) {
+    const uint64_t in1 = static_cast<uint32_t>(win8(d0, d1, pb));
+    const uint64_t in2 = static_cast<uint32_t>(win8(d0, d1, pb + L - 4));
+    return rrmxmx((in2 + (in1 << 32)) ^ (sec64(8) ^ sec64(16)), L);
+  }
+  if (L) {
+    const uint32_t c1 = win1(d0, d1, pb), c2 = win1(d0, d1, pb + (L >> 1)),
+                   c3 = win1(d0, d1, pb + L - 1);
+    const uint32_t combined = (c1 << 16) | (c2 << 24) | c3 | (L << 8);
+    const uint32_t bf = static_cast<uint32_t>(sec64(0)) ^ static_cast<uint32_t>(sec64(4));
+    return xxh64_avalanche(static_cast<uint64_t>(combined ^ bf));
+  }
+  return xxh64_avalanche(sec64(56) ^ sec64(64));
+}
+
 struct LaneKeys {
   uint64_t k0, k1;    // accumulate keys for (stripe L/4, pair L%4)
   uint64_t kl0, kl1;  // last-stripe keys (XXH_SECRET_LASTACC_START = 7)
@@ -579,10 +678,18 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
   const uint32_t m = static_cast<uint32_t>(off & 3);
   const uint64_t q0 = (off & ~3ull) + 1024ull * P.g + 64 * s4 + 16 * p;
+  const bool shrt = valid && !lng;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    const bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
-    const uint64_t o = need ? q0 + 256 * k : 0;
+    bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
+    uint64_t o = need ? q0 + 256 * k : 0;
+    uint32_t mk = m;
+    if (k == 0 && shrt) {  // a short message's chunk (xxh3_short_row)
+      const uint64_t ph = short_phys(off, P.size, t);
+      need = true;
+      o = ph & ~3ull;
+      mk = static_cast<uint32_t>(ph & 3);
+    }
     const u32x4a4 v = ld16_a4(a.base + o);
     d.x[k][0] = v.x;
     d.x[k][1] = v.y;
@@ -590,7 +697,7 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
     d.x[k][3] = v.w;
     // the dword after the piece only matters for unaligned starts; then it
     // holds a message byte, so it never crosses into an unmapped page
-    d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
+    d.x[k][4] = ld4_a4(a.base + (need && mk ? o + 16 : o));
   }
   // the finishing step's words (last stripe, type byte / stored checksum,
   // modifier): loaded only in steps where some row of the wave finishes
@@ -612,9 +719,9 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
     // trailer without last_bytes[] only the type byte
     const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
     const uint64_t E = off + P.size;
-    const uint64_t t0 = (lastp && mem_last) ? (E & ~3ull) : 0;
+    const uint64_t t0 = ((lastp || shrt) && mem_last) ? (E & ~3ull) : 0;
     d.t0 = ld4v(a.base + t0);
-    d.t1 = MODE == kModeVerify ? ld4v(a.base + (lastp ? t0 + 4 : 0)) : 0u;
+    d.t1 = MODE == kModeVerify ? ld4v(a.base + ((lastp || shrt) ? t0 + 4 : 0)) : 0u;
     const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
     d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
     d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
@@ -625,7 +732,9 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kernel(BlockArgs a) {
   __shared__ uint64_t cold[4 * kColdN];
+  __shared__ uint64_t shsec[64];
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
+  short_secrets_fill(shsec, threadIdx.x);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
@@ -762,12 +871,13 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kern
       uint32_t stored = MODE == kModeVerify
                             ? (tb == 3 ? cu.t1 : __builtin_amdgcn_alignbyte(cu.t1, cu.t0, tb + 1))
                             : 0u;
-      if (fin && valid && !lng) {  // short input: the length-class formulas
-        const uint8_t* pp = a.base + off;
-        const uint64_t hs = xxh3_short(pp, C.size);
-        h = mk64(retire(static_cast<uint32_t>(hs)), retire(static_cast<uint32_t>(hs >> 32)));
-        if (MODE != kModeRaw) lastb = retire(ldu8(pp + C.size));
-        if (MODE == kModeVerify) stored = retire(ldu32(pp + C.size + 1));
+      if (__ballot(fin && valid && !lng)) {  // short inputs: the row's chunks
+        const uint64_t ph = short_phys(off, C.size, t);
+        uint64_t d0, d1;
+        xx_words(cu.x[0], static_cast<uint32_t>(ph & 3), d0, d1);
+        const uint32_t pb = static_cast<uint32_t>(off - short_phys(off, C.size, 0));
+        const uint64_t hs = xxh3_short_row(d0, d1, C.size, t, pb, shsec);
+        if (fin && valid && !lng) h = hs;
       }
       if (has_extra) lastb = cu.extra;
       const uint64_t i = kbeg + (C.rel == kNoMsg ? 0 : C.rel);
@@ -874,14 +984,19 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const bool lng = valid && P.size > 240;
   const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
   const uint32_t hs = P.hs();
+  const bool shrt = valid && !lng;  // one fragment (wal_hash.h gathers the others)
   uint32_t fm = 0;
   uint64_t alt_phys = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    const bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
+    bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
     const uint32_t ps = 1024u * P.g + 64 * s4 + 16 * p + 256 * k;
     const uint32_t jk = P.jc + (ps >= P.bn ? 1u : 0u);
-    const uint64_t phys = P0 + ps + static_cast<uint64_t>(hs) * jk;
+    uint64_t phys = P0 + ps + static_cast<uint64_t>(hs) * jk;
+    if (k == 0 && shrt) {  // a short record's chunk (xxh3_short_row)
+      need = true;
+      phys = short_phys(P0, P.size, t);
+    }
     const uint64_t o = need ? (phys & ~3ull) : 0;
     const uint32_t m = need ? static_cast<uint32_t>(phys & 3) : 0u;
     const u32x4a4 v = ld16_a4(a.base + o);
@@ -891,7 +1006,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
     d.x[k][3] = v.w;
     d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
     fm |= m << (2 * k);
-    const bool straddle = need && ps < P.bn && ps + 16 > P.bn;
+    const bool straddle = need && !shrt && ps < P.bn && ps + 16 > P.bn;
     if (straddle) {
       alt_phys = phys + hs;  // the bytes past the boundary: hs further on
       fm |= (1u << 8) | (k << 9) | ((P.bn - ps) << 11) | (static_cast<uint32_t>(alt_phys & 3) << 15);
@@ -931,8 +1046,10 @@ xxh3_frag_kernel(BlockArgs a) {
   // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
   __shared__ uint64_t cold[4 * kColdN];
   __shared__ uint64_t keys[24];
+  __shared__ uint64_t shsec[64];
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   if (threadIdx.x < 24) keys[threadIdx.x] = sec64(8 * threadIdx.x);
+  short_secrets_fill(shsec, threadIdx.x);
   __syncthreads();
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
@@ -1061,9 +1178,13 @@ xxh3_frag_kernel(BlockArgs a) {
         tm += shfl_xor64(tm, 2);
         h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
       }
-      if (fin && valid && !lng) {  // short record: one fragment, in place
-        const uint64_t hs2 = xxh3_short(a.base + C.off(), C.size);
-        h = mk64(retire(static_cast<uint32_t>(hs2)), retire(static_cast<uint32_t>(hs2 >> 32)));
+      if (__ballot(fin && valid && !lng)) {  // short records: the row's chunks
+        uint64_t d0, d1;
+        xx_words(cu.x[0], fm & 3u, d0, d1);
+        const uint64_t P0 = C.off();
+        const uint32_t pb = static_cast<uint32_t>(P0 - short_phys(P0, C.size, 0));
+        const uint64_t hs2 = xxh3_short_row(d0, d1, C.size, t, pb, shsec);
+        if (fin && valid && !lng) h = hs2;
       }
       if (fin && t == 0 && a.out64) a.out64[C.rel] = valid ? h : 0ull;
     }

@@ -307,6 +307,47 @@ def test_emu_wal_record_xxh3_fragment_edges(recyclable):
     assert (np.asarray(h).view(np.uint64) == W.expected_hashes(payload, lens)).all()
 
 
+def test_emu_xxh3_short_inputs_on_rows():
+    """every length 0..260 at every start alignment, and inputs ending in the
+    buffer's first 16 bytes (the <= 16-byte window is then loaded from 0):
+    the row-parallel short path (xxh3_short_row) in raw, compute and verify
+    modes"""
+    rng = np.random.default_rng(77)
+    sizes, offs = [], []
+    pos = 0
+    for o in range(16):  # at the buffer start
+        for L in (0, 1, 2, 3, 4, 7, 8, 9, 15, 16 - o if o < 16 else 1):
+            if o + L <= 16:
+                offs.append(o)
+                sizes.append(L)
+    pos = 64
+    for L in range(0, 261):
+        for m in range(4):
+            pos += m
+            offs.append(pos)
+            sizes.append(L)
+            pos += L + 5
+    sizes += [241, 1000, 5000]  # long ones in the same launch
+    for L in sizes[-3:]:
+        offs.append(pos)
+        pos += L + 5
+    offs = np.array(offs, np.uint64)
+    sizes = np.array(sizes, np.uint32)
+    base = rng.integers(0, 256, pos + 8192, dtype=np.uint8)
+    got = emu.xxh3(base, offs, sizes)
+    for k in range(len(offs)):
+        o, n = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.xxh3_64(base[o:o + n]), (k, o, n)
+    keep = offs >= 64  # block modes need the 5 trailer bytes in front of the next block
+    offs, sizes = offs[keep], sizes[keep]
+    want = O.block_checksum_batch(4, base, offs, sizes)
+    assert (emu.block_checksum(4, base, offs, sizes) == want).all()
+    types = rng.integers(0, 8, len(offs), dtype=np.uint8)
+    b2, out = emu.block_trailer(4, base, offs, sizes, types, None)
+    comp, st, ok, bad = emu.block_verify(4, b2, offs, sizes)
+    assert bad == 0 and (comp == out).all()
+
+
 def test_emu_rows_extra_dword_windows():
     """4096- and 1024·k-byte blocks at every start alignment: the rows kernel
     ends windows that are one dword longer than whole rounds one dword early

@@ -1,0 +1,11 @@
+#!/bin/bash
+# GPU parity after the rows slow-path / init changes, then C5 and C2
+set -eo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+OUT=gpurun_out/r02m
+mkdir -p "$OUT"
+timeout -k 10 600 python -u -m pytest -x -q --timeout 300 --timeout-method thread tests/test_gpu_parity.py tests/test_wal_recover.py tests/test_table_writer.py -m gpu > "$OUT/tests.log" 2>&1 || { tail -40 "$OUT/tests.log"; exit 1; }
+tail -2 "$OUT/tests.log"
+timeout -k 10 300 python -u tools/prof_wal.py > "$OUT/wal.json" 2> "$OUT/wal.err" || { tail -20 "$OUT/wal.err"; exit 1; }
+cat "$OUT/wal.json"
+bash tools/gpu_bench_cfgs.sh r02m C3 NS16X

@@ -11,7 +11,8 @@
 // of <= 240 bytes that span a block boundary, records whose last fragment is
 // under 64 bytes (the last stripe would straddle), fragment runs a writer
 // never produces -- are gathered into scratch (one workgroup per record) and
-// hashed there.  The accessor F describes a pipeline's fragments:
+// hashed there, as one compact batch.  The accessor F describes a
+// pipeline's fragments:
 //   F::begin(j), F::end(j)   fragment range of logical record j
 //   F::header(q)             log offset of fragment q's header
 //   F::use(q)                false: fragment q is not part of the record (the
@@ -80,14 +81,36 @@ __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F
   glen[j] = regular ? 0 : total;
 }
 
-// one workgroup per gathered record: its fragments back to back at dst + goff[j]
+__global__ void __launch_bounds__(kWhLanes) wh_flag_kernel(const uint64_t* glen, uint64_t n,
+                                                           uint64_t* flag) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (j < n) flag[j] = glen[j] ? 1u : 0u;
+}
+
+// the gathered records' compact list: list[gpos[j]] = j, with their scratch
+// offsets and lengths as descriptors of one XXH3 batch
+__global__ void __launch_bounds__(kWhLanes) wh_list_kernel(const uint64_t* glen,
+                                                           const uint64_t* goff,
+                                                           const uint64_t* gpos, uint64_t n,
+                                                           uint64_t* list, uint64_t* boff,
+                                                           uint32_t* blen) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (j >= n || glen[j] == 0) return;
+  const uint64_t i = gpos[j];
+  list[i] = j;
+  boff[i] = goff[j];
+  blen[i] = static_cast<uint32_t>(glen[j]);
+}
+
+// one workgroup per gathered record: its fragments back to back at dst + boff[i]
 template <class F>
-__global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log, F f, uint64_t n,
-                                                             const uint64_t* glen,
-                                                             const uint64_t* goff, uint8_t* dst) {
-  for (uint64_t j = blockIdx.x; j < n; j += gridDim.x) {
-    if (glen[j] == 0) continue;
-    uint8_t* d = dst + goff[j];
+__global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log, F f,
+                                                             const uint64_t* list,
+                                                             const uint64_t* boff, uint64_t ng,
+                                                             uint8_t* dst) {
+  for (uint64_t i = blockIdx.x; i < ng; i += gridDim.x) {
+    const uint64_t j = list[i];
+    uint8_t* d = dst + boff[i];
     for (uint64_t q = f.begin(j); q < f.end(j); ++q) {
       if (!f.use(q)) continue;
       const uint64_t h = f.header(q);
@@ -99,22 +122,14 @@ __global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log,
   }
 }
 
-__global__ void __launch_bounds__(kWhLanes) wh_gdesc_kernel(const uint64_t* glen,
-                                                            const uint64_t* goff, uint64_t n,
-                                                            uint64_t* off, uint32_t* len) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
-  if (j >= n) return;
-  off[j] = goff[j];
-  len[j] = static_cast<uint32_t>(glen[j]);
-}
-
 __global__ void __launch_bounds__(kWhLanes) wh_select_kernel(const uint64_t* glen,
+                                                             const uint64_t* gpos,
                                                              const uint64_t* ha,
                                                              const uint64_t* hb, uint64_t n,
                                                              uint64_t* out) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
   if (j >= n) return;
-  out[j] = glen[j] ? hb[j] : ha[j];
+  out[j] = glen[j] ? hb[gpos[j]] : ha[j];
 }
 
 inline size_t wh_up256(size_t b) { return (b + 255) & ~size_t(255); }
@@ -129,31 +144,39 @@ template <class F>
 hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f, uint64_t n,
                                 uint64_t* out, hipStream_t st, const char** name) {
   if (n == 0) return hipSuccess;
-  const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * (n / kScanTile + 2));
+  const uint64_t nt = n / kScanTile + 2;
+  const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * nt);
   void* scratch = nullptr;
-  hipError_t e = scratch_alloc(&scratch, 7 * s8 + 3 * s4 + st8, st);
+  hipError_t e = scratch_alloc(&scratch, 8 * s8 + 3 * s4 + 2 * st8, st);
   if (e != hipSuccess) return e;
   uint8_t* p = static_cast<uint8_t*>(scratch);
   uint64_t* p0 = reinterpret_cast<uint64_t*>(p);
   uint64_t* glen = reinterpret_cast<uint64_t*>(p + s8);
   uint64_t* goff = reinterpret_cast<uint64_t*>(p + 2 * s8);
-  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 3 * s8);
-  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 4 * s8);
-  uint64_t* boff = reinterpret_cast<uint64_t*>(p + 5 * s8);
-  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 7 * s8 + 3 * s4);
-  uint32_t* len = reinterpret_cast<uint32_t*>(p + 7 * s8);
-  uint32_t* info = reinterpret_cast<uint32_t*>(p + 7 * s8 + s4);
-  uint32_t* blen = reinterpret_cast<uint32_t*>(p + 7 * s8 + 2 * s4);
+  uint64_t* gpos = reinterpret_cast<uint64_t*>(p + 3 * s8);
+  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 4 * s8);
+  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 5 * s8);
+  uint64_t* list = reinterpret_cast<uint64_t*>(p + 6 * s8);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(p + 7 * s8);  // (reused as the flags)
+  uint32_t* len = reinterpret_cast<uint32_t*>(p + 8 * s8);
+  uint32_t* info = reinterpret_cast<uint32_t*>(p + 8 * s8 + s4);
+  uint32_t* blen = reinterpret_cast<uint32_t*>(p + 8 * s8 + 2 * s4);
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4);
+  uint64_t* tiles2 = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4 + st8);
   hipLaunchKernelGGL(wh_prep_kernel<F>, wh_grid(n), dim3(kWhLanes), 0, st, log, f, n, p0, len,
                      info, glen);
   scan_u64(glen, n, tiles, goff, st);
-  uint64_t gtotal = 0;
-  if ((e = hipMemcpyAsync(&gtotal, tiles + (n + kScanTile - 1) / kScanTile, 8,
-                          hipMemcpyDeviceToHost, st)) != hipSuccess ||
+  hipLaunchKernelGGL(wh_flag_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, n, boff);
+  scan_u64(boff, n, tiles2, gpos, st);
+  uint64_t tot[2] = {0, 0};  // gathered bytes, gathered records
+  const uint64_t ntl = (n + kScanTile - 1) / kScanTile;
+  if ((e = hipMemcpyAsync(&tot[0], tiles + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(&tot[1], tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
       (e = hipStreamSynchronize(st)) != hipSuccess) {
     (void)scratch_free(scratch, st);
     return e;
   }
+  const uint64_t gtotal = tot[0], ng = tot[1];
   // in place across the fragments (every record; gathered ones have length 0)
   BlockArgs fa{};
   fa.base = log;
@@ -165,28 +188,29 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
   fa.n = n;
   e = log_len >= 4096 ? launch_xxh3_frag(fa, st, name) : launch_xxh3_blocks(kModeRaw, fa, st, name);
   void* gbuf = nullptr;
-  if (e == hipSuccess && gtotal) {
+  if (e == hipSuccess && ng) {
     e = scratch_alloc(&gbuf, wh_up256(gtotal + 4096), st);
     if (e == hipSuccess) {
-      const uint32_t gg = static_cast<uint32_t>(n < 65536 ? n : 65536);
-      hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, st, log, f, n, glen,
-                         goff, static_cast<uint8_t*>(gbuf));
-      hipLaunchKernelGGL(wh_gdesc_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, goff, n, boff,
-                         blen);
-      BlockArgs ga = fa;
+      hipLaunchKernelGGL(wh_list_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, goff, gpos, n,
+                         list, boff, blen);
+      const uint32_t gg = static_cast<uint32_t>(ng < 65536 ? ng : 65536);
+      hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, st, log, f, list, boff,
+                         ng, static_cast<uint8_t*>(gbuf));
+      BlockArgs ga{};
       ga.base = static_cast<uint8_t*>(gbuf);
       ga.base_len = wh_up256(gtotal + 4096);
       ga.offsets = boff;
       ga.sizes = blen;
-      ga.init_crcs = nullptr;
       ga.out64 = hb;
+      ga.n = ng;
       const char* gname = nullptr;
       e = launch_xxh3_blocks(kModeRaw, ga, st, &gname);
     }
   }
   if (e == hipSuccess) {
-    if (gtotal) {
-      hipLaunchKernelGGL(wh_select_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, ha, hb, n, out);
+    if (ng) {
+      hipLaunchKernelGGL(wh_select_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, gpos, ha, hb,
+                         n, out);
       e = hipGetLastError();
     } else {
       e = hipMemcpyAsync(out, ha, 8 * n, hipMemcpyDeviceToDevice, st);

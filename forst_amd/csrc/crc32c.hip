@@ -1249,7 +1249,6 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
                                            uint64_t kbeg, CRStep& d) {
   const uint32_t t = lane & 15;
   const int64_t w0 = P.w0();
-  const uint32_t cA = P.cA(), tA = P.tA();
   if (PROBE == 3) {  // diagnostics: the same bytes as 16-B aligned, row-contiguous pieces
     const int64_t rb = (w0 & ~int64_t(15)) + static_cast<int64_t>(P.g) * kRowRound + 16 * t;
 #pragma unroll
@@ -1267,15 +1266,18 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
     d.t0 = d.t1 = d.t2 = d.mod = d.extra = 0u;
     return;
   }
+  // the lane's chain-0 segment; chain 1 is 512 bytes on.  Round-0 segments
+  // in front of the head hold no message byte: they are loaded from where
+  // they are and discarded by the head reset; only a segment in front of the
+  // buffer start (a message ending in its first KiB) is loaded from 0 (the
+  // head lane's is realigned by q dwords in the head step).  No branch: a
+  // step's loads must not depend on one, or the compiler's vmcnt waits for
+  // the current step's data also wait for the step in flight.
+  const int64_t rs = w0 + static_cast<int64_t>(P.g) * kRowRound + kSeg2 * t;
 #pragma unroll
   for (uint32_t c = 0; c < 2; ++c) {
-    int64_t so = w0 + static_cast<int64_t>(P.g) * kRowRound + kRowChain * c + kSeg2 * t;
-    // round 0: segments in front of the head hold no message byte (their
-    // words are zeroed), a head segment in front of the buffer is loaded
-    // from 0 and realigned
-    const bool pre = P.g == 0 && (c < cA || (c == cA && t < tA));
-    so = (pre || so < 0) ? 0 : so;
-    const uint8_t* sp = a.base + so;
+    const int64_t so = rs + kRowChain * c;
+    const uint8_t* sp = a.base + (so < 0 ? 0 : so);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const u32x4a4 v = ld16_a4(sp + 16 * q);
@@ -1286,31 +1288,36 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
     }
   }
   // the finishing step's words: tail dword at the window end (last round of a
-  // fast block), stored checksum, modifier / type byte / init -- loaded only
-  // in steps where some row of the wave finishes a block
+  // fast block), stored checksum, modifier / type byte / init.  Loaded in
+  // every step (from offset 0 when not needed): a step's load count must not
+  // depend on a branch, or the compiler's vmcnt waits for the current step's
+  // data also wait for the loads of the step in flight.
+  const uint32_t nt = P.nt();
   const bool lastr = !P.slow() && P.g + 1 >= P.R;
-  const bool fin = P.rel != kNoBlk && (P.slow() || lastr);
-  d.t0 = d.t1 = d.t2 = d.mod = d.extra = 0u;
-  if (__ballot(fin)) {
-    const uint32_t nt = P.nt();
-    const bool xt = MODE != kModeRaw && P.xtra();
-    const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
-    const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
-    const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
-    d.t0 = ld4v(a.base + t0);
-    // t1: the word after the tail (verify: stored checksum), else the extra
-    // window dword; t2: the extra window dword in verify mode
-    const uint64_t tx = lastr && xt ? wE : t0;
-    d.t1 = MODE == kModeRaw ? 0u
-                            : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
-    d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
-    const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
-    d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
-    if (MODE != kModeRaw && a.last_bytes) d.extra = a.last_bytes[idx];
-  }
-  // raw mode's per-message init: the head (round 0) and the slow path read it
-  if (MODE == kModeRaw && a.init_crcs && __ballot(P.rel != kNoBlk && (fin || P.g == 0)))
-    d.extra = a.init_crcs[kbeg + (P.rel == kNoBlk ? 0 : P.rel)];
+  const bool xt = MODE != kModeRaw && P.xtra();
+  const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
+  const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
+  const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
+  d.t0 = ld4v(a.base + t0);
+  // t1: the word after the tail (verify: stored checksum), else the extra
+  // window dword; t2: the extra window dword in verify mode
+  const uint64_t tx = lastr && xt ? wE : t0;
+  d.t1 = MODE == kModeRaw ? 0u
+                          : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
+  d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
+  // optional arrays: (read in the ISA) a branch around these loads keeps the
+  // compiler's vmcnt waits precise, a pointer select to a zero word does not
+  const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
+  if (MODE != kModeRaw)
+    d.mod = a.modifiers ? a.modifiers[idx] : 0u;
+  else
+    d.mod = 0u;
+  if (MODE == kModeRaw)
+    d.extra = a.init_crcs ? a.init_crcs[idx] : 0u;
+  else if (MODE != kModeVerify)
+    d.extra = a.last_bytes ? a.last_bytes[idx] : 0u;
+  else
+    d.extra = 0u;
 }
 
 // PROBE (diagnostics build only): 1 = same loads and row bookkeeping, no
@@ -1327,8 +1334,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15;
   const Lanes2 K = lanes2(lane);
-  const uint32_t s0c[4] = {uniform(kCrcS0[0]), uniform(kCrcS0[1]), uniform(kCrcS0[2]),
-                           uniform(kCrcS0[3])};
+  __shared__ uint32_t s0t[4];  // head states by start alignment (a select, not branches)
+  if (threadIdx.x < 4) s0t[threadIdx.x] = kCrcS0[threadIdx.x];
+  __syncthreads();
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * (DEPTH == 2 ? kRowsD2Waves : kWaves);
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * (DEPTH == 2 ? kRowsD2Waves : kWaves) + wave;
   const bool has_extra = (MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes;
@@ -1402,22 +1410,48 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     const bool fast = C.rel != kNoBlk && !C.slow();
     const bool r0 = C.g == 0;
     // ---- one 1 KiB round of every row ----
-    uint32_t w[2][8];
+    // A row at round 0 starts its block: its chain states start at 0 (J3(0) =
+    // 0), segments wholly in front of the head end the round at state 0, and
+    // in the head lane the running value is RESET at the head word to
+    // (word & bm) ^ S0 (the head dword without the bytes in front of the
+    // message, plus the initial state moved back over them), which discards
+    // whatever the words in front of it added.  Steps without a row at
+    // round 0 run the plain chains.
+    const bool head = PROBE == 0 && __ballot(fast && r0);
+    if (PROBE == 1 || PROBE == 3) {
 #pragma unroll
-    for (int c = 0; c < 2; ++c)
+      for (int c = 0; c < 2; ++c) {
+        uint32_t x = r0 ? 0u : s[c];
 #pragma unroll
-      for (int j = 0; j < 8; ++j) w[c][j] = cu.w[c][j];
-    if (PROBE != 1 && PROBE != 3 && __ballot(fast && r0)) {  // some row starts a block: its head
+        for (int j = 0; j < 8; ++j) x ^= cu.w[c][j];
+        s[c] = x;
+      }
+    } else if (!head) {
+#pragma unroll
+      for (int c = 0; c < 2; ++c) {
+        uint32_t lj[4], lg[4];
+        rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);
+        rep_look<false>(Lb, K, cu.w[c][0], lg);
+        uint32_t x = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]),
+                          xor3(lg[2], lg[3], cu.w[c][1]));
+#pragma unroll
+        for (int j = 2; j < 8; ++j) x = g_then(Lb, K, x, cu.w[c][j]);
+        s[c] = g_then(Lb, K, x, 0u);
+      }
+    } else {
       const uint32_t cA = C.cA(), tA = C.tA(), jA = C.jA(), q = C.q(), m = C.m();
       const uint32_t bm = 0xffffffffu << (8 * m);
       // raw mode with per-message inits: the GF(2) unstep; without (crc32c::Value,
       // every WAL record) S0 is the block modes' constant
-      const uint32_t S0 = MODE == kModeRaw && a.init_crcs
-                              ? unstep_m(~cu.extra, m)
-                              : (m == 0 ? s0c[0] : m == 1 ? s0c[1] : m == 2 ? s0c[2] : s0c[3]);
+      const uint32_t S0 = MODE == kModeRaw && a.init_crcs ? unstep_m(~cu.extra, m) : s0t[m];
 #pragma unroll
       for (uint32_t c = 0; c < 2; ++c) {
         const bool hl = fast && r0 && c == cA && t == tA;  // the head lane of the row
+        const bool pre = fast && r0 && (c < cA || (c == cA && t < tA));
+        const uint32_t hj = hl ? jA : 8u;
+        uint32_t wc[8];
+#pragma unroll
+        for (int j = 0; j < 8; ++j) wc[j] = cu.w[c][j];
         if (__ballot(hl && q != 0)) {  // head segment loaded from 0: shift up q dwords
           uint32_t sh[8];
 #pragma unroll
@@ -1425,43 +1459,25 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
             uint32_t v = 0;
 #pragma unroll
             for (int qq = 1; qq < 8; ++qq)
-              if (qq <= j) v = (q == static_cast<uint32_t>(qq)) ? w[c][j - qq] : v;
+              if (qq <= j) v = (q == static_cast<uint32_t>(qq)) ? wc[j - qq] : v;
             sh[j] = v;
           }
 #pragma unroll
-          for (int j = 0; j < 8; ++j) w[c][j] = (hl && q != 0) ? sh[j] : w[c][j];
+          for (int j = 0; j < 8; ++j) wc[j] = (hl && q != 0) ? sh[j] : wc[j];
         }
-        const uint32_t js = !(fast && r0) ? 0u
-                            : (c < cA || (c == cA && t < tA)) ? 8u
-                            : hl ? jA
-                                 : 0u;
+        uint32_t lj[4], lg[4];
+        rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);
+        rep_look<false>(Lb, K, hj == 0 ? ((wc[0] & bm) ^ S0) : wc[0], lg);
+        uint32_t x = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]),
+                          xor3(lg[2], lg[3], wc[1]));
+        x = hj == 1 ? ((wc[1] & bm) ^ S0) : x;
 #pragma unroll
-        for (uint32_t j = 0; j < 8; ++j) {
-          uint32_t v = j < js ? 0u : w[c][j];
-          v = (hl && j == jA) ? ((v & bm) ^ S0) : v;
-          w[c][j] = v;
+        for (uint32_t j = 2; j < 8; ++j) {
+          x = g_then(Lb, K, x, wc[j]);
+          x = hj == j ? ((wc[j] & bm) ^ S0) : x;
         }
+        s[c] = pre ? 0u : g_then(Lb, K, x, 0u);
       }
-    }
-    if (PROBE == 1 || PROBE == 3) {
-#pragma unroll
-      for (int c = 0; c < 2; ++c) {
-        uint32_t x = r0 ? 0u : s[c];
-#pragma unroll
-        for (int j = 0; j < 8; ++j) x ^= w[c][j];
-        s[c] = x;
-      }
-    }
-#pragma unroll
-    for (int c = 0; c < ((PROBE == 1 || PROBE == 3) ? 0 : 2); ++c) {
-      uint32_t lj[4], lg[4];
-      rep_look<true>(Lb, K, r0 ? 0u : s[c], lj);  // J3(0) = 0: a row at round 0 starts fresh
-      rep_look<false>(Lb, K, w[c][0], lg);
-      uint32_t x = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]),
-                        xor3(lg[2], lg[3], w[c][1]));
-#pragma unroll
-      for (int j = 2; j < 8; ++j) x = g_then(Lb, K, x, w[c][j]);
-      s[c] = g_then(Lb, K, x, 0u);
     }
     // ---- rows that finish a block in this step ----
     const bool fin = C.rel != kNoBlk && (C.slow() || C.g + 1 >= C.R);

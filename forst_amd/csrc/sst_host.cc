@@ -343,12 +343,15 @@ __attribute__((visibility("default"))) int forst_sst_properties_decode(const uin
 namespace forstdb {
 namespace {
 
-// Status::CopyAppendMessage(s, " in ", file) of ReadFooterFromFile and the
-// block readers (format.cc:548-551)
-Status from_sst_rc(int rc, const std::string& file) {
+// Footer errors carry Status::CopyAppendMessage(s, " in ", file) of
+// ReadFooterFromFile (format.cc:548-551); errors of the block iterators that
+// parse the metaindex, properties and index blocks do not (block.h:559
+// CorruptionError, "bad entry in block"; block.cc:1242 "bad block contents")
+Status from_sst_rc(int rc, const std::string& file, bool in_file = true) {
+  const std::string sfx = in_file ? " in " + file : std::string();
   if (rc == kTooShort) return Status::Corruption(g_sst_err + file);
-  if (rc == FORST_ECORRUPT) return Status::Corruption(g_sst_err + " in " + file);
-  if (rc == FORST_EUNSUPPORTED) return Status::NotSupported(g_sst_err + " in " + file);
+  if (rc == FORST_ECORRUPT) return Status::Corruption(g_sst_err + sfx);
+  if (rc == FORST_EUNSUPPORTED) return Status::NotSupported(g_sst_err + sfx);
   return Status::InvalidArgument("forst_sst: " + std::to_string(rc));
 }
 
@@ -497,7 +500,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   if (!s.ok()) return s;
   std::vector<MetaEntry> meta;
   rc = metaindex_entries(host_file + mi.off, mi.size, &meta);
-  if (rc) return from_sst_rc(rc, file_name);
+  if (rc) return from_sst_rc(rc, file_name, false);
   // 3. properties (ReadTablePropertiesHelper) and the index handle (fv >= 6)
   forst_sst_properties props;
   std::memset(&props, 0, sizeof(props));
@@ -510,7 +513,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       s = host_block(e.h, "properties");
       if (!s.ok()) return s;
       rc = properties(host_file + e.h.off, e.h.size, &props);
-      if (rc) return from_sst_rc(rc, file_name);
+      if (rc) return from_sst_rc(rc, file_name, false);
       s = verify({e.h}, nullptr);
       if (s.IsCorruption() && props.global_seqno_value_offset != 0 &&
           props.global_seqno_value_offset + 8 <= e.h.size) {
@@ -538,7 +541,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   const bool first_key = props.index_type == 3;  // kBinarySearchWithFirstKey
   std::vector<Handle> top, data;
   rc = index_handles(host_file + ix.off, ix.size, delta, first_key, &top);
-  if (rc) return from_sst_rc(rc, file_name);
+  if (rc) return from_sst_rc(rc, file_name, false);
   if (props.index_type == 2) {  // kTwoLevelIndexSearch: top level -> partitions
     rep.index_partitions = top.size();
     s = verify(top, nullptr);
@@ -547,7 +550,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       s = host_block(p, "index partition");
       if (!s.ok()) return s;
       rc = index_handles(host_file + p.off, p.size, delta, first_key, &data);
-      if (rc) return from_sst_rc(rc, file_name);
+      if (rc) return from_sst_rc(rc, file_name, false);
     }
   } else {
     data.swap(top);

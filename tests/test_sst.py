@@ -292,9 +292,21 @@ def test_ingested_global_seqno_rewrite_still_verifies():
         b[at:at + 8] = struct.pack("<Q", 123456789)  # the ingested file's global seqno
         r = sst.verify_file(bytes(b), file_name=name)
         assert r.status == 0, r.message
-        b[po + 2] ^= 0x40  # any other byte of the block still fails
-        r = sst.verify_file(bytes(b), file_name=name)
-        assert r.status == 2 and b"block checksum mismatch" in r.message
+        blk = bytes(b[po:po + pn])
+        cmp_at = po + blk.index(b"leveldb.BytewiseComparator") + 3
+        b2 = bytearray(b)
+        b2[cmp_at] ^= 0x40  # any other byte of the block still fails its checksum
+        r = sst.verify_file(bytes(b2), file_name=name)
+        assert r.status == 2 and b"block checksum mismatch" in r.message, r.message
+        # an entry that no longer parses: the block iterator's error, which
+        # carries no file name (block.h:559 CorruptionError; the properties are
+        # decoded before their checksum, meta_blocks.cc:256-262)
+        b3 = bytearray(b)
+        b3[po + 1] = 0xFF  # first entry's non_shared varint: runs past the block
+        b3[po + 2] = 0xFF
+        b3[po + 3] = 0x7F
+        r = sst.verify_file(bytes(b3), file_name=name)
+        assert r.status == 2 and r.message == b"Corruption: bad entry in block", r.message
 
 
 @pytest.mark.gpu

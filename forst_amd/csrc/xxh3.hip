@@ -700,33 +700,30 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
     d.x[k][4] = ld4_a4(a.base + (need && mk ? o + 16 : o));
   }
   // the finishing step's words (last stripe, type byte / stored checksum,
-  // modifier): loaded only in steps where some row of the wave finishes
+  // modifier), loaded in every step (from offset 0 when not needed): a
+  // step's load count must not depend on a branch, or the compiler's vmcnt
+  // waits for the current step's data also wait for the step in flight
   const bool lastp = lng && P.g == nb;
-  const bool fin = P.rel != kNoMsg && (!lng || P.g == nb);
-  d.l[0] = d.l[1] = d.l[2] = d.l[3] = d.l[4] = 0u;
-  d.t0 = d.t1 = d.mod = d.extra = 0u;
-  if (__ballot(fin)) {
-    const uint64_t lq = off + P.size - 64 + 16 * p;
-    const uint32_t ml = static_cast<uint32_t>(lq & 3);
-    const uint64_t lo = lastp ? (lq & ~3ull) : 0;
-    const u32x4a4 v = ld16_a4(a.base + lo);
-    d.l[0] = v.x;
-    d.l[1] = v.y;
-    d.l[2] = v.z;
-    d.l[3] = v.w;
-    d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
-    // type byte at E = off + size, stored LE32 at E + 1 (verify); for compute /
-    // trailer without last_bytes[] only the type byte
-    const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
-    const uint64_t E = off + P.size;
-    const uint64_t t0 = ((lastp || shrt) && mem_last) ? (E & ~3ull) : 0;
-    d.t0 = ld4v(a.base + t0);
-    d.t1 = MODE == kModeVerify ? ld4v(a.base + ((lastp || shrt) ? t0 + 4 : 0)) : 0u;
-    const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
-    d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
-    d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
-                                                                                : 0u;
-  }
+  const uint64_t lq = off + P.size - 64 + 16 * p;
+  const uint32_t ml = static_cast<uint32_t>(lq & 3);
+  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+  const u32x4a4 v = ld16_a4(a.base + lo);
+  d.l[0] = v.x;
+  d.l[1] = v.y;
+  d.l[2] = v.z;
+  d.l[3] = v.w;
+  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+  // type byte at E = off + size, stored LE32 at E + 1 (verify); for compute /
+  // trailer without last_bytes[] only the type byte
+  const bool mem_last = MODE == kModeVerify || (MODE != kModeRaw && !a.last_bytes);
+  const uint64_t E = off + P.size;
+  const uint64_t t0 = ((lastp || shrt) && mem_last) ? (E & ~3ull) : 0;
+  d.t0 = ld4v(a.base + t0);
+  d.t1 = MODE == kModeVerify ? ld4v(a.base + ((lastp || shrt) ? t0 + 4 : 0)) : 0u;
+  const uint64_t idx = kbeg + (P.rel == kNoMsg ? 0 : P.rel);
+  d.mod = (MODE != kModeRaw && a.modifiers) ? a.modifiers[idx] : 0u;
+  d.extra = ((MODE == kModeCompute || MODE == kModeTrailer) && a.last_bytes) ? a.last_bytes[idx]
+                                                                              : 0u;
 }
 
 template <int MODE>
@@ -1020,21 +1017,18 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   d.alt[3] = av.w;
   d.alt[4] = ld4_a4(a.base + ((fm >> 8) & 1u ? ao + 16 : ao));
   d.fm = fm;
-  // last stripe at L - 64, inside the last fragment (fragment j_last): only
-  // in steps where some row of the wave finishes a long record
+  // last stripe at L - 64, inside the last fragment (fragment j_last); loaded
+  // in every step (at 0 when not needed: see rows_issue)
   const bool lastp = lng && P.g == nb;
-  d.l[0] = d.l[1] = d.l[2] = d.l[3] = d.l[4] = 0u;
-  if (__ballot(lastp)) {
-    const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
-    const uint64_t lo = lastp ? (lq & ~3ull) : 0;
-    const uint32_t ml = static_cast<uint32_t>(lq & 3);
-    const u32x4a4 lv = ld16_a4(a.base + lo);
-    d.l[0] = lv.x;
-    d.l[1] = lv.y;
-    d.l[2] = lv.z;
-    d.l[3] = lv.w;
-    d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
-  }
+  const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
+  const uint32_t ml = static_cast<uint32_t>(lq & 3);
+  const u32x4a4 lv = ld16_a4(a.base + lo);
+  d.l[0] = lv.x;
+  d.l[1] = lv.y;
+  d.l[2] = lv.z;
+  d.l[3] = lv.w;
+  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
 }
 
 // WPE: waves per SIMD the register allocation targets (3, the default: 168

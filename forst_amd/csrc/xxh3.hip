@@ -1050,7 +1050,8 @@ xxh3_frag_kernel(BlockArgs a) {
   const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
   const uint64_t* ck = cold + kColdN * p;
   // K0[k] = keys[s4 + 2p + 4k], K1[k] = keys[s4 + 2p + 4k + 1]
-  const uint64_t ks0 = sec64(128 + 16 * p), ks1 = sec64(136 + 16 * p);
+  // (the scramble keys sec64(128 + 16p), sec64(136 + 16p) are keys[16 + 2p],
+  // keys[17 + 2p], read where used: one spilled register pair fewer)
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
   BatchFeed feed;
@@ -1155,8 +1156,8 @@ xxh3_frag_kernel(BlockArgs a) {
     acc1 += sum1;
     const bool full = C.g < nbC;
     if (full) {
-      acc0 = scramble(acc0, ks0);
-      acc1 = scramble(acc1, ks1);
+      acc0 = scramble(acc0, kq[16 - s4]);  // keys[16 + 2p] (kq = keys + s4 + 2p)
+      acc1 = scramble(acc1, kq[17 - s4]);
     }
     const bool fin = C.rel != kNoMsg && !(lng && full);
     if (__ballot(fin)) {

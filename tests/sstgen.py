@@ -1,13 +1,15 @@
 """tests/sstgen.py -- TEST INFRASTRUCTURE ONLY: writes SST files in the
 block-based table format for the whole-file verify tests.
 
-A restatement of the reference's WRITER side (parity unpinned at the file
-level: the reference SST builder does not compile from a few source files --
-FooterBuilder needs the magic-number definitions of
-block_based_table_builder.cc / plain_table_builder.cc and BlockBuilder needs
-db/dbformat.cc and monitoring/perf_context.cc -- so no reference-written SST
-can be produced here; block checksums themselves are the oracle's, which is
-pinned to the reference vectors).  Followed:
+Layout follows the reference writer (file:line below).  Every encoding goes
+through a codec: PyCodec is this file's restatement; tests/golden/
+gen_sst_golden.py runs the SAME writer with a codec that calls the
+reference's own BlockBuilder, BlockHandle / IndexValue encoders,
+PropertyBlockBuilder, MetaIndexBuilder, FooterBuilder and
+ComputeBuiltinChecksumWithLastByte + ChecksumModifierForContext (compiled
+from /root/reference, tests/golden/ref_sst_shim.cc) and commits the files as
+tests/golden/sst/*.sst -- tests/test_sst_pinned.py checks that PyCodec writes
+them byte for byte, which pins every file this module writes.  Followed:
   BlockBuilder            table/block_based/block_builder.cc:46-260
   IndexValue / handles    table/format.cc:60-121
   ShortenedIndexBuilder   table/block_based/index_builder.h:184-264
@@ -17,6 +19,8 @@ pinned to the reference vectors).  Followed:
   Finish() order          block_based_table_builder.cc:1966-2024
   FooterBuilder::Build    table/format.cc:230-351
   trailer                 block_based_table_builder.cc:1311-1360
+The block ORDER and which properties are written are this writer's choice
+(a subset of the reference's properties); the encodings are pinned.
 """
 import struct
 
@@ -78,12 +82,67 @@ class BlockBuilder:
         return out + struct.pack("<I", len(self.restarts))
 
 
+class PyCodec:
+    """the encodings, restated (tests/golden/gen_sst_golden.py has the
+    reference-backed twin)"""
+
+    def block(self, restart_interval, delta_keys, value_delta, entries):
+        b = BlockBuilder(restart_interval, delta_keys, value_delta)
+        for key, value, delta in entries:
+            b.add(key, value, delta)
+        return b.finish()
+
+    def handle(self, off, n):
+        return handle(off, n)
+
+    def index_value(self, off, n, first_key, have_first_key, prev):
+        """IndexValue::EncodeTo: full (prev None) or delta-encoded"""
+        if prev is None:
+            out = handle(off, n)
+        else:
+            out = varint(zigzag(n - prev[1]))
+        if have_first_key:
+            out += varint(len(first_key)) + first_key
+        return out
+
+    def properties(self, props):
+        """props: (name, "u64" | "str", value); sorted, restart INT_MAX"""
+        return self.block(2**31 - 1, True, False,
+                          [(k, varint(v) if kind == "u64" else v, None)
+                           for k, kind, v in sorted(props)])
+
+    def metaindex(self, entries):
+        """entries: (name, (offset, size)); sorted, restart 1"""
+        return self.block(1, True, False, [(k, handle(*h), None) for k, h in sorted(entries)])
+
+    def trailer(self, ctype, contents, ctype_byte, bcc, off):
+        c = O.compute_builtin_checksum_with_last_byte(ctype, contents, ctype_byte)
+        c = (c + O.checksum_modifier_for_context(bcc, off)) & 0xFFFFFFFF
+        return bytes([ctype_byte]) + struct.pack("<I", c)
+
+    def footer(self, fv, ctype, footer_offset, mi, ix, bcc):  # FooterBuilder::Build
+        if fv == 0:
+            part2 = handle(*mi) + handle(*ix)
+            return part2 + bytes(40 - len(part2)) + struct.pack("<Q", LEGACY_MAGIC)
+        part3 = struct.pack("<IQ", fv, MAGIC)
+        if fv < 6:
+            part2 = handle(*mi) + handle(*ix)
+            return bytes([ctype]) + part2 + bytes(40 - len(part2)) + part3
+        body = bytearray(bytes([ctype]) + EXT_MAGIC + struct.pack("<III", 0, bcc, mi[1])
+                         + bytes(24) + part3)
+        c = O.compute_builtin_checksum(ctype, bytes(body))
+        c = (c + O.checksum_modifier_for_context(bcc, footer_offset)) & 0xFFFFFFFF
+        body[5:9] = struct.pack("<I", c)
+        return bytes(body)
+
+
 class SstWriter:
     """kinds of the recorded blocks: data, filter, index, partition, properties,
     metaindex"""
 
     def __init__(self, fv=5, ctype=1, index_type=0, base_context=0, restart_interval=1,
-                 seed=1):
+                 seed=1, codec=None):
+        self.codec = codec or PyCodec()
         self.fv, self.ctype, self.index_type = fv, ctype, index_type
         self.bcc = base_context if fv >= 6 else 0
         self.ri = restart_interval
@@ -95,35 +154,33 @@ class SstWriter:
     def write_block(self, contents, kind, ctype_byte=0):
         off = len(self.f)
         n = len(contents)
-        c = O.compute_builtin_checksum_with_last_byte(self.ctype, contents, ctype_byte)
-        c = (c + O.checksum_modifier_for_context(self.bcc, off)) & 0xFFFFFFFF
-        self.f += contents + bytes([ctype_byte]) + struct.pack("<I", c)
+        self.f += contents + self.codec.trailer(self.ctype, contents, ctype_byte, self.bcc, off)
         self.blocks.append((kind, off, n))
         return off, n
 
     def data_block(self, nkeys, first):
-        b = BlockBuilder(16)
+        ents = []
         keys = []
         for k in range(nkeys):
             key = b"user%010d" % (first + k) + struct.pack("<Q", (first + k) << 8 | 1)
             val = self.rng.integers(0, 256, int(self.rng.integers(10, 300)), np.uint8).tobytes()
-            b.add(key, val)
+            ents.append((key, val, None))
             keys.append(key)
-        return b.finish(), keys
+        return self.codec.block(16, True, False, ents), keys
 
-    def _index_entries(self, builder, entries):
+    def _index_block(self, entries, first_keys):
+        """an index block (ShortenedIndexBuilder / a partition): separator ->
+        IndexValue, delta-encoded after the first entry when the format
+        version has value delta encoding"""
+        ents = []
         prev = None
         for sep, (off, n), first_key in entries:
-            full = handle(off, n)
-            if self.index_type == 3:
-                full += varint(len(first_key)) + first_key
-            delta = None
-            if prev is not None:
-                delta = varint(zigzag(n - prev[1]))
-                if self.index_type == 3:
-                    delta += varint(len(first_key)) + first_key
-            builder.add(sep, full, delta)
+            full = self.codec.index_value(off, n, first_key, first_keys, None)
+            delta = (self.codec.index_value(off, n, first_key, first_keys, prev)
+                     if prev is not None else None)
+            ents.append((sep, full, delta))
             prev = (off, n)
+        return self.codec.block(self.ri, True, self.value_delta, ents)
 
     def build(self, n_data=40, filter_block=True, partition_size=8, compress_type_bytes=None,
               external=False):
@@ -145,63 +202,36 @@ class SstWriter:
             parts = [entries[i:i + partition_size] for i in range(0, len(entries), partition_size)]
             tops = []
             for p in parts:
-                pb = BlockBuilder(self.ri, True, self.value_delta)
-                self._index_entries(pb, p)
-                tops.append((p[-1][0], self.write_block(pb.finish(), "partition"), b""))
-            tb = BlockBuilder(self.ri, True, self.value_delta)
-            saved, self.index_type = self.index_type, 0
-            self._index_entries(tb, tops)
-            self.index_type = saved
-            ix = self.write_block(tb.finish(), "index")
+                tops.append((p[-1][0], self.write_block(self._index_block(p, False), "partition"),
+                             b""))
+            ix = self.write_block(self._index_block(tops, False), "index")
         else:
-            ib = BlockBuilder(self.ri, True, self.value_delta)
-            self._index_entries(ib, entries)
-            ix = self.write_block(ib.finish(), "index")
+            ix = self.write_block(self._index_block(entries, self.index_type == 3), "index")
         if self.fv >= 6:
             meta[b"rocksdb.index"] = ix
         # properties (sorted, restart interval INT_MAX)
-        props = {
-            b"rocksdb.block.based.table.index.type": struct.pack("<I", self.index_type),
-            b"rocksdb.index.value.is.delta.encoded": varint(1 if self.value_delta else 0),
-            b"rocksdb.index.key.is.user.key": varint(0),
-            b"rocksdb.num.data.blocks": varint(n_data),
-            b"rocksdb.format.version": varint(self.fv),
-            b"rocksdb.data.size": varint(entries[-1][1][0] + entries[-1][1][1] + 5),
-            b"rocksdb.comparator": b"leveldb.BytewiseComparator",
-            b"rocksdb.column.family.name": b"",
-        }
+        props = [
+            # (BlockBasedTablePropertiesCollector, block_based_table_builder.cc:226-262)
+            (b"rocksdb.block.based.table.index.type", "str", struct.pack("<I", self.index_type)),
+            (b"rocksdb.index.value.is.delta.encoded", "u64", 1 if self.value_delta else 0),
+            (b"rocksdb.index.key.is.user.key", "u64", 0),
+            (b"rocksdb.num.data.blocks", "u64", n_data),
+            (b"rocksdb.format.version", "u64", self.fv),
+            (b"rocksdb.data.size", "u64", entries[-1][1][0] + entries[-1][1][1] + 5),
+            (b"rocksdb.comparator", "str", b"leveldb.BytewiseComparator"),
+            (b"rocksdb.column.family.name", "str", b""),
+        ]
         if self.index_type == 2:
-            props[b"rocksdb.index.partitions"] = varint(len(parts))
+            props.append((b"rocksdb.index.partitions", "u64", len(parts)))
         if external:  # SstFileWriter's collector (sst_file_writer_collectors.h): version 2, seqno 0
-            props[b"rocksdb.external_sst_file.version"] = struct.pack("<I", 2)
-            props[b"rocksdb.external_sst_file.global_seqno"] = struct.pack("<Q", 0)
-        pbld = BlockBuilder(2**31 - 1)
-        for name in sorted(props):
-            pbld.add(name, props[name])
-        meta[b"rocksdb.properties"] = self.write_block(pbld.finish(), "properties")
-        mb = BlockBuilder(1)
-        for name in sorted(meta):
-            mb.add(name, handle(*meta[name]))
-        mi = self.write_block(mb.finish(), "metaindex")
+            props.append((b"rocksdb.external_sst_file.version", "str", struct.pack("<I", 2)))
+            props.append((b"rocksdb.external_sst_file.global_seqno", "str", struct.pack("<Q", 0)))
+        meta[b"rocksdb.properties"] = self.write_block(self.codec.properties(props), "properties")
+        mi = self.write_block(self.codec.metaindex(list(meta.items())), "metaindex")
         self.meta_names = sorted(meta)
         self.footer_offset = len(self.f)
-        self.f += self.footer(mi, ix)
+        self.f += self.codec.footer(self.fv, self.ctype, self.footer_offset, mi, ix, self.bcc)
         return bytes(self.f)
-
-    def footer(self, mi, ix):  # FooterBuilder::Build, format.cc:230-351
-        if self.fv == 0:
-            part2 = handle(*mi) + handle(*ix)
-            return part2 + bytes(40 - len(part2)) + struct.pack("<Q", LEGACY_MAGIC)
-        part3 = struct.pack("<IQ", self.fv, MAGIC)
-        if self.fv < 6:
-            part2 = handle(*mi) + handle(*ix)
-            return bytes([self.ctype]) + part2 + bytes(40 - len(part2)) + part3
-        body = bytearray(bytes([self.ctype]) + EXT_MAGIC + struct.pack("<III", 0, self.bcc, mi[1])
-                         + bytes(24) + part3)
-        c = O.compute_builtin_checksum(self.ctype, bytes(body))
-        c = (c + O.checksum_modifier_for_context(self.bcc, self.footer_offset)) & 0xFFFFFFFF
-        body[5:9] = struct.pack("<I", c)
-        return bytes(body)
 
     def verify_order(self):
         """(offset, size) in the order VerifyChecksum checks them: meta blocks

@@ -8,7 +8,8 @@ GPU: forst_sst_verify_file over whole files -- every checksum on the device
 -- returns OK with the right block counts, and for injected corruption the
 reference's exact Status text of the first failing block.
 
-File-level layout parity is unpinned (tests/sstgen.py header); every block
+The layout of the files tests/sstgen.py writes is pinned to the reference's
+own writer code (tests/test_sst_pinned.py, tests/golden/sst); every block
 checksum is pinned through the oracle."""
 import struct
 

@@ -9,11 +9,9 @@ the reference vectors).  fv 0-6 x all five ChecksumTypes x index types, tiny
 windows (many GPU launches, both windows alternating) and the default window,
 block_align padding, and a 20 000-block fv6 stream against the oracle.
 
-File layout parity beyond the checksums is unpinned: the reference writer
-(BlockBasedTableBuilder, FooterBuilder) cannot be built here -- its objects
-pull in ObjectRegistry, whose builtins_ table lives in util/build_version.cc,
-generated from build_version.cc.in by the reference's build system
-(DESIGN.md §5)."""
+The file layout is pinned: tests/sstgen.py writes the reference-encoded files
+of tests/golden/sst byte for byte (tests/test_sst_pinned.py, which also
+rewrites those files through this writer)."""
 import struct
 
 import numpy as np

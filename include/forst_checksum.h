@@ -54,8 +54,11 @@
  *    memory pool with stream-ordered alloc/free and is zeroed with
  *    hipMemsetAsync.  No call copies to the host or synchronises except
  *    forst_wal_verify_batch, forst_wal_record_xxh3_batch and
- *    forst_wal_recover_batch (each reads a record count back once) and the
- *    explicitly synchronous host-memory / SST-file entry points below.
+ *    forst_wal_recover_batch, which read counts back (1, 2 and 4 stream
+ *    synchronisations per call: record total; logical records + gathered
+ *    bytes; items, tokens, emitted counts, gathered bytes), and the
+ *    explicitly synchronous host-memory / SST-file / table-writer entry
+ *    points below.
  *  - `base` must be 4-byte aligned; blocks live at base + offsets[i] and may
  *    start at any byte (SST blocks are packed back-to-back with 5-byte
  *    trailers, so starts are unaligned).  base_len bounds every access: a
@@ -64,8 +67,10 @@
  *  - Per-block checksum mismatch is data, not an error.  Return values are
  *    FORST_OK or a negative FORST_E* code for invalid arguments / HIP errors.
  *  - Thread safety: every entry point is reentrant; concurrent calls on
- *    different streams are independent (no global mutable state besides the
- *    immutable per-device table cache set up by forst_init_device()).
+ *    different streams are independent.  Shared state: the immutable
+ *    per-device table cache set up by forst_init_device() and the per-device
+ *    stream-ordered scratch pool (hipMemPool, thread-safe); error messages
+ *    are thread-local.
  */
 #ifndef FORST_CHECKSUM_H_
 #define FORST_CHECKSUM_H_

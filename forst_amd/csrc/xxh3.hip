@@ -430,13 +430,11 @@ __device__ __forceinline__ void xx_issue(const uint8_t* __restrict__ base, uint3
 
 __device__ __forceinline__ void xx_words(const uint32_t (&x)[5], uint32_t m, uint64_t& d0,
                                          uint64_t& d1) {
-  uint32_t x0 = x[0], x1 = x[1], x2 = x[2], x3 = x[3];
-  if (m) {
-    x0 = __builtin_amdgcn_alignbyte(x[1], x[0], m);
-    x1 = __builtin_amdgcn_alignbyte(x[2], x[1], m);
-    x2 = __builtin_amdgcn_alignbyte(x[3], x[2], m);
-    x3 = __builtin_amdgcn_alignbyte(x[4], x[3], m);
-  }
+  // v_alignbyte_b32 by 0 returns the low word: no branch on m
+  const uint32_t x0 = __builtin_amdgcn_alignbyte(x[1], x[0], m);
+  const uint32_t x1 = __builtin_amdgcn_alignbyte(x[2], x[1], m);
+  const uint32_t x2 = __builtin_amdgcn_alignbyte(x[3], x[2], m);
+  const uint32_t x3 = __builtin_amdgcn_alignbyte(x[4], x[3], m);
   d0 = mk64(x0, x1);
   d1 = mk64(x2, x3);
 }
@@ -982,40 +980,59 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
   const uint32_t hs = P.hs();
   const bool shrt = valid && !lng;  // one fragment (wal_hash.h gathers the others)
+  // Chunk k of the lane sits at window offset lof + 256k, logical offset
+  // wpos + lof + 256k; it lies past the window's boundary (hs bytes further on)
+  // iff 256k >= dl.  bn >= wpos always (frow_next), so dl fits in 32 bits.  All
+  // chunks share two physical frames: B (before the boundary) and B + hs;
+  // their dword-aligned starts differ by dA, so every load address is the
+  // lane's frame pointer R plus a small 32-bit offset (no per-chunk 64-bit
+  // multiply-add), and a chunk that is not needed loads from the buffer start.
+  const uint32_t lof = 64 * s4 + 16 * p;
+  const uint32_t wpos = 1024u * P.g;
+  const uint32_t dw = P.bn - wpos;
+  const int32_t dl = static_cast<int32_t>(dw < 2048u ? dw : 2048u) - static_cast<int32_t>(lof);
+  const uint64_t B = P0 + wpos + lof + static_cast<uint64_t>(hs) * P.jc;
+  const uint32_t m0 = static_cast<uint32_t>(B) & 3u;
+  const uint32_t m1 = (static_cast<uint32_t>(B) + hs) & 3u;
+  const uint32_t dA = ((static_cast<uint32_t>(B) + hs) & ~3u) - (static_cast<uint32_t>(B) & ~3u);
+  const uint8_t* R = a.base + (B & ~3ull);
+  const uint32_t lim = P.g < nb ? 4u : (nbS > s4 ? (nbS - s4 + 3) >> 2 : 0u);  // chunks k < lim
   uint32_t fm = 0;
-  uint64_t alt_phys = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    bool need = lng && (P.g < nb || s4 + 4 * k < nbS);
-    const uint32_t ps = 1024u * P.g + 64 * s4 + 16 * p + 256 * k;
-    const uint32_t jk = P.jc + (ps >= P.bn ? 1u : 0u);
-    uint64_t phys = P0 + ps + static_cast<uint64_t>(hs) * jk;
-    if (k == 0 && shrt) {  // a short record's chunk (xxh3_short_row)
-      need = true;
-      phys = short_phys(P0, P.size, t);
+    const bool past = static_cast<int32_t>(256 * k) >= dl;
+    const bool need = lng && k < lim;
+    const uint8_t* q = R + (256 * k + (past ? dA : 0u));
+    const uint32_t m = past ? m1 : m0;
+    const uint8_t* pq = need ? q : a.base;
+    const uint8_t* pq4 = need && m ? q + 16 : pq;
+    uint32_t mm = need ? m : 0u;
+    if (k == 0) {  // a short record's chunk (xxh3_short_row)
+      const uint64_t sp = short_phys(P0, P.size, t);
+      pq = shrt ? a.base + (sp & ~3ull) : pq;
+      mm = shrt ? static_cast<uint32_t>(sp) & 3u : mm;
+      pq4 = shrt && mm ? pq + 16 : (shrt ? pq : pq4);
     }
-    const uint64_t o = need ? (phys & ~3ull) : 0;
-    const uint32_t m = need ? static_cast<uint32_t>(phys & 3) : 0u;
-    const u32x4a4 v = ld16_a4(a.base + o);
+    const u32x4a4 v = ld16_a4(pq);
     d.x[k][0] = v.x;
     d.x[k][1] = v.y;
     d.x[k][2] = v.z;
     d.x[k][3] = v.w;
-    d.x[k][4] = ld4_a4(a.base + (need && m ? o + 16 : o));
-    fm |= m << (2 * k);
-    const bool straddle = need && !shrt && ps < P.bn && ps + 16 > P.bn;
-    if (straddle) {
-      alt_phys = phys + hs;  // the bytes past the boundary: hs further on
-      fm |= (1u << 8) | (k << 9) | ((P.bn - ps) << 11) | (static_cast<uint32_t>(alt_phys & 3) << 15);
-    }
+    d.x[k][4] = ld4_a4(pq4);
+    fm |= mm << (2 * k);
   }
-  const uint64_t ao = (fm >> 8) & 1u ? (alt_phys & ~3ull) : 0;
-  const u32x4a4 av = ld16_a4(a.base + ao);
+  // the one chunk of the lane that straddles the boundary (0 < dl - 256k < 16)
+  // takes the bytes past it from the shifted frame: the same chunk hs on
+  const uint32_t ks = static_cast<uint32_t>(dl) >> 8, cut = static_cast<uint32_t>(dl) & 255u;
+  const bool straddle = lng && dl > 0 && dl < 1024 && cut != 0 && cut < 16 && ks < lim;
+  const uint8_t* qa = straddle ? R + (256 * ks + dA) : a.base;
+  const u32x4a4 av = ld16_a4(qa);
   d.alt[0] = av.x;
   d.alt[1] = av.y;
   d.alt[2] = av.z;
   d.alt[3] = av.w;
-  d.alt[4] = ld4_a4(a.base + ((fm >> 8) & 1u ? ao + 16 : ao));
+  d.alt[4] = ld4_a4(straddle && m1 ? qa + 16 : qa);
+  if (straddle) fm |= (1u << 8) | (ks << 9) | (cut << 11) | (m1 << 15);
   d.fm = fm;
   // last stripe at L - 64, inside the last fragment (fragment j_last); loaded
   // in every step (at 0 when not needed: see rows_issue)
@@ -1121,7 +1138,38 @@ xxh3_frag_kernel(BlockArgs a) {
       acc1 = ck[kColdI1];
     }
     uint64_t sum0 = 0, sum1 = 0;
-    const uint32_t fm = cu.fm;
+    uint32_t fm = cu.fm;
+    // the slot across the boundary (one lane per row, in ~1 step in 32):
+    // merged once, out of line, into that chunk's words (realigned, m := 0),
+    // so the chunk loop below carries no per-chunk test
+    if (__ballot((fm >> 8) & 1u)) {
+      uint32_t f2 = fm;
+#ifndef FORST_HOST_EMULATION
+      asm volatile("" : "+v"(f2));  // nothing of the merge is hoisted out of the branch
+#endif
+      if ((f2 >> 8) & 1u) {
+        uint64_t a0, a1;
+        xx_words(cu.alt, (f2 >> 15) & 3u, a0, a1);
+        const uint32_t cut = (f2 >> 11) & 15u;  // bytes before the boundary
+        const uint64_t mlo = cut >= 8 ? ~0ull : ((1ull << (8 * cut)) - 1);
+        const uint64_t mhi = cut >= 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull;
+        const uint32_t ks = (f2 >> 9) & 3u;
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          if (ks == k) {
+            uint64_t d0, d1;
+            xx_words(cu.x[k], (f2 >> (2 * k)) & 3u, d0, d1);
+            d0 = (d0 & mlo) | (a0 & ~mlo);
+            d1 = (d1 & mhi) | (a1 & ~mhi);
+            cu.x[k][0] = static_cast<uint32_t>(d0);
+            cu.x[k][1] = static_cast<uint32_t>(d0 >> 32);
+            cu.x[k][2] = static_cast<uint32_t>(d1);
+            cu.x[k][3] = static_cast<uint32_t>(d1 >> 32);
+          }
+        }
+        fm = f2 & ~(3u << (2 * ks));
+      }
+    }
     // re-read the keys from LDS every step (an opaque index keeps the
     // compiler from hoisting them back into registers)
     uint32_t kix = s4 + 2 * p;
@@ -1133,15 +1181,6 @@ xxh3_frag_kernel(BlockArgs a) {
     for (uint32_t k = 0; k < 4; ++k) {
       uint64_t d0, d1;
       xx_words(cu.x[k], (fm >> (2 * k)) & 3u, d0, d1);
-      if (((fm >> 8) & 1u) && ((fm >> 9) & 3u) == k) {  // the slot across the boundary
-        uint64_t a0, a1;
-        xx_words(cu.alt, (fm >> 15) & 3u, a0, a1);
-        const uint32_t cut = (fm >> 11) & 15u;  // bytes before the boundary
-        const uint64_t mlo = cut >= 8 ? ~0ull : ((1ull << (8 * cut)) - 1);
-        const uint64_t mhi = cut >= 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull;
-        d0 = (d0 & mlo) | (a0 & ~mlo);
-        d1 = (d1 & mhi) | (a1 & ~mhi);
-      }
       const uint64_t c0 = mul32to64(d0 ^ kq[4 * k]) + d1;  // acc[2p] (xxhash.h:4926-4927)
       const uint64_t c1 = d0 + mul32to64(d1 ^ kq[4 * k + 1]);  // acc[2p+1]
       const bool use = C.g < nbC || s4 + 4 * k < nbSC;

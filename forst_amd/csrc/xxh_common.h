@@ -85,10 +85,10 @@ __device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
 // DPP row rotate (within 16-lane rows), one VALU op, no LDS traffic
 template <int N>
 __device__ __forceinline__ uint64_t row_ror64(uint64_t v) {
-  const uint32_t lo = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(v), 0x120 + N,
-                                                  0xf, 0xf, false);
-  const uint32_t hi = __builtin_amdgcn_update_dpp(0u, static_cast<uint32_t>(v >> 32),
-                                                  0x120 + N, 0xf, 0xf, false);
+  // every lane reads a live lane of its row: no "old" operand to initialise
+  const uint32_t lo = __builtin_amdgcn_mov_dpp(static_cast<uint32_t>(v), 0x120 + N, 0xf, 0xf, true);
+  const uint32_t hi = __builtin_amdgcn_mov_dpp(static_cast<uint32_t>(v >> 32), 0x120 + N, 0xf, 0xf,
+                                               true);
   return mk64(lo, hi);
 }
 

@@ -172,6 +172,10 @@ inline uint32_t __builtin_amdgcn_update_dpp(uint32_t old, uint32_t src, int ctrl
   const uint32_t n = static_cast<uint32_t>(ctrl - 0x120) & 15;
   return emu::exchange(src, (lane & ~15u) | ((lane - n) & 15u));
 }
+// v_mov_b32_dpp with bound_ctrl: lanes without a source lane get 0
+inline uint32_t __builtin_amdgcn_mov_dpp(uint32_t src, int ctrl, int rm, int bm, bool) {
+  return __builtin_amdgcn_update_dpp(0u, src, ctrl, rm, bm, true);
+}
 typedef uint32_t emu_u32x2 __attribute__((ext_vector_type(2)));
 // v_permlane16_swap / v_permlane32_swap: swap odd 16-lane rows (upper 32-lane
 // half) of `old` with even rows (lower half) of `src`; returns {old', src'}

@@ -1405,7 +1405,13 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   // cu: the current step's data (ready); nx: the buffer that receives the
   // loads issued now (the position DEPTH steps ahead)
   auto step = [&](CRStep& cu, CRStep& nx) -> bool {
-    if (__ballot(C.rel != kNoBlk) == 0) return false;
+    // raw mode (WAL records, mixed sizes): no early return (see
+    // xxh3_frag_kernel), both step copies issue on every path round the loop
+    // and the next step's loads overlap this step's wait (C5 verify / writer
+    // +1.5 %); the block modes keep the early exit, which measured better on
+    // uniform blocks (A/B on one box: C2 0.600 vs 0.592)
+    const bool live = __ballot(C.rel != kNoBlk) != 0;
+    if ((DEPTH == 2 || MODE != kModeRaw) && !live) return false;
     crow_issue<MODE, PROBE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
     const bool fast = C.rel != kNoBlk && !C.slow();
     const bool r0 = C.g == 0;
@@ -1553,6 +1559,13 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
           atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
       }
     }
+#ifndef FORST_HOST_EMULATION
+    // the finishing words are read only when a row finishes; a use on every
+    // path retires their loads here (a precise wait, the next step's loads
+    // are younger), so reusing their registers in the next step needs no
+    // full vmcnt(0) wait on the step in flight
+    asm volatile("" ::"v"(cu.t0), "v"(cu.t1), "v"(cu.t2), "v"(cu.mod), "v"(cu.extra));
+#endif
     C = I;
     if (DEPTH == 2) {
       I = I2;
@@ -1560,13 +1573,20 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     } else {
       advance(C, I);
     }
-    return true;
+    return live;
   };
   if (DEPTH == 2) {
     while (step(X, Z) && step(Y, X) && step(Z, Y)) {
     }
   } else {
-    while (step(X, Y) && step(Y, X)) {
+    if (MODE == kModeRaw) {
+      for (bool more = true; more;) {
+        step(X, Y);
+        more = step(Y, X);
+      }
+    } else {
+      while (step(X, Y) && step(Y, X)) {
+      }
     }
   }
 }

@@ -37,7 +37,7 @@ struct BlockArgs {
   // *ticket (zeroed per launch) or, without one, dealt round-robin
   unsigned long long* ticket;
   uint64_t share1;
-  int kernel_hint;  // CRC: 0 by mean block size, 1 rows kernel, 2 v2 kernel
+  int kernel_hint;  // CRC: 0 by mean block size, 1 rows kernel, 2 v2 kernel; XXH3: 3 v1 kernel
 };
 
 struct WalArgs {

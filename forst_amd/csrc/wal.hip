@@ -84,6 +84,7 @@ struct WalScratch {
   uint64_t* desc_off;     // [total]
   uint32_t* desc_len;     // [total]
   uint32_t* computed;     // [total]
+  uint32_t* stored;       // [total] unmasked stored CRC (fill, from the header it reads anyway)
 };
 
 // The header chain of log block b, as far as the reader can follow it without
@@ -94,7 +95,7 @@ struct WalScratch {
 template <bool FILL>
 __device__ __forceinline__ uint32_t walk_block(const WalArgs& a, uint64_t b, uint32_t* stop,
                                                uint64_t out_base, uint64_t* d_off,
-                                               uint32_t* d_len) {
+                                               uint32_t* d_len, uint32_t* d_stored) {
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
   uint32_t status = 0, cnt = 0;
@@ -121,6 +122,7 @@ __device__ __forceinline__ uint32_t walk_block(const WalArgs& a, uint64_t b, uin
     if (FILL) {
       d_off[out_base + cnt] = pos + 6;
       d_len[out_base + cnt] = hs + length - 6;
+      d_stored[out_base + cnt] = crc_unmask(ld_le32(h));  // log_reader.cc:522-523
     }
     ++cnt;
     pos += hs + length;
@@ -151,7 +153,7 @@ __global__ void __launch_bounds__(kTile) wal_walk_kernel(WalArgs a, WalScratch s
   const uint64_t bi = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   uint32_t cnt = 0, stop = 0;
   if (bi < a.n_blocks) {
-    cnt = walk_block<false>(a, a.first_block + bi, &stop, 0, nullptr, nullptr);
+    cnt = walk_block<false>(a, a.first_block + bi, &stop, 0, nullptr, nullptr, nullptr);
     s.cnt[bi] = cnt;
     s.stop[bi] = stop;
   }
@@ -192,12 +194,14 @@ __global__ void __launch_bounds__(kTile) wal_fill_kernel(WalArgs a, WalScratch s
   if (bi < a.n_blocks) {
     s.base[bi] = base;
     uint32_t stop;
-    if (cnt) walk_block<true>(a, a.first_block + bi, &stop, base, s.desc_off, s.desc_len);
+    if (cnt)
+      walk_block<true>(a, a.first_block + bi, &stop, base, s.desc_off, s.desc_len, s.stored);
   }
 }
 
 // first failing record of the block in reader order: a CRC mismatch among the
-// structurally valid records (kBadRecordChecksum, 1), else the walk's stop
+// structurally valid records (kBadRecordChecksum, 1), else the walk's stop.
+// Reads the fill's per-record arrays only (no third walk over the headers).
 __global__ void __launch_bounds__(kTile) wal_status_kernel(WalArgs a, WalScratch s) {
   const uint64_t bi = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   if (bi >= a.n_blocks) return;
@@ -206,11 +210,10 @@ __global__ void __launch_bounds__(kTile) wal_status_kernel(WalArgs a, WalScratch
   const uint64_t start = (a.first_block + bi) * kLogBlock;
   uint32_t status = s.stop[bi] >> 24, pos = s.stop[bi] & 0xffffffu, nrec = cnt;
   for (uint32_t j = 0; j < cnt; ++j) {
-    const uint64_t off = s.desc_off[base + j] - 6;
-    if (crc_unmask(ld_le32(a.log + off)) != s.computed[base + j]) {
+    if (s.stored[base + j] != s.computed[base + j]) {
       status = 1;
       nrec = j;
-      pos = static_cast<uint32_t>(off - start);
+      pos = static_cast<uint32_t>(s.desc_off[base + j] - 6 - start);
       break;
     }
   }
@@ -416,11 +419,10 @@ hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* o
   uint32_t* b_out = reinterpret_cast<uint32_t*>(p + 4 * s8 + 3 * s4);
   uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 4 * s8 + 4 * s4);
   hipLaunchKernelGGL(split_flag_kernel, grid, dim3(kTile), 0, stream, len, n, flag);
-  hipLaunchKernelGGL(scan_tiles_kernel, grid, dim3(kTile), 0, stream, flag, n, tiles);
-  hipLaunchKernelGGL(scan_top_kernel, dim3(1), dim3(kScanThreads), 0, stream, tiles, nt);
-  hipLaunchKernelGGL(scan_apply_kernel, grid, dim3(kTile), 0, stream, flag, n, tiles, pos);
+  scan_u64(flag, n, tiles, pos, stream);
+  const uint64_t nst = (n + kScanTile - 1) / kScanTile;
   uint64_t n_small = 0;
-  if ((e = hipMemcpyAsync(&n_small, tiles + nt, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
+  if ((e = hipMemcpyAsync(&n_small, tiles + nst, 8, hipMemcpyDeviceToHost, stream)) != hipSuccess ||
       (e = hipStreamSynchronize(stream)) != hipSuccess) {
     (void)scratch_free(scratch, stream);
     return e;
@@ -489,13 +491,14 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream, const char** 
   }
   void* desc = nullptr;
   const size_t sz_off = up256(8 * total), sz_len = up256(4 * total);
-  if ((e = scratch_alloc(&desc, sz_off + 2 * sz_len, stream)) != hipSuccess) {
+  if ((e = scratch_alloc(&desc, sz_off + 3 * sz_len, stream)) != hipSuccess) {
     (void)scratch_free(scratch, stream);
     return e;
   }
   s.desc_off = static_cast<uint64_t*>(desc);
   s.desc_len = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(desc) + sz_off);
   s.computed = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(desc) + sz_off + sz_len);
+  s.stored = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(desc) + sz_off + 2 * sz_len);
   hipLaunchKernelGGL(wal_fill_kernel, grid, dim3(kTile), 0, stream, a, s);
   *name = "wal_walk_kernel";
   if (total) e = crc_records(a.log, a.log_len, s.desc_off, s.desc_len, total, s.computed, stream, name);

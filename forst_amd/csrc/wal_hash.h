@@ -203,6 +203,7 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
       ga.sizes = blen;
       ga.out64 = hb;
       ga.n = ng;
+      ga.kernel_hint = 3;  // few records (C5: 22 K of 10 M), long ones: one per wave
       const char* gname = nullptr;
       e = launch_xxh3_blocks(kModeRaw, ga, st, &gname);
     }

@@ -97,7 +97,7 @@ __device__ __forceinline__ uint32_t unmask(uint32_t m) {  // util/crc32c.h:39
 template <bool FILL>
 __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev, uint32_t* ev_pos,
                                   uint64_t base, uint64_t* it_off, uint8_t* it_old,
-                                  uint64_t* crc_off, uint32_t* crc_len) {
+                                  uint64_t* crc_off, uint32_t* crc_len, uint32_t* crc_stored) {
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
   const bool eof_block = end - start < kLogBlock;  // ReadMore read short: eof_
@@ -146,6 +146,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       it_old[base + n] = 0;
       crc_off[base + n] = pos + 6;
       crc_len[base + n] = hs + length - 6;
+      crc_stored[base + n] = unmask(ld_le32(h));  // log_reader.cc:522-523
     }
     ++n;
     pos += hs + length;
@@ -159,16 +160,18 @@ __global__ void __launch_bounds__(kLanes) rw_count_kernel(RecoverArgs a, uint64_
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
   uint32_t ev, ep;
-  cnt[b] = rw_walk_block<false>(a, b, &ev, &ep, 0, nullptr, nullptr, nullptr, nullptr);
+  cnt[b] = rw_walk_block<false>(a, b, &ev, &ep, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
 }
 
 __global__ void __launch_bounds__(kLanes) rw_fill_kernel(RecoverArgs a, const uint64_t* base,
                                                          uint64_t* it_off, uint8_t* it_old,
                                                          uint64_t* crc_off, uint32_t* crc_len,
-                                                         uint32_t* ev, uint32_t* ev_pos) {
+                                                         uint32_t* crc_stored, uint32_t* ev,
+                                                         uint32_t* ev_pos) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
-  rw_walk_block<true>(a, b, &ev[b], &ev_pos[b], base[b], it_off, it_old, crc_off, crc_len);
+  rw_walk_block<true>(a, b, &ev[b], &ev_pos[b], base[b], it_off, it_old, crc_off, crc_len,
+                      crc_stored);
 }
 
 // ---- per block: CRC truncation, reader position, stop -------------------------
@@ -180,6 +183,9 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
                                                           const uint64_t* base,
                                                           const uint64_t* it_off,
                                                           const uint8_t* it_old,
+                                                          const uint64_t* crc_off,
+                                                          const uint32_t* crc_len,
+                                                          const uint32_t* crc_stored,
                                                           const uint32_t* computed, uint32_t* ev,
                                                           uint32_t* ev_pos, uint64_t* acc,
                                                           uint64_t* rp_end,
@@ -192,17 +198,21 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
   const uint64_t n = cnt[b], i0 = base[b];
   uint64_t k = 0, last_end = start;
   uint32_t e = ev[b], ep = ev_pos[b];
+  // the fill's per-item arrays (stored CRC, record extent); the header is
+  // re-read only for skipped old records (kSkipAnyCorruptedRecords)
   for (; k < n; ++k) {
-    const uint64_t off = it_off[i0 + k];
-    const uint8_t* h = a.log + off;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t hs = recyclable_type(h[6]) ? kLogRHdr : kLogHdr;
-    if (!it_old[i0 + k] && unmask(ld_le32(h)) != computed[i0 + k]) {
+    if (it_old[i0 + k]) {
+      const uint8_t* h = a.log + it_off[i0 + k];
+      const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
+      last_end = it_off[i0 + k] + (recyclable_type(h[6]) ? kLogRHdr : kLogHdr) + length;
+      continue;
+    }
+    if (crc_stored[i0 + k] != computed[i0 + k]) {
       e = kEvChecksum;
-      ep = static_cast<uint32_t>(off - start);
+      ep = static_cast<uint32_t>(crc_off[i0 + k] - 6 - start);
       break;
     }
-    last_end = off + hs + length;
+    last_end = crc_off[i0 + k] + crc_len[i0 + k];
   }
   acc[b] = k;
   ev[b] = e;
@@ -543,7 +553,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   }
   // phase 2: items, CRCs, block truncation, tokens, state machine
   const uint64_t ni = n_items, nt_max = n_items + nb + 1;
-  const size_t p2 = 3 * up256(8 * ni) + up256(ni) + 2 * up256(4 * ni) +  // items
+  const size_t p2 = 3 * up256(8 * ni) + up256(ni) + 3 * up256(4 * ni) +  // items
                     up256(nt_max) * 2 + up256(8 * nt_max) * 2 + up256(4 * nt_max) +  // tokens
                     up256(8 * (nb + 2)) +                                          // token base
                     up256(8 * nt_max) * 8 + up256(8 * (nt_max + 1)) * 2 +          // fsm
@@ -558,6 +568,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint8_t* it_old = A.take<uint8_t>(ni);
   uint64_t* crc_off = A.take<uint64_t>(ni);
   uint32_t* crc_len = A.take<uint32_t>(ni);
+  uint32_t* crc_stored = A.take<uint32_t>(ni);
   uint32_t* computed = A.take<uint32_t>(ni);
   Tokens t{A.take<uint8_t>(nt_max), A.take<uint64_t>(nt_max), A.take<uint32_t>(nt_max),
            A.take<uint64_t>(nt_max), A.take<uint8_t>(nt_max)};
@@ -576,7 +587,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint64_t* tiles2 = A.take<uint64_t>(nt_max / kScanTile + 2);
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, ibase, it_off, it_old,
-                       crc_off, crc_len, ev, ev_pos);
+                       crc_off, crc_len, crc_stored, ev, ev_pos);
     if (ni) {
       BlockArgs cb{};
       cb.base = log;
@@ -593,7 +604,8 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       }
     }
     hipLaunchKernelGGL(rw_block_kernel, grid_for(nb), dim3(kLanes), 0, st, a, cnt, ibase, it_off,
-                       it_old, computed, ev, ev_pos, acc, rp_end, first_stop, recycled);
+                       it_old, crc_off, crc_len, crc_stored, computed, ev, ev_pos, acc, rp_end,
+                       first_stop, recycled);
   }
   hipLaunchKernelGGL(rw_ntok_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, acc, ev, first_stop,
                      ntok);

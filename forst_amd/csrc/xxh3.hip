@@ -1496,6 +1496,10 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
   XxKernel k = a.base_len < 4096                     ? XxKernel::kSimple
                : (a.n >= 0xffffffffull || big) ? XxKernel::kV1
                                                      : XxKernel::kRows;
+  // kernel_hint 3: one message per wave (a short list of long messages, e.g.
+  // wal_hash.h's gathered records: rows would leave most rows idle while a
+  // few walk 32 KiB records 1 KiB per step)
+  if (a.kernel_hint == 3 && a.base_len >= 4096) k = XxKernel::kV1;
 #ifdef FORST_DIAG
   if (a.base_len >= 4096) {
     const std::string v = diag_env("FORST_XXH3_VARIANT");

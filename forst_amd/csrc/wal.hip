@@ -288,23 +288,30 @@ __device__ __forceinline__ FragInfo frag_info(const WalArgs& a, uint64_t i) {
   return f;
 }
 
-// start flags (kFullType / kFirstType)
-__global__ void __launch_bounds__(kTile) rec_start_kernel(WalArgs a, uint64_t* start) {
+// start flags (kFullType / kFirstType) and each fragment's header fields,
+// packed (length | type << 16 | ok << 20 | recyclable << 21): the one pass
+// over the headers; the later kernels read the packed word
+__global__ void __launch_bounds__(kTile) rec_start_kernel(WalArgs a, uint64_t* start,
+                                                          uint32_t* pinfo) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   if (i >= a.n_records) return;
   const FragInfo f = frag_info(a, i);
   start[i] = f.ok && (f.type == 1 || f.type == 2) ? 1 : 0;
+  pinfo[i] = f.ok ? (f.len | (f.type << 16) | (1u << 20) |
+                     (f.off - a.header_offsets[i] == kLogRHdr ? 1u << 21 : 0u))
+                  : 0u;
 }
 
 // per logical record: first fragment and kind
 __global__ void __launch_bounds__(kTile) rec_owner_kernel(WalArgs a, const uint64_t* start,
+                                                          const uint32_t* pinfo,
                                                           const uint64_t* lid_excl,
                                                           uint64_t* first_phys, uint8_t* kind) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   if (i >= a.n_records) return;
   if (start[i]) {
     first_phys[lid_excl[i]] = i;
-    kind[lid_excl[i]] = static_cast<uint8_t>(frag_info(a, i).type);
+    kind[lid_excl[i]] = static_cast<uint8_t>((pinfo[i] >> 16) & 15u);
   }
 }
 
@@ -315,6 +322,7 @@ struct A14Frags {
   WalArgs a;
   const uint64_t* first;
   const uint8_t* kind;
+  const uint32_t* pinfo;
   uint64_t n_logical;
   __device__ uint64_t begin(uint64_t j) const { return first[j]; }
   __device__ uint64_t end(uint64_t j) const {
@@ -322,15 +330,10 @@ struct A14Frags {
     return j + 1 < n_logical ? first[j + 1] : a.n_records;
   }
   __device__ uint64_t header(uint64_t q) const { return a.header_offsets[q]; }
-  __device__ bool use(uint64_t q) const { return frag_info(a, q).ok; }
+  __device__ uint32_t hs(uint64_t q) const { return (pinfo[q] >> 21) & 1u ? kLogRHdr : kLogHdr; }
+  __device__ uint32_t len(uint64_t q) const { return pinfo[q] & 0xffffu; }
+  __device__ bool use(uint64_t q) const { return (pinfo[q] >> 20) & 1u; }
 };
-
-__global__ void __launch_bounds__(kTile) rec_first_kernel(uint64_t n_logical,
-                                                          const uint64_t* first_phys,
-                                                          uint64_t* out_first) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
-  if (j < n_logical) out_first[j] = first_phys[j];
-}
 
 #ifdef FORST_DIAG
 // ---- raw CRC of a record list split by size (A/B variant) -------------------
@@ -541,20 +544,23 @@ hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out
   if (a.n_records == 0) return hipSuccess;
   const uint64_t n = a.n_records, nt = (n + kTile - 1) / kTile;
   const dim3 grid(static_cast<uint32_t>(nt));
-  // scratch: start, lid, first_phys (u64 x n), kind (u8 x n), tile sums
-  const size_t s8 = up256(8 * n), s1 = up256(n), st = up256(8 * (nt + 2));
+  // scratch: start, lid, first_phys (u64 x n; the caller's out_first when
+  // given), kind (u8 x n), packed header fields (u32 x n), tile sums
+  const size_t s8 = up256(8 * n), s1 = up256(n), s4 = up256(4 * n), st = up256(8 * (nt + 2));
   void* scratch = nullptr;
-  hipError_t e = scratch_alloc(&scratch, 3 * s8 + s1 + st, stream);
+  hipError_t e = scratch_alloc(&scratch, 3 * s8 + s1 + s4 + st, stream);
   if (e != hipSuccess) return e;
   uint8_t* p = static_cast<uint8_t*>(scratch);
   uint64_t* start = reinterpret_cast<uint64_t*>(p);
   uint64_t* lid = reinterpret_cast<uint64_t*>(p + s8);
-  uint64_t* first = reinterpret_cast<uint64_t*>(p + 2 * s8);
+  uint64_t* first = out_first ? out_first : reinterpret_cast<uint64_t*>(p + 2 * s8);
   uint8_t* kind = p + 3 * s8;
-  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 3 * s8 + s1);
-  hipLaunchKernelGGL(rec_start_kernel, grid, dim3(kTile), 0, stream, a, start);
+  uint32_t* pinfo = reinterpret_cast<uint32_t*>(p + 3 * s8 + s1);
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 3 * s8 + s1 + s4);
+  hipLaunchKernelGGL(rec_start_kernel, grid, dim3(kTile), 0, stream, a, start, pinfo);
   scan_u64(start, n, tiles, lid, stream);
-  hipLaunchKernelGGL(rec_owner_kernel, grid, dim3(kTile), 0, stream, a, start, lid, first, kind);
+  hipLaunchKernelGGL(rec_owner_kernel, grid, dim3(kTile), 0, stream, a, start, pinfo, lid, first,
+                     kind);
   uint64_t n_logical = 0;
   if ((e = hipMemcpyAsync(&n_logical, tiles + (n + kScanTile - 1) / kScanTile, 8,
                           hipMemcpyDeviceToHost, stream)) != hipSuccess ||
@@ -563,13 +569,8 @@ hipError_t launch_wal_record_xxh3(const WalArgs& a, uint64_t* out, uint64_t* out
     return e;
   }
   if (n_logical) {
-    const A14Frags f{a, first, kind, n_logical};
+    const A14Frags f{a, first, kind, pinfo, n_logical};
     e = hash_logical_records(a.log, a.log_len, f, n_logical, out, stream, name);
-    if (e == hipSuccess && out_first) {
-      hipLaunchKernelGGL(rec_first_kernel, dim3(static_cast<uint32_t>((n_logical + kTile - 1) / kTile)),
-                         dim3(kTile), 0, stream, n_logical, first, out_first);
-      e = hipGetLastError();
-    }
   }
   *n_logical_host = n_logical;
   const hipError_t f1 = scratch_free(scratch, stream);

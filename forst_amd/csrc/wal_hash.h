@@ -15,6 +15,9 @@
 // pipeline's fragments:
 //   F::begin(j), F::end(j)   fragment range of logical record j
 //   F::header(q)             log offset of fragment q's header
+//   F::hs(q), F::len(q)      its header size (7 / 11) and payload length, from
+//                            the pipeline's own per-fragment arrays (no
+//                            further reads of the header bytes)
 //   F::use(q)                false: fragment q is not part of the record (the
 //                            record is then gathered without it)
 #pragma once
@@ -31,14 +34,6 @@ namespace {
 
 constexpr uint32_t kWhBlock = 32768;  // db/log_format.h:45
 constexpr uint32_t kWhLanes = 256;
-
-__device__ __forceinline__ uint32_t wh_hs(const uint8_t* log, uint64_t hdr) {
-  const uint32_t t = log[hdr + 6];  // recyclable types: db/log_format.h:20-41
-  return ((t >= 5 && t <= 8) || t == 11) ? 11u : 7u;
-}
-__device__ __forceinline__ uint32_t wh_len(const uint8_t* log, uint64_t hdr) {
-  return static_cast<uint32_t>(log[hdr + 4]) | (static_cast<uint32_t>(log[hdr + 5]) << 8);
-}
 
 // per logical record: in-place descriptor (p0, len, info = hs | j_last << 8)
 // for the frag kernel, or glen = len when it must be gathered (its frag
@@ -61,7 +56,7 @@ __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F
       continue;
     }
     const uint64_t h = f.header(q);
-    const uint32_t hs = wh_hs(log, h), l = wh_len(log, h);
+    const uint32_t hs = f.hs(q), l = f.len(q);
     if (q > b && (h != prev_end || (h & (kWhBlock - 1)) != 0)) regular = false;
     if (q + 1 < e && ((h + hs + l) & (kWhBlock - 1)) != 0) regular = false;  // fills its block
     if (q == b) hs0 = hs;
@@ -74,7 +69,7 @@ __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F
   const bool multi = nz > 1;
   if (multi && (total <= 240 || last_len < 64)) regular = false;
   if (total > 0xffffffffull) regular = false;
-  if (nz == 0) start = e > b && f.use(b) ? f.header(b) + wh_hs(log, f.header(b)) : 0;
+  if (nz == 0) start = e > b && f.use(b) ? f.header(b) + f.hs(b) : 0;
   p0[j] = start;
   len[j] = regular ? static_cast<uint32_t>(total) : 0u;
   info[j] = multi ? (hs0 | ((nz - 1) << 8)) : 0u;
@@ -114,9 +109,19 @@ __global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log,
     for (uint64_t q = f.begin(j); q < f.end(j); ++q) {
       if (!f.use(q)) continue;
       const uint64_t h = f.header(q);
-      const uint8_t* src = log + h + wh_hs(log, h);
-      const uint32_t l = wh_len(log, h);
-      for (uint32_t x = threadIdx.x; x < l; x += kWhLanes) d[x] = src[x];
+      const uint8_t* src = log + h + f.hs(q);
+      const uint32_t l = f.len(q);
+      // whole destination dwords from (unaligned) 4-byte source reads; the
+      // <= 3 bytes at either end (shared with the neighbouring fragments'
+      // dwords) byte by byte
+      const uint32_t head = static_cast<uint32_t>((4 - (reinterpret_cast<uintptr_t>(d) & 3)) & 3);
+      const uint32_t hb = head < l ? head : l;
+      const uint32_t nw = (l - hb) >> 2;
+      const uint32_t tb = hb + 4 * nw;
+      if (threadIdx.x < hb) d[threadIdx.x] = src[threadIdx.x];
+      if (threadIdx.x < l - tb) d[tb + threadIdx.x] = src[tb + threadIdx.x];
+      uint32_t* dw = reinterpret_cast<uint32_t*>(d + hb);
+      for (uint32_t x = threadIdx.x; x < nw; x += kWhLanes) dw[x] = ldu32(src + hb + 4 * x);
       d += l;
     }
   }

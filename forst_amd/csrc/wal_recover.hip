@@ -97,7 +97,8 @@ __device__ __forceinline__ uint32_t unmask(uint32_t m) {  // util/crc32c.h:39
 template <bool FILL>
 __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev, uint32_t* ev_pos,
                                   uint64_t base, uint64_t* it_off, uint8_t* it_old,
-                                  uint64_t* crc_off, uint32_t* crc_len, uint32_t* crc_stored) {
+                                  uint64_t* crc_off, uint32_t* crc_len, uint32_t* crc_stored,
+                                  uint32_t* ipack) {
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
   const bool eof_block = end - start < kLogBlock;  // ReadMore read short: eof_
@@ -132,6 +133,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
         it_old[base + n] = 1;
         crc_off[base + n] = 0;
         crc_len[base + n] = 0;
+        ipack[base + n] = length | (recyc ? 1u << 16 : 0u);
       }
       ++n;
       pos += hs + length;
@@ -147,6 +149,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       crc_off[base + n] = pos + 6;
       crc_len[base + n] = hs + length - 6;
       crc_stored[base + n] = unmask(ld_le32(h));  // log_reader.cc:522-523
+      ipack[base + n] = length | (recyc ? 1u << 16 : 0u);
     }
     ++n;
     pos += hs + length;
@@ -160,18 +163,19 @@ __global__ void __launch_bounds__(kLanes) rw_count_kernel(RecoverArgs a, uint64_
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
   uint32_t ev, ep;
-  cnt[b] = rw_walk_block<false>(a, b, &ev, &ep, 0, nullptr, nullptr, nullptr, nullptr, nullptr);
+  cnt[b] = rw_walk_block<false>(a, b, &ev, &ep, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
+                                nullptr);
 }
 
 __global__ void __launch_bounds__(kLanes) rw_fill_kernel(RecoverArgs a, const uint64_t* base,
                                                          uint64_t* it_off, uint8_t* it_old,
                                                          uint64_t* crc_off, uint32_t* crc_len,
-                                                         uint32_t* crc_stored, uint32_t* ev,
-                                                         uint32_t* ev_pos) {
+                                                         uint32_t* crc_stored, uint32_t* ipack,
+                                                         uint32_t* ev, uint32_t* ev_pos) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
   rw_walk_block<true>(a, b, &ev[b], &ev_pos[b], base[b], it_off, it_old, crc_off, crc_len,
-                      crc_stored);
+                      crc_stored, ipack);
 }
 
 // ---- per block: CRC truncation, reader position, stop -------------------------
@@ -480,9 +484,12 @@ struct RecFrags {
   const uint32_t* n_frag;
   const uint64_t* item;
   const uint64_t* it_off;
+  const uint32_t* ipack;  // item: length | recyclable << 16 (rw_fill)
   __device__ uint64_t begin(uint64_t j) const { return head_tok[j]; }
   __device__ uint64_t end(uint64_t j) const { return head_tok[j] + n_frag[j]; }
   __device__ uint64_t header(uint64_t q) const { return it_off[item[q]]; }
+  __device__ uint32_t hs(uint64_t q) const { return (ipack[item[q]] >> 16) & 1u ? kLogRHdr : kLogHdr; }
+  __device__ uint32_t len(uint64_t q) const { return ipack[item[q]] & 0xffffu; }
   __device__ bool use(uint64_t) const { return true; }
 };
 
@@ -553,7 +560,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   }
   // phase 2: items, CRCs, block truncation, tokens, state machine
   const uint64_t ni = n_items, nt_max = n_items + nb + 1;
-  const size_t p2 = 3 * up256(8 * ni) + up256(ni) + 3 * up256(4 * ni) +  // items
+  const size_t p2 = 3 * up256(8 * ni) + up256(ni) + 4 * up256(4 * ni) +  // items
                     up256(nt_max) * 2 + up256(8 * nt_max) * 2 + up256(4 * nt_max) +  // tokens
                     up256(8 * (nb + 2)) +                                          // token base
                     up256(8 * nt_max) * 8 + up256(8 * (nt_max + 1)) * 2 +          // fsm
@@ -569,6 +576,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint64_t* crc_off = A.take<uint64_t>(ni);
   uint32_t* crc_len = A.take<uint32_t>(ni);
   uint32_t* crc_stored = A.take<uint32_t>(ni);
+  uint32_t* ipack = A.take<uint32_t>(ni);
   uint32_t* computed = A.take<uint32_t>(ni);
   Tokens t{A.take<uint8_t>(nt_max), A.take<uint64_t>(nt_max), A.take<uint32_t>(nt_max),
            A.take<uint64_t>(nt_max), A.take<uint8_t>(nt_max)};
@@ -587,7 +595,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint64_t* tiles2 = A.take<uint64_t>(nt_max / kScanTile + 2);
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, ibase, it_off, it_old,
-                       crc_off, crc_len, crc_stored, ev, ev_pos);
+                       crc_off, crc_len, crc_stored, ipack, ev, ev_pos);
     if (ni) {
       BlockArgs cb{};
       cb.base = log;
@@ -694,7 +702,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, nullptr,
                      nullptr, emit_at, rep_at, full, nr, reps, rep_cap, head_tok);
   if (nr) {
-    const RecFrags rf{head_tok, r_nf, t.item, it_off};
+    const RecFrags rf{head_tok, r_nf, t.item, it_off, ipack};
     e = hash_logical_records(log, log_len, rf, nr, full.hash, st, name);
   }
   // copy the (capacity-limited) record list out

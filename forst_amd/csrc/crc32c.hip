@@ -1608,6 +1608,61 @@ __global__ void __launch_bounds__(64 * kRowsD2Waves) crc32c_rows_d2_kernel(Block
 __global__ void __launch_bounds__(64 * kRowsD2Waves) crc32c_rows_d2_probe_kernel(BlockArgs a) {
   crc32c_rows_body<kModeVerify, 1, 2>(a);
 }
+
+// Access-pattern probe (diagnostics only, FORST_CRC_VARIANT=pat<G>_<C>): no
+// CRC work, no work feed.  Groups of G lanes (16 = a row, 64 = the wave) walk
+// their blocks (static: group k of the grid takes blocks k, k + ngroups, ...)
+// in C-byte steps, one step of loads in flight ahead of an XOR of the
+// current one: the memory ceiling of "C contiguous bytes per group per step"
+// against the rows kernel's 1 KiB per row and the v2 kernel's 4 KiB per wave.
+// The plain streaming ceiling (diagnostics only, FORST_CRC_VARIANT=stream):
+// the whole buffer read once, every wave a contiguous 4 KiB per step (16 B
+// per lane, 4 loads per lane in flight), grid-stride, no descriptors.
+__global__ void __launch_bounds__(kThreads) crc32c_stream_probe_kernel(BlockArgs a) {
+  const uint64_t nthr = static_cast<uint64_t>(gridDim.x) * kThreads;
+  const uint64_t n16 = a.base_len / 16;
+  uint32_t acc = 0;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kThreads + threadIdx.x; i < n16;
+       i += 4 * nthr) {
+    u32x4a4 v[4];
+#pragma unroll
+    for (int k = 0; k < 4; ++k) {
+      const uint64_t j = i + k * nthr;
+      v[k] = ld16_a4(a.base + 16 * (j < n16 ? j : i));
+    }
+#pragma unroll
+    for (int k = 0; k < 4; ++k) acc ^= v[k].x ^ v[k].y ^ v[k].z ^ v[k].w;
+  }
+  if (a.out32 && threadIdx.x == 0) a.out32[blockIdx.x] = acc;
+}
+
+template <int G, int C>
+__global__ void __launch_bounds__(kThreads) crc32c_pattern_probe_kernel(BlockArgs a) {
+  constexpr int kPer = C / G / 16;  // 16-byte loads per lane per step
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t gl = lane % G;
+  const uint64_t ng = static_cast<uint64_t>(gridDim.x) * (kThreads / G);
+  const uint64_t g0 = static_cast<uint64_t>(blockIdx.x) * (kThreads / G) + threadIdx.x / G;
+  uint32_t acc = 0;
+  for (uint64_t b = g0; b < a.n; b += ng) {
+    const uint64_t off = a.offsets[b] & ~15ull;
+    const uint32_t sz = a.sizes[b];
+    const uint32_t steps = (sz + 16 + C - 1) / C;
+    u32x4a4 cur[kPer], nxt[kPer];
+#pragma unroll
+    for (int k = 0; k < kPer; ++k) cur[k] = ld16_a4(a.base + off + 16 * (gl + G * k));
+    for (uint32_t st = 0; st < steps; ++st) {
+      const uint64_t o2 = off + static_cast<uint64_t>(st + 1 < steps ? st + 1 : st) * C;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) nxt[k] = ld16_a4(a.base + o2 + 16 * (gl + G * k));
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) acc ^= cur[k].x ^ cur[k].y ^ cur[k].z ^ cur[k].w;
+#pragma unroll
+      for (int k = 0; k < kPer; ++k) cur[k] = nxt[k];
+    }
+    if (gl == 0 && a.out32) a.out32[b] = acc;
+  }
+}
 #endif
 
 // One wave per block, no streaming: serves buffers shorter than one 4 KiB
@@ -1687,6 +1742,7 @@ enum class CrcKernel {
   kV2,      // one block per wave, two chains per lane (crc32c_stream2_kernel)
 #ifdef FORST_DIAG
   kV1, kRowsD2, kRowsProbeLoad, kRowsProbeNoFin, kRowsD2ProbeLoad, kRowsProbeContig, kV2ProbeLoad, kV2ProbeRounds, kV2ProbeNoHead,
+  kPat16_1k, kPat16_2k, kPat16_4k, kPat64_4k, kStream,
 #endif
 };
 
@@ -1727,6 +1783,11 @@ const char* crc_kernel_name(CrcKernel k, int mode) {
     case CrcKernel::kRowsProbeNoFin: return "crc32c_rows_probe_kernel<2>";
     case CrcKernel::kRowsD2ProbeLoad: return "crc32c_rows_d2_probe_kernel";
     case CrcKernel::kRowsProbeContig: return "crc32c_rows_probe_kernel<3>";
+    case CrcKernel::kPat16_1k: return "crc32c_pattern_probe_kernel<16,1024>";
+    case CrcKernel::kPat16_2k: return "crc32c_pattern_probe_kernel<16,2048>";
+    case CrcKernel::kPat16_4k: return "crc32c_pattern_probe_kernel<16,4096>";
+    case CrcKernel::kPat64_4k: return "crc32c_pattern_probe_kernel<64,4096>";
+    case CrcKernel::kStream: return "crc32c_stream_probe_kernel";
     case CrcKernel::kV2ProbeLoad: return "crc32c_stream2_probe_kernel<1>";
     case CrcKernel::kV2ProbeRounds: return "crc32c_stream2_probe_kernel<2>";
     case CrcKernel::kV2ProbeNoHead: return "crc32c_stream2_probe_kernel<3>";
@@ -1758,6 +1819,21 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
       return launch_fed(crc32c_rows_d2_probe_kernel, grid, kRowsD2Waves, a, s);
     case CrcKernel::kRowsProbeContig:
       return launch_fed(crc32c_rows_probe_kernel<3>, grid, kWaves, a, s);
+    case CrcKernel::kPat16_1k:
+      hipLaunchKernelGGL((crc32c_pattern_probe_kernel<16, 1024>), dim3(grid), dim3(kThreads), 0, s, a);
+      return hipGetLastError();
+    case CrcKernel::kPat16_2k:
+      hipLaunchKernelGGL((crc32c_pattern_probe_kernel<16, 2048>), dim3(grid), dim3(kThreads), 0, s, a);
+      return hipGetLastError();
+    case CrcKernel::kPat16_4k:
+      hipLaunchKernelGGL((crc32c_pattern_probe_kernel<16, 4096>), dim3(grid), dim3(kThreads), 0, s, a);
+      return hipGetLastError();
+    case CrcKernel::kPat64_4k:
+      hipLaunchKernelGGL((crc32c_pattern_probe_kernel<64, 4096>), dim3(grid), dim3(kThreads), 0, s, a);
+      return hipGetLastError();
+    case CrcKernel::kStream:
+      hipLaunchKernelGGL(crc32c_stream_probe_kernel, dim3(4 * grid), dim3(kThreads), 0, s, a);
+      return hipGetLastError();
     case CrcKernel::kV2ProbeLoad:
       return launch_kernel(crc32c_stream2_probe_kernel<1>, grid, kThreads, a, s);
     case CrcKernel::kV2ProbeRounds:
@@ -1784,6 +1860,11 @@ CrcKernel diag_crc_kernel(CrcKernel k, int mode) {
   if (v == "rows_probe_nofin" && vf) return CrcKernel::kRowsProbeNoFin;
   if (v == "rows_d2_probe_load" && vf) return CrcKernel::kRowsD2ProbeLoad;
   if (v == "rows_probe_contig" && vf) return CrcKernel::kRowsProbeContig;
+  if (v == "pat16_1k" && vf) return CrcKernel::kPat16_1k;
+  if (v == "pat16_2k" && vf) return CrcKernel::kPat16_2k;
+  if (v == "pat16_4k" && vf) return CrcKernel::kPat16_4k;
+  if (v == "pat64_4k" && vf) return CrcKernel::kPat64_4k;
+  if (v == "stream" && vf) return CrcKernel::kStream;
   if (v == "probe_load" && vf) return CrcKernel::kV2ProbeLoad;
   if (v == "probe_rounds" && vf) return CrcKernel::kV2ProbeRounds;
   if (v == "probe_nohead" && vf) return CrcKernel::kV2ProbeNoHead;

@@ -185,17 +185,40 @@ __global__ void __launch_bounds__(kScanThreads) wal_scan_kernel(WalScratch s, ui
   if (t == 0) s.tile_prefix[n_tiles] = carry;
 }
 
+// The records of a tile's 256 log blocks are one contiguous run of the
+// descriptor arrays; lane b's records are interleaved with its neighbours'
+// in that run, so direct stores are partial-line writes.  When the run fits,
+// the lanes write it into LDS and the workgroup stores it coalesced.
+constexpr uint32_t kFillCap = 2560;  // records staged per tile (40 KiB of LDS)
+
 __global__ void __launch_bounds__(kTile) wal_fill_kernel(WalArgs a, WalScratch s) {
   __shared__ uint32_t sh[kTile];
+  __shared__ uint64_t l_off[kFillCap];
+  __shared__ uint32_t l_len[kFillCap], l_st[kFillCap];
   const uint64_t bi = static_cast<uint64_t>(blockIdx.x) * kTile + threadIdx.x;
   const uint32_t cnt = bi < a.n_blocks ? s.cnt[bi] : 0u;
   uint32_t tot;
-  const uint64_t base = s.tile_prefix[blockIdx.x] + wg_exclusive_scan(cnt, sh, &tot);
+  const uint32_t excl = wg_exclusive_scan(cnt, sh, &tot);
+  const uint64_t wg_base = s.tile_prefix[blockIdx.x];
+  const uint64_t base = wg_base + excl;
+  const bool staged = tot <= kFillCap;  // workgroup-uniform
   if (bi < a.n_blocks) {
     s.base[bi] = base;
     uint32_t stop;
-    if (cnt)
-      walk_block<true>(a, a.first_block + bi, &stop, base, s.desc_off, s.desc_len, s.stored);
+    if (cnt) {
+      if (staged)
+        walk_block<true>(a, a.first_block + bi, &stop, excl, l_off, l_len, l_st);
+      else
+        walk_block<true>(a, a.first_block + bi, &stop, base, s.desc_off, s.desc_len, s.stored);
+    }
+  }
+  if (staged) {
+    __syncthreads();
+    for (uint32_t i = threadIdx.x; i < tot; i += kTile) {
+      s.desc_off[wg_base + i] = l_off[i];
+      s.desc_len[wg_base + i] = l_len[i];
+      s.stored[wg_base + i] = l_st[i];
+    }
   }
 }
 

@@ -133,7 +133,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
         it_old[base + n] = 1;
         crc_off[base + n] = 0;
         crc_len[base + n] = 0;
-        ipack[base + n] = length | (recyc ? 1u << 16 : 0u);
+        ipack[base + n] = length | (type << 16) | (recyc ? 1u << 24 : 0u);
       }
       ++n;
       pos += hs + length;
@@ -149,7 +149,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       crc_off[base + n] = pos + 6;
       crc_len[base + n] = hs + length - 6;
       crc_stored[base + n] = unmask(ld_le32(h));  // log_reader.cc:522-523
-      ipack[base + n] = length | (recyc ? 1u << 16 : 0u);
+      ipack[base + n] = length | (type << 16) | (recyc ? 1u << 24 : 0u);
     }
     ++n;
     pos += hs + length;
@@ -259,6 +259,7 @@ struct Tokens {
 __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const uint64_t* base,
                                                           const uint64_t* it_off,
                                                           const uint8_t* it_old,
+                                                          const uint32_t* ipack,
                                                           const uint64_t* acc, const uint32_t* ev,
                                                           const uint32_t* ev_pos,
                                                           const uint64_t* rp_end,
@@ -286,9 +287,9 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
   const uint64_t n = acc[b], i0 = base[b];
   for (uint64_t k = 0; k < n; ++k, ++o) {
     const uint64_t off = it_off[i0 + k];
-    const uint8_t* h = a.log + off;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t type = h[6];
+    const uint32_t pk = ipack[i0 + k];  // the fill's header fields (no header re-read)
+    const uint32_t length = pk & 0xffffu;
+    const uint32_t type = (pk >> 16) & 0xffu;
     const uint32_t nt = (type >= 5 && type <= 8) ? type - 4 : type;  // recyclable -> legacy
     uint8_t kind = nt == 1   ? kTkFull
                    : nt == 2 ? kTkFirst
@@ -304,7 +305,7 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
     t.len[o] = length;
     t.pos[o] = rp;
     t.type[o] = static_cast<uint8_t>(type);
-    rp = off + (recyclable_type(type) ? kLogRHdr : kLogHdr) + length;
+    rp = off + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr) + length;
   }
   const uint32_t e = ev[b];
   if (e == kEvNone) return;
@@ -484,11 +485,11 @@ struct RecFrags {
   const uint32_t* n_frag;
   const uint64_t* item;
   const uint64_t* it_off;
-  const uint32_t* ipack;  // item: length | recyclable << 16 (rw_fill)
+  const uint32_t* ipack;  // item: length | type << 16 | recyclable << 24 (rw_fill)
   __device__ uint64_t begin(uint64_t j) const { return head_tok[j]; }
   __device__ uint64_t end(uint64_t j) const { return head_tok[j] + n_frag[j]; }
   __device__ uint64_t header(uint64_t q) const { return it_off[item[q]]; }
-  __device__ uint32_t hs(uint64_t q) const { return (ipack[item[q]] >> 16) & 1u ? kLogRHdr : kLogHdr; }
+  __device__ uint32_t hs(uint64_t q) const { return (ipack[item[q]] >> 24) & 1u ? kLogRHdr : kLogHdr; }
   __device__ uint32_t len(uint64_t q) const { return ipack[item[q]] & 0xffffu; }
   __device__ bool use(uint64_t) const { return true; }
 };
@@ -627,7 +628,8 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     return e;
   }
   hipLaunchKernelGGL(rw_token_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, ibase, it_off,
-                     it_old, acc, ev, ev_pos, rp_end, tok_base, first_stop, recycled, t, unsup_d);
+                     it_old, ipack, acc, ev, ev_pos, rp_end, tok_base, first_stop, recycled, t,
+                     unsup_d);
   const dim3 tg = grid_for(n_tok);
   hipLaunchKernelGGL(rw_head_kernel, tg, dim3(kLanes), 0, st, t, n_tok, head, plen);
   scan_u64(head, n_tok, tiles2, seg, st);

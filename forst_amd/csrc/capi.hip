@@ -112,6 +112,10 @@ hipError_t feed_setup(BlockArgs& a, uint64_t nw, hipStream_t stream) {
     a.share1 = a.n / (2 * 64 * nw) * 64;
     return hipSuccess;
   }
+  if (mode == "rr0") {  // round-robin chunks only: every wave sweeps the buffer in step
+    a.share1 = 0;
+    return hipSuccess;
+  }
 #endif
   a.share1 = a.n / (2 * 64 * nw) * 64;
   void* p = nullptr;

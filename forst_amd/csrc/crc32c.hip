@@ -1179,17 +1179,22 @@ __device__ __forceinline__ void fill_tables3(uint32_t* L) {
 
 // a row's position (block of the wave share, 1 KiB round) and the block's
 // window, derived once when the block is assigned; row-uniform, one copy per
-// lane
+// lane.  Offsets are relative to base and kept in the form the step's loads
+// use, so a step issues its loads with a few adds (the per-step address
+// arithmetic was a third of a 4 KiB block's VALU instructions).
 struct CRowPos {
-  uint32_t off_lo, off_hi, size, rel, g;
-  uint32_t w0_lo, w0_hi;  // round-0 window start (int64, may be < 0)
-  uint32_t R;             // rounds
-  uint32_t pk;            // cA:1 tA:4 jA:3 q:3 nt:2 m:2 valid:1 slow:1
-  __device__ __forceinline__ uint64_t off() const {
-    return (static_cast<uint64_t>(off_hi) << 32) | off_lo;
+  uint32_t rp_lo, rp_hi;  // this round's window start (int64; < 0 only in round 0 near offset 0)
+  uint32_t tp_lo, tp_hi;  // fast rows: the last round's finishing word t0, minus 4; slow: block offset
+  uint32_t rel;           // descriptor index (kNoBlk: none)
+  uint32_t rl;            // rounds left, this one included
+  // cA:1 tA:4 jA:3 q:3 nt:2 m:2 valid:1 slow:1 xtra:1 d1:2 r0:1 | 24: slow rows' size:4
+  // (every field a fast row needs after the derive is here: 7 VGPRs per copy)
+  uint32_t pk;
+  __device__ __forceinline__ int64_t rp() const {
+    return static_cast<int64_t>((static_cast<uint64_t>(rp_hi) << 32) | rp_lo);
   }
-  __device__ __forceinline__ int64_t w0() const {
-    return static_cast<int64_t>((static_cast<uint64_t>(w0_hi) << 32) | w0_lo);
+  __device__ __forceinline__ uint64_t tp() const {
+    return (static_cast<uint64_t>(tp_hi) << 32) | tp_lo;
   }
   __device__ __forceinline__ uint32_t cA() const { return pk & 1u; }
   __device__ __forceinline__ uint32_t tA() const { return (pk >> 1) & 15u; }
@@ -1200,13 +1205,24 @@ struct CRowPos {
   __device__ __forceinline__ bool valid() const { return (pk >> 15) & 1u; }
   __device__ __forceinline__ bool slow() const { return (pk >> 16) & 1u; }
   __device__ __forceinline__ bool xtra() const { return (pk >> 17) & 1u; }
+  __device__ __forceinline__ uint32_t d1() const { return (pk >> 16) & 12u; }  // bytes: 0, 4, 8
+  __device__ __forceinline__ bool r0() const { return (pk >> 20) & 1u; }
+  __device__ __forceinline__ uint32_t slow_size() const { return (pk >> 24) & 15u; }
+  // fast rows: offset + size of the block (where a trailer goes), from the
+  // window end: E - the type byte when it is in memory
+  template <int MODE>
+  __device__ __forceinline__ uint64_t end(bool mlb) const {
+    const uint64_t t0 = tp() + 4;
+    const uint64_t we = (MODE == kModeVerify || nt() > 0) ? t0 : t0 + 4;
+    return we + nt() - (mlb ? 1u : 0u);
+  }
 };
 
 template <int MODE>
-__device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
-  const uint64_t off = P.off();
-  const bool valid = P.rel != kNoBlk && desc_in_range<MODE>(a, Desc{off, P.size, 0, 0});
-  const uint64_t E = off + P.size + (mem_last_byte<MODE>(a) ? 1u : 0u);
+__device__ __forceinline__ void crow_derive(const BlockArgs& a, uint64_t off, uint32_t size,
+                                            CRowPos& P) {
+  const bool valid = P.rel != kNoBlk && desc_in_range<MODE>(a, Desc{off, size, 0, 0});
+  const uint64_t E = off + size + (mem_last_byte<MODE>(a) ? 1u : 0u);
   const uint64_t ws = off & ~3ull;
   const uint64_t we = E & ~3ull;
   const uint64_t d4 = we - ws;
@@ -1224,19 +1240,32 @@ __device__ __forceinline__ void crow_derive(const BlockArgs& a, CRowPos& P) {
   const uint32_t q = seg_head < 0 ? static_cast<uint32_t>(-seg_head) >> 2 : 0u;
   const uint32_t nt = static_cast<uint32_t>(E - we);
   const uint32_t m = static_cast<uint32_t>(off & 3);
+  // the finishing words: t0 = the tail dword at the window end (verify: the
+  // word holding the stored checksum when nt = 0), t1 = the word after it
+  // (verify, nt > 0) or the extra window dword (compute / trailer, xtra), t2
+  // = the extra window dword (verify, xtra) -- loaded at tp + 4, tp + d1 and
+  // tp, so t0 >= 4 (else the slow path: messages ending in the first dwords)
+  const uint64_t t0 = (nt > 0 || MODE == kModeVerify) ? we : we - 4;
+  const uint32_t d1 = MODE == kModeVerify ? (nt > 0 ? 8u : 4u) : (xtra && nt > 0 ? 0u : 4u);
   // messages without one whole dword take the slow path (its loads are serial
   // and unprefetched: a WAL record of 40 B through it cost a wave ~10 dependent
   // load latencies); everything else, however short, is one prefetched round
-  const bool slow = !valid || d4 < 4;
+  const bool slow = !valid || d4 < 4 || t0 < 4;
+  const uint64_t tp = slow ? off : t0 - 4;
   if (slow) {  // the slow path loads on its own; dummy round loads at [0, 1 KiB)
     R = 1;
     w0 = 0;
   }
-  P.R = R;
-  P.w0_lo = static_cast<uint32_t>(w0);
-  P.w0_hi = static_cast<uint32_t>(static_cast<uint64_t>(w0) >> 32);
-  P.pk = (slow ? 0u : (cA | (tA << 1) | (jA << 5) | (q << 8) | (xtra ? 1u << 17 : 0u))) |
-         (nt << 11) | (m << 13) | (valid ? 1u << 15 : 0u) | (slow ? 1u << 16 : 0u);
+  P.rl = R;
+  P.rp_lo = static_cast<uint32_t>(w0);
+  P.rp_hi = static_cast<uint32_t>(static_cast<uint64_t>(w0) >> 32);
+  P.tp_lo = static_cast<uint32_t>(tp);
+  P.tp_hi = static_cast<uint32_t>(tp >> 32);
+  // a valid slow block has fewer than 12 checksummed bytes (d4 < 4 or t0 < 4)
+  P.pk = (slow ? (valid ? (size & 15u) << 24 : 0u)
+               : (cA | (tA << 1) | (jA << 5) | (q << 8) | (xtra ? 1u << 17 : 0u) |
+                  ((d1 >> 2) << 18))) |
+         (nt << 11) | (m << 13) | (valid ? 1u << 15 : 0u) | (slow ? 1u << 16 : 0u) | (1u << 20);
 }
 
 struct CRStep {
@@ -1248,9 +1277,8 @@ template <int MODE, int PROBE = 0>
 __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, const CRowPos& P,
                                            uint64_t kbeg, CRStep& d) {
   const uint32_t t = lane & 15;
-  const int64_t w0 = P.w0();
   if (PROBE == 3) {  // diagnostics: the same bytes as 16-B aligned, row-contiguous pieces
-    const int64_t rb = (w0 & ~int64_t(15)) + static_cast<int64_t>(P.g) * kRowRound + 16 * t;
+    const int64_t rb = (P.rp() & ~int64_t(15)) + 16 * t;
 #pragma unroll
     for (uint32_t c = 0; c < 2; ++c)
 #pragma unroll
@@ -1270,14 +1298,18 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
   // in front of the head hold no message byte: they are loaded from where
   // they are and discarded by the head reset; only a segment in front of the
   // buffer start (a message ending in its first KiB) is loaded from 0 (the
-  // head lane's is realigned by q dwords in the head step).  No branch: a
-  // step's loads must not depend on one, or the compiler's vmcnt waits for
-  // the current step's data also wait for the step in flight.
-  const int64_t rs = w0 + static_cast<int64_t>(P.g) * kRowRound + kSeg2 * t;
+  // head lane's is realigned by q dwords in the head step).  No branch around
+  // a load: a step's loads must not depend on one, or the compiler's vmcnt
+  // waits for the current step's data also wait for the step in flight.
+  int64_t s0 = P.rp() + kSeg2 * t;
+  int64_t s1 = s0 + kRowChain;
+  if (__ballot(s0 < 0)) {  // rare (addresses only): a round in front of offset 0
+    s0 = s0 < 0 ? 0 : s0;
+    s1 = s1 < 0 ? 0 : s1;
+  }
 #pragma unroll
   for (uint32_t c = 0; c < 2; ++c) {
-    const int64_t so = rs + kRowChain * c;
-    const uint8_t* sp = a.base + (so < 0 ? 0 : so);
+    const uint8_t* sp = a.base + (c ? s1 : s0);
 #pragma unroll
     for (int q = 0; q < 2; ++q) {
       const u32x4a4 v = ld16_a4(sp + 16 * q);
@@ -1287,24 +1319,13 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
       d.w[c][4 * q + 3] = v.w;
     }
   }
-  // the finishing step's words: tail dword at the window end (last round of a
-  // fast block), stored checksum, modifier / type byte / init.  Loaded in
-  // every step (from offset 0 when not needed): a step's load count must not
-  // depend on a branch, or the compiler's vmcnt waits for the current step's
-  // data also wait for the loads of the step in flight.
-  const uint32_t nt = P.nt();
-  const bool lastr = !P.slow() && P.g + 1 >= P.R;
-  const bool xt = MODE != kModeRaw && P.xtra();
-  const uint64_t wE = static_cast<uint64_t>(w0 + static_cast<int64_t>(P.R) * kRowRound);
-  const uint64_t we = wE + (xt ? 4u : 0u);  // the message's last dword boundary
-  const uint64_t t0 = !lastr ? 0 : (nt > 0 || MODE == kModeVerify) ? we : we - 4;
-  d.t0 = ld4v(a.base + t0);
-  // t1: the word after the tail (verify: stored checksum), else the extra
-  // window dword; t2: the extra window dword in verify mode
-  const uint64_t tx = lastr && xt ? wE : t0;
-  d.t1 = MODE == kModeRaw ? 0u
-                          : ld4v(a.base + (MODE == kModeVerify ? (lastr && nt ? t0 + 4 : t0) : tx));
-  d.t2 = MODE == kModeVerify ? ld4v(a.base + tx) : 0u;
+  // the finishing step's words, loaded in every step (from offset 0 when not
+  // needed): a step's load count must not depend on a branch (see above)
+  const bool lastr = !P.slow() && P.rl <= 1;
+  const uint8_t* pb = a.base + (lastr ? P.tp() : 0);
+  d.t0 = ld4_a4(pb + 4);
+  d.t1 = MODE == kModeRaw ? 0u : ld4_a4(pb + P.d1());
+  d.t2 = MODE == kModeVerify ? ld4_a4(pb) : 0u;
   // optional arrays: (read in the ISA) a branch around these loads keeps the
   // compiler's vmcnt waits precise, a pointer select to a zero word does not
   const uint64_t idx = kbeg + (P.rel == kNoBlk ? 0 : P.rel);
@@ -1360,23 +1381,27 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
     const uint32_t sz_n = __shfl(nb.size, src);
     const bool in_n = j >= 64;
-    P.off_lo = in_n ? lo_n : lo_c;
-    P.off_hi = in_n ? hi_n : hi_c;
-    P.size = in_n ? sz_n : sz_c;
+    const uint64_t off = (static_cast<uint64_t>(in_n ? hi_n : hi_c) << 32) | (in_n ? lo_n : lo_c);
+    const uint32_t size = in_n ? sz_n : sz_c;
     const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
     P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoBlk;
-    P.g = 0;
-    crow_derive<MODE>(a, P);
+    crow_derive<MODE>(a, off, size, P);
   };
   uint64_t next = 4;
   CRowPos C;
   fetch(lane >> 4, C);
   auto advance = [&](const CRowPos& P, CRowPos& I) {
-    const bool more = P.rel != kNoBlk && !P.slow() && P.g + 1 < P.R;
+    const bool more = P.rel != kNoBlk && !P.slow() && P.rl > 1;
     const bool need = P.rel != kNoBlk && !more;
     const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
     I = P;
-    if (more) I.g = P.g + 1;
+    if (more) {
+      I.rl = P.rl - 1;
+      I.pk = P.pk & ~(1u << 20);
+      const int64_t rp = P.rp() + kRowRound;
+      I.rp_lo = static_cast<uint32_t>(rp);
+      I.rp_hi = static_cast<uint32_t>(static_cast<uint64_t>(rp) >> 32);
+    }
     // rows in the middle of their blocks (every row, 3 steps in 4 of a batch
     // of 4 KiB blocks): no descriptor work
     if (rows) {
@@ -1388,6 +1413,12 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
         kbrel += kBatch;
         cb = nb;
+#ifndef FORST_HOST_EMULATION
+        // cb's copies are made here, so the batch loads below can land in
+        // nb's registers directly (a load into a temporary and a move after
+        // it waited for every load in flight, the step's prefetch included)
+        asm volatile("" : "+v"(cb.off_lo), "+v"(cb.off_hi), "+v"(cb.size));
+#endif
         cg = ng;
         ng = feed_next(a, nw, lane, feed);
         load_batch<MODE>(a, ng, a.n, lane, nb);
@@ -1414,7 +1445,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     if ((DEPTH == 2 || MODE != kModeRaw) && !live) return false;
     crow_issue<MODE, PROBE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
     const bool fast = C.rel != kNoBlk && !C.slow();
-    const bool r0 = C.g == 0;
+    const bool r0 = C.r0();
     // ---- one 1 KiB round of every row ----
     // A row at round 0 starts its block: its chain states start at 0 (J3(0) =
     // 0), segments wholly in front of the head end the round at state 0, and
@@ -1486,7 +1517,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       }
     }
     // ---- rows that finish a block in this step ----
-    const bool fin = C.rel != kNoBlk && (C.slow() || C.g + 1 >= C.R);
+    const bool fin = C.rel != kNoBlk && (C.slow() || C.rl <= 1);
     if (PROBE != 0 && fin && t == 15 && a.out32) a.out32[C.rel] = s[0] ^ s[1] ^ cu.t0;
     if (PROBE == 0 && __ballot(fin)) {
       // chain states to the row end (A[15 - t]), row XOR, chain 0 over chain 1
@@ -1520,11 +1551,11 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         if (MODE == kModeVerify) stored = nt ? __builtin_amdgcn_alignbyte(cu.t1, cu.t0, nt) : cu.t0;
       }
       if (calc && C.slow() && C.valid()) {
-        const uint8_t* pp = a.base + C.off();
+        const uint8_t* pp = a.base + C.tp();  // slow rows: the block offset
         const uint32_t init = MODE == kModeRaw ? cu.extra : 0u;
-        crc = small_crc2(Lb, K, pp, C.size + (mem_last_byte<MODE>(a) ? 1u : 0u), init,
+        crc = small_crc2(Lb, K, pp, C.slow_size() + (mem_last_byte<MODE>(a) ? 1u : 0u), init,
                          has_extra ? 1u : 0u, cu.extra);
-        if (MODE == kModeVerify) stored = retire(ldu32(pp + C.size + 1));
+        if (MODE == kModeVerify) stored = retire(ldu32(pp + C.slow_size() + 1));
         crc = retire(crc);
       }
       const bool valid = C.valid();
@@ -1548,7 +1579,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
           // byte store per wave instead of five per finishing row
           const uint32_t k = t - 11;
           if (calc && valid && (k != 0 || a.last_bytes)) {
-            uint8_t* pw = a.base_w + C.off() + C.size;
+            uint8_t* pw = a.base_w + C.template end<MODE>(mem_last_byte<MODE>(a));
             pw[k] = static_cast<uint8_t>(k == 0 ? cu.extra : out >> (8 * (k - 1)));
           }
         }

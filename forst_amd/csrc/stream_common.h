@@ -46,7 +46,10 @@ __device__ __forceinline__ uint64_t feed_claim(const BlockArgs& a, uint64_t nw, 
   if (a.ticket) {
     // the whole wave issues the atomic (no divergent branch in the hot loop):
     // lane 0 claims on ticket[0], the other lanes add 0 to their own slots
-    const unsigned long long v = atomicAdd(a.ticket + lane, lane == 0 ? 1ull : 0ull);
+    // (the address is formed here, not hoisted out of the kernel's loop: a
+    // loop-invariant VGPR pair the register allocator would have to keep)
+    const uint32_t l = lane + vzero();
+    const unsigned long long v = atomicAdd(a.ticket + l, l == 0 ? 1ull : 0ull);
     t = uniform64(v);
   } else {
     t = f.rr;

@@ -1346,6 +1346,12 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
 // DEPTH 2 (diagnostics build only): two steps of loads in flight per wave
 // (three step buffers, 12-wave workgroups at 3 waves/SIMD) instead of one.
 constexpr uint32_t kRowsD2Waves = 12;
+#ifdef FORST_DIAG
+// diagnostics build only: per-wave start / end wall clock (100 MHz) of the
+// last rows-kernel launch, for the tail analysis (tools/wave_tail.py)
+constexpr uint32_t kDiagWaves = 8192;
+__device__ unsigned long long g_wave_t0[kDiagWaves], g_wave_t1[kDiagWaves];
+#endif
 template <int MODE, int PROBE, int DEPTH>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
@@ -1364,6 +1370,12 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
 
   // descriptor batches from the work feed: lane j <-> descriptor cg + j (cb),
   // ng + j (nb); a row's rel is the descriptor's global index (n < 2^32 - 1)
+#ifdef FORST_DIAG
+  if (lane == 0 && gw < kDiagWaves) {
+    g_wave_t0[gw] = wall_clock64();
+    g_wave_t1[gw] = 0;
+  }
+#endif
   BatchFeed feed;
   uint64_t cg = feed_first(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
@@ -1436,6 +1448,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   // cu: the current step's data (ready); nx: the buffer that receives the
   // loads issued now (the position DEPTH steps ahead)
   auto step = [&](CRStep& cu, CRStep& nx) -> bool {
+
     // raw mode (WAL records, mixed sizes): no early return (see
     // xxh3_frag_kernel), both step copies issue on every path round the loop
     // and the next step's loads overlap this step's wait (C5 verify / writer
@@ -1620,6 +1633,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       }
     }
   }
+#ifdef FORST_DIAG
+  if (lane == 0 && gw < kDiagWaves) g_wave_t1[gw] = wall_clock64();
+#endif
 }
 
 template <int MODE>
@@ -2089,6 +2105,17 @@ hipError_t launch_wal_record_crc_wave(const WalArgs& a, hipStream_t stream,
 #endif  // FORST_DIAG
 
 }  // namespace forst
+
+#ifdef FORST_DIAG
+// diagnostics build only: per-wave start / end clocks of the last rows launch
+extern "C" __attribute__((visibility("default"))) int forst_diag_wave_times(
+    unsigned long long* t0, unsigned long long* t1, unsigned n) {
+  if (n > forst::kDiagWaves) n = forst::kDiagWaves;
+  if (hipMemcpyFromSymbol(t0, HIP_SYMBOL(forst::g_wave_t0), n * 8) != hipSuccess) return -3;
+  if (hipMemcpyFromSymbol(t1, HIP_SYMBOL(forst::g_wave_t1), n * 8) != hipSuccess) return -3;
+  return 0;
+}
+#endif
 
 #ifdef FORST_DEBUG_BOUNDS
 // diagnostics build only: first out-of-bounds access recorded by the CRC

@@ -1355,6 +1355,7 @@ __device__ unsigned long long g_wave_t0[kDiagWaves], g_wave_t1[kDiagWaves];
 template <int MODE, int PROBE, int DEPTH>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
+  feed_init();
   fill_tables3(L);
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
   const uint32_t lane = threadIdx.x & 63;
@@ -1377,26 +1378,27 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   }
 #endif
   BatchFeed feed;
-  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  constexpr bool kWgFeed = MODE != kModeRaw;  // stream_common.h
+  uint64_t cg = feed_first<kWgFeed>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
-  uint64_t ng = feed_next(a, nw, lane, feed);
+  uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
+  uint64_t ng = feed_next<kWgFeed>(a, nw, lane, feed);
+  uint32_t nlen = feed.len;
   DescBatch cb, nb;
   uint64_t kbrel = 0;  // stream position of cb's first entry
   load_batch<MODE>(a, cg, a.n, lane, cb);
   load_batch<MODE>(a, ng, a.n, lane, nb);
   const uint64_t kbeg = 0;
   auto fetch = [&](uint64_t rel, CRowPos& P) {
-    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
-    const int src = static_cast<int>(j & 63u);
-    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
-    const uint32_t sz_c = __shfl(cb.size, src);
-    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
-    const uint32_t sz_n = __shfl(nb.size, src);
-    const bool in_n = j >= 64;
-    const uint64_t off = (static_cast<uint64_t>(in_n ? hi_n : hi_c) << 32) | (in_n ? lo_n : lo_c);
-    const uint32_t size = in_n ? sz_n : sz_c;
-    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
-    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoBlk;
+    const BatchSlot q = batch_slot(rel, kbrel, cg, clen, ng, nlen, a.n);
+    const uint32_t lo_c = __shfl(cb.off_lo, q.src), hi_c = __shfl(cb.off_hi, q.src);
+    const uint32_t sz_c = __shfl(cb.size, q.src);
+    const uint32_t lo_n = __shfl(nb.off_lo, q.src), hi_n = __shfl(nb.off_hi, q.src);
+    const uint32_t sz_n = __shfl(nb.size, q.src);
+    const uint64_t off =
+        (static_cast<uint64_t>(q.in_n ? hi_n : hi_c) << 32) | (q.in_n ? lo_n : lo_c);
+    const uint32_t size = q.in_n ? sz_n : sz_c;
+    P.rel = q.valid ? static_cast<uint32_t>(q.gi) : kNoBlk;
     crow_derive<MODE>(a, off, size, P);
   };
   uint64_t next = 4;
@@ -1422,8 +1424,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       fetch(next + rank, F);
       next += static_cast<uint64_t>(__popcll(rows));
       if (need) I = F;
-      if (next >= kbrel + kBatch) {  // every block of cb is assigned: slide the batches
-        kbrel += kBatch;
+      if (next >= kbrel + clen) {  // every block of cb is assigned: slide the batches
+        kbrel += clen;
+        clen = nlen;
         cb = nb;
 #ifndef FORST_HOST_EMULATION
         // cb's copies are made here, so the batch loads below can land in
@@ -1432,7 +1435,8 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         asm volatile("" : "+v"(cb.off_lo), "+v"(cb.off_hi), "+v"(cb.size));
 #endif
         cg = ng;
-        ng = feed_next(a, nw, lane, feed);
+        ng = feed_next<kWgFeed>(a, nw, lane, feed);
+        nlen = feed.len;
         load_batch<MODE>(a, ng, a.n, lane, nb);
       }
     }
@@ -1850,6 +1854,8 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
     case CrcKernel::kSimple:
       return launch_kernel(crc32c_block_kernel_simple<M>, grid, kThreads, a, s);
     case CrcKernel::kRows:
+      // block modes: the workgroup feed (stream_common.h), no ticket counter
+      if (M != kModeRaw) return launch_kernel(crc32c_rows_kernel<M>, grid, 64 * kWaves, a, s);
       return launch_fed(crc32c_rows_kernel<M>, grid, kWaves, a, s);
     case CrcKernel::kV2:
       return launch_kernel(crc32c_stream2_kernel<M>, grid, kThreads, a, s);

@@ -16,6 +16,15 @@ namespace forst {
 
 constexpr uint32_t kBatch = 64;
 
+__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
+  // (the builtin returns int: cast before any widening, or it sign-extends)
+  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(l)));
+}
+__device__ __forceinline__ uint64_t readlane64(uint32_t lo, uint32_t hi, uint32_t l) {
+  return (static_cast<uint64_t>(readlane32(hi, l)) << 32) | readlane32(lo, l);
+}
+
+
 // [kbeg, kend): wave gw's contiguous share of n blocks over nw waves
 __device__ __forceinline__ void wave_share(uint64_t n, uint64_t nw, uint64_t gw, uint64_t& kbeg,
                                            uint64_t& kend) {
@@ -24,8 +33,8 @@ __device__ __forceinline__ void wave_share(uint64_t n, uint64_t nw, uint64_t gw,
   kend = kbeg + q + (gw < rem ? 1 : 0);
 }
 
-// Work feed of the rows kernels: a wave consumes a stream of 64-descriptor
-// batches -- first its static share [gw * share1, (gw + 1) * share1)
+// Global work feed of the rows kernels (WG = false): a wave consumes a stream
+// of 64-descriptor batches -- first its static share [gw * share1, (gw + 1) * share1)
 // (share1 a multiple of 64, nw * share1 <= n), then 64-descriptor chunks
 // starting at nw * share1 + 64 * t, t claimed from a.ticket (one atomic per
 // chunk; a wave whose blocks ran long simply claims fewer chunks), or dealt
@@ -38,10 +47,17 @@ struct BatchFeed {
   uint64_t g;    // start of the last batch handed out
   uint64_t lim;  // end of the static share / chunk it belongs to
   uint64_t rr;   // round-robin ticket (no counter)
+  uint32_t len;  // entries of the last batch handed out (0 once exhausted)
 };
 
-__device__ __forceinline__ uint64_t feed_claim(const BlockArgs& a, uint64_t nw, uint32_t lane,
-                                               BatchFeed& f) {
+__device__ __forceinline__ void feed_set_len(const BlockArgs& a, BatchFeed& f) {
+  const uint64_t e = f.lim < a.n ? f.lim : a.n;
+  const uint64_t l = f.g < e ? e - f.g : 0;
+  f.len = static_cast<uint32_t>(l < kBatch ? l : kBatch);
+}
+
+__device__ __forceinline__ uint64_t feed_claim_global(const BlockArgs& a, uint64_t nw,
+                                                      uint32_t lane, BatchFeed& f) {
   uint64_t t;
   if (a.ticket) {
     // the whole wave issues the atomic (no divergent branch in the hot loop):
@@ -57,24 +73,99 @@ __device__ __forceinline__ uint64_t feed_claim(const BlockArgs& a, uint64_t nw, 
   }
   f.g = nw * a.share1 + static_cast<uint64_t>(kBatch) * t;
   f.lim = f.g + kBatch;
+  feed_set_len(a, f);
   return f.g;
 }
 
+// Workgroup feed (WG = true; the CRC rows kernel's block modes): workgroup b
+// owns the contiguous range [b * W, (b + 1) * W) of descriptors (W = n / grid
+// rounded up to 16), and its waves take 16-descriptor batches of it from an
+// LDS counter.
+// - An LDS atomic waits on lgkmcnt only, so a claim does not drain the
+//   wave's loads in flight (a global claim does: vmcnt(0)).
+// - The 16-descriptor grain lets the fast and slow waves of a SIMD finish
+//   together. The four waves of a SIMD progress at different rates
+//   (age-ordered), and the global feed's last 64-descriptor chunk left them
+//   idle for 7-13 % of a C2 launch (tools/wave_tail.py).
+// Workgroups are not balanced against each other: measured, the spread of
+// their finish times is a few per cent on uniform blocks.  Mixed sizes
+// (XXH3 C3, WAL records) keep the global feed.
+constexpr uint32_t kWgChunk = 16;
+__device__ __forceinline__ uint32_t* feed_lds_ctr() {
+  __shared__ uint32_t ctr;
+  return &ctr;
+}
+// zeroes the workgroup counter: before the kernel's first __syncthreads
+__device__ __forceinline__ void feed_init() {
+  if (threadIdx.x == 0) *feed_lds_ctr() = 0;
+}
+__device__ __forceinline__ uint64_t feed_claim_wg(const BlockArgs& a, uint32_t lane,
+                                                  BatchFeed& f) {
+  uint32_t p = 0;
+  if (lane == 0) p = atomicAdd(feed_lds_ctr(), kWgChunk);
+  p = readlane32(p, 0);
+  const uint64_t G = gridDim.x;
+  const uint64_t W = ((a.n + G - 1) / G + kWgChunk - 1) / kWgChunk * kWgChunk;
+  const uint64_t lo = blockIdx.x * W < a.n ? blockIdx.x * W : a.n;
+  const uint64_t hi = lo + W < a.n ? lo + W : a.n;
+  f.g = lo + p;
+  if (f.g >= hi) {
+    f.g = a.n;  // exhausted (stays so)
+    f.len = 0;
+  } else {
+    f.len = static_cast<uint32_t>(hi - f.g < kWgChunk ? hi - f.g : kWgChunk);
+  }
+  f.lim = f.g + f.len;
+  return f.g;
+}
+
+template <bool WG>
 __device__ __forceinline__ uint64_t feed_first(const BlockArgs& a, uint64_t nw, uint64_t gw,
                                                uint32_t lane, BatchFeed& f) {
   f.rr = gw;
-  if (a.share1 == 0) return feed_claim(a, nw, lane, f);
+  if (WG) return feed_claim_wg(a, lane, f);
+  if (a.share1 == 0) return feed_claim_global(a, nw, lane, f);
   f.g = gw * a.share1;
   f.lim = f.g + a.share1;
+  feed_set_len(a, f);
   return f.g;
 }
 
+template <bool WG>
 __device__ __forceinline__ uint64_t feed_next(const BlockArgs& a, uint64_t nw, uint32_t lane,
                                               BatchFeed& f) {
-  if (f.g >= a.n) return f.g;  // exhausted: stays exhausted, no more claims
+  if (f.g >= a.n) {  // exhausted: stays exhausted, no more claims
+    f.len = 0;
+    return f.g;
+  }
+  if (WG) return feed_claim_wg(a, lane, f);
   f.g += kBatch;
-  if (f.g < f.lim) return f.g;
-  return feed_claim(a, nw, lane, f);
+  if (f.g < f.lim) {
+    feed_set_len(a, f);
+    return f.g;
+  }
+  return feed_claim_global(a, nw, lane, f);
+}
+
+// where stream position rel lies in the (current, next) batch pair of
+// lengths clen / nlen: the source lane, which batch, the descriptor index and
+// whether it exists
+struct BatchSlot {
+  int src;
+  bool in_n, valid;
+  uint64_t gi;
+};
+__device__ __forceinline__ BatchSlot batch_slot(uint64_t rel, uint64_t kbrel, uint64_t cg,
+                                                uint32_t clen, uint64_t ng, uint32_t nlen,
+                                                uint64_t n) {
+  const uint32_t j = static_cast<uint32_t>(rel - kbrel);
+  BatchSlot b;
+  b.in_n = j >= clen;
+  const uint32_t k = b.in_n ? j - clen : j;
+  b.src = static_cast<int>(k & 63u);
+  b.gi = (b.in_n ? ng : cg) + k;
+  b.valid = k < (b.in_n ? nlen : clen) && b.gi < n;
+  return b;
 }
 
 // per-lane descriptor batch (lane j <-> block kb + j)
@@ -102,14 +193,6 @@ __device__ __forceinline__ void load_batch(const BlockArgs& a, uint64_t kb, uint
     const uint8_t* lp = a.last_bytes ? a.last_bytes : reinterpret_cast<const uint8_t*>(a.sizes);
     d.extra = lp[i];
   }
-}
-
-__device__ __forceinline__ uint32_t readlane32(uint32_t v, uint32_t l) {
-  // (the builtin returns int: cast before any widening, or it sign-extends)
-  return static_cast<uint32_t>(__builtin_amdgcn_readlane(static_cast<int>(v), static_cast<int>(l)));
-}
-__device__ __forceinline__ uint64_t readlane64(uint32_t lo, uint32_t hi, uint32_t l) {
-  return (static_cast<uint64_t>(readlane32(hi, l)) << 32) | readlane32(lo, l);
 }
 
 // descriptor k (kb <= k < kb + 128) from the current / next batch, uniform

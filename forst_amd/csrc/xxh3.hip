@@ -749,27 +749,26 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kern
   // message cg + j (cb), ng + j (nb); a row's rel is the message's global
   // index (n < 2^32 - 1), kbrel the stream position of cb's first entry
   BatchFeed feed;
-  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  uint64_t cg = feed_first<false>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
-  uint64_t ng = feed_next(a, nw, lane, feed);
+  uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
+  uint64_t ng = feed_next<false>(a, nw, lane, feed);
+  uint32_t nlen = feed.len;
   const uint64_t kbeg = 0;
   DescBatch cb, nb;
   uint64_t kbrel = 0;
   load_batch<MODE>(a, cg, a.n, lane, cb);
   load_batch<MODE>(a, ng, a.n, lane, nb);
   auto fetch = [&](uint64_t rel, RowPos& P) {
-    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
-    const int src = static_cast<int>(j & 63u);
-    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
-    const uint32_t sz_c = __shfl(cb.size, src);
-    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
-    const uint32_t sz_n = __shfl(nb.size, src);
-    const bool in_n = j >= 64;
-    P.off_lo = in_n ? lo_n : lo_c;
-    P.off_hi = in_n ? hi_n : hi_c;
-    P.size = in_n ? sz_n : sz_c;
-    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
-    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoMsg;
+    const BatchSlot q = batch_slot(rel, kbrel, cg, clen, ng, nlen, a.n);
+    const uint32_t lo_c = __shfl(cb.off_lo, q.src), hi_c = __shfl(cb.off_hi, q.src);
+    const uint32_t sz_c = __shfl(cb.size, q.src);
+    const uint32_t lo_n = __shfl(nb.off_lo, q.src), hi_n = __shfl(nb.off_hi, q.src);
+    const uint32_t sz_n = __shfl(nb.size, q.src);
+    P.off_lo = q.in_n ? lo_n : lo_c;
+    P.off_hi = q.in_n ? hi_n : hi_c;
+    P.size = q.in_n ? sz_n : sz_c;
+    P.rel = q.valid ? static_cast<uint32_t>(q.gi) : kNoMsg;
     P.g = 0;
   };
   // rows start on messages 0..3 of the stream
@@ -793,11 +792,13 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kern
       fetch(next + rank, F);
       next += static_cast<uint64_t>(__popcll(rows));
       if (need) I = F;
-      if (next >= kbrel + kBatch) {  // every message of cb is assigned: slide the batches
-        kbrel += kBatch;
+      if (next >= kbrel + clen) {  // every message of cb is assigned: slide the batches
+        kbrel += clen;
+        clen = nlen;
         cb = nb;
         cg = ng;
-        ng = feed_next(a, nw, lane, feed);
+        ng = feed_next<false>(a, nw, lane, feed);
+        nlen = feed.len;
         load_batch<MODE>(a, ng, a.n, lane, nb);
       }
     }
@@ -1074,27 +1075,26 @@ xxh3_frag_kernel(BlockArgs a) {
   const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
   const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
   BatchFeed feed;
-  uint64_t cg = feed_first(a, nw, gw, lane, feed);
+  uint64_t cg = feed_first<false>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
-  uint64_t ng = feed_next(a, nw, lane, feed);
+  uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
+  uint64_t ng = feed_next<false>(a, nw, lane, feed);
+  uint32_t nlen = feed.len;
   DescBatch cb, nb;
   uint64_t kbrel = 0;
   load_batch<kModeRaw>(a, cg, a.n, lane, cb);  // extra = frag_info (init_crcs)
   load_batch<kModeRaw>(a, ng, a.n, lane, nb);
   auto fetch = [&](uint64_t rel, FRow& P) {
-    const uint32_t j = static_cast<uint32_t>(rel - kbrel);
-    const int src = static_cast<int>(j & 63u);
-    const bool in_n = j >= 64;
-    const uint32_t lo_c = __shfl(cb.off_lo, src), hi_c = __shfl(cb.off_hi, src);
-    const uint32_t sz_c = __shfl(cb.size, src), in_c = __shfl(cb.extra, src);
-    const uint32_t lo_n = __shfl(nb.off_lo, src), hi_n = __shfl(nb.off_hi, src);
-    const uint32_t sz_n = __shfl(nb.size, src), in_nn = __shfl(nb.extra, src);
-    P.off_lo = in_n ? lo_n : lo_c;
-    P.off_hi = in_n ? hi_n : hi_c;
-    P.size = in_n ? sz_n : sz_c;
-    P.info = in_n ? in_nn : in_c;
-    const uint64_t gi = (in_n ? ng : cg) + (j & 63u);
-    P.rel = gi < a.n ? static_cast<uint32_t>(gi) : kNoMsg;
+    const BatchSlot q = batch_slot(rel, kbrel, cg, clen, ng, nlen, a.n);
+    const uint32_t lo_c = __shfl(cb.off_lo, q.src), hi_c = __shfl(cb.off_hi, q.src);
+    const uint32_t sz_c = __shfl(cb.size, q.src), in_c = __shfl(cb.extra, q.src);
+    const uint32_t lo_n = __shfl(nb.off_lo, q.src), hi_n = __shfl(nb.off_hi, q.src);
+    const uint32_t sz_n = __shfl(nb.size, q.src), in_nn = __shfl(nb.extra, q.src);
+    P.off_lo = q.in_n ? lo_n : lo_c;
+    P.off_hi = q.in_n ? hi_n : hi_c;
+    P.size = q.in_n ? sz_n : sz_c;
+    P.info = q.in_n ? in_nn : in_c;
+    P.rel = q.valid ? static_cast<uint32_t>(q.gi) : kNoMsg;
     frow_start(P);
   };
   const uint32_t row = lane >> 4;
@@ -1115,11 +1115,13 @@ xxh3_frag_kernel(BlockArgs a) {
       fetch(next + rank, F);
       next += static_cast<uint64_t>(__popcll(rows));
       if (need) I = F;
-      if (next >= kbrel + kBatch) {
-        kbrel += kBatch;
+      if (next >= kbrel + clen) {
+        kbrel += clen;
+        clen = nlen;
         cb = nb;
         cg = ng;
-        ng = feed_next(a, nw, lane, feed);
+        ng = feed_next<false>(a, nw, lane, feed);
+        nlen = feed.len;
         load_batch<kModeRaw>(a, ng, a.n, lane, nb);
 #ifndef FORST_HOST_EMULATION
         // retire the descriptor loads on this (rare) path: left pending, they

@@ -203,6 +203,7 @@ inline uint32_t atomicXor(uint32_t* p, uint32_t v) { return __atomic_fetch_xor(p
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);
 }
+inline uint32_t atomicAdd(uint32_t* p, uint32_t v) { return __atomic_fetch_add(p, v, __ATOMIC_RELAXED); }
 inline uint32_t atomicOr(uint32_t* p, uint32_t v) { return __atomic_fetch_or(p, v, __ATOMIC_RELAXED); }
 inline unsigned long long atomicMin(unsigned long long* p, unsigned long long v) {
   unsigned long long cur = __atomic_load_n(p, __ATOMIC_RELAXED);

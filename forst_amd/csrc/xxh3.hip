@@ -23,6 +23,10 @@ namespace {
 
 constexpr uint32_t kWaves = 4;  // 256-thread workgroups, no LDS
 constexpr uint32_t kThreads = kWaves * 64;
+// the rows kernel: one 12-wave workgroup per CU (3 waves per SIMD), so the
+// workgroup feed (stream_common.h) balances every wave of a CU
+constexpr uint32_t kRowsWaves = 12;
+constexpr uint32_t kRowsThreads = kRowsWaves * 64;
 
 __device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
   h ^= h >> 33;
@@ -725,9 +729,11 @@ __device__ __forceinline__ void rows_issue(const BlockArgs& a, uint32_t lane, co
 }
 
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kernel(BlockArgs a) {
+__global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
+    xxh3_rows_kernel(BlockArgs a) {
   __shared__ uint64_t cold[4 * kColdN];
   __shared__ uint64_t shsec[64];
+  feed_init();
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   short_secrets_fill(shsec, threadIdx.x);
   __syncthreads();
@@ -743,16 +749,16 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kern
     K1[k] = sec64(8 * (s4 + 4 * k) + 16 * p + 8);
   }
   const uint64_t ks0 = sec64(128 + 16 * p), ks1 = sec64(136 + 16 * p);
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kRowsWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kRowsWaves + wave;
   // descriptor batches from the work feed (stream_common.h): lane j <->
   // message cg + j (cb), ng + j (nb); a row's rel is the message's global
   // index (n < 2^32 - 1), kbrel the stream position of cb's first entry
   BatchFeed feed;
-  uint64_t cg = feed_first<false>(a, nw, gw, lane, feed);
+  uint64_t cg = feed_first<MODE != kModeRaw>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
-  uint64_t ng = feed_next<false>(a, nw, lane, feed);
+  uint64_t ng = feed_next<MODE != kModeRaw>(a, nw, lane, feed);
   uint32_t nlen = feed.len;
   const uint64_t kbeg = 0;
   DescBatch cb, nb;
@@ -797,7 +803,7 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(3) xxh3_rows_kern
         clen = nlen;
         cb = nb;
         cg = ng;
-        ng = feed_next<false>(a, nw, lane, feed);
+        ng = feed_next<MODE != kModeRaw>(a, nw, lane, feed);
         nlen = feed.len;
         load_batch<MODE>(a, ng, a.n, lane, nb);
       }
@@ -1370,7 +1376,7 @@ template <int MODE>
 uint32_t rows_occupancy() {
   static const uint32_t occ = [] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_rows_kernel<MODE>, kThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_rows_kernel<MODE>, kRowsThreads, 0) !=
             hipSuccess ||
         o < 1)
       o = 1;
@@ -1392,8 +1398,9 @@ enum class XxKernel {
 #endif
 };
 
-hipError_t launch_kernel(void (*k)(BlockArgs), uint32_t grid, BlockArgs a, hipStream_t s) {
-  hipLaunchKernelGGL(k, dim3(grid), dim3(kThreads), 0, s, a);
+hipError_t launch_kernel(void (*k)(BlockArgs), uint32_t grid, BlockArgs a, hipStream_t s,
+                         uint32_t threads = kThreads) {
+  hipLaunchKernelGGL(k, dim3(grid), dim3(threads), 0, s, a);
   return hipGetLastError();
 }
 
@@ -1419,12 +1426,14 @@ hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const
     case XxKernel::kRows: {
       *name = kNames[1][M];
       const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
-          1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),
+          1, std::min<uint64_t>((a.n + 4 * kRowsWaves - 1) / (4 * kRowsWaves),
                                 uint64_t(di.num_cus) * rows_occupancy<M>())));
+      // block modes: the workgroup feed (stream_common.h), no ticket counter
+      if (M != kModeRaw) return launch_kernel(xxh3_rows_kernel<M>, grid, a, s, kRowsThreads);
       BlockArgs b = a;
-      hipError_t e = feed_setup(b, uint64_t(grid) * kWaves, s);
+      hipError_t e = feed_setup(b, uint64_t(grid) * kRowsWaves, s);
       if (e != hipSuccess) return e;
-      e = launch_kernel(xxh3_rows_kernel<M>, grid, b, s);
+      e = launch_kernel(xxh3_rows_kernel<M>, grid, b, s, kRowsThreads);
       const hipError_t f = scratch_free(b.ticket, s);
       return e != hipSuccess ? e : f;
     }

@@ -1378,7 +1378,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   }
 #endif
   BatchFeed feed;
-  constexpr bool kWgFeed = MODE != kModeRaw;  // stream_common.h
+  // block modes: the workgroup feed; WAL records (raw) keep the global one,
+  // measured 4 % faster for them (stream_common.h)
+  constexpr bool kWgFeed = MODE != kModeRaw;
   uint64_t cg = feed_first<kWgFeed>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)

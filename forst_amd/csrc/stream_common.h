@@ -99,13 +99,14 @@ __device__ __forceinline__ uint32_t* feed_lds_ctr() {
 __device__ __forceinline__ void feed_init() {
   if (threadIdx.x == 0) *feed_lds_ctr() = 0;
 }
+template <uint32_t CHUNK>
 __device__ __forceinline__ uint64_t feed_claim_wg(const BlockArgs& a, uint32_t lane,
                                                   BatchFeed& f) {
   uint32_t p = 0;
-  if (lane == 0) p = atomicAdd(feed_lds_ctr(), kWgChunk);
+  if (lane == 0) p = atomicAdd(feed_lds_ctr(), CHUNK);
   p = readlane32(p, 0);
   const uint64_t G = gridDim.x;
-  const uint64_t W = ((a.n + G - 1) / G + kWgChunk - 1) / kWgChunk * kWgChunk;
+  const uint64_t W = ((a.n + G - 1) / G + CHUNK - 1) / CHUNK * CHUNK;
   const uint64_t lo = blockIdx.x * W < a.n ? blockIdx.x * W : a.n;
   const uint64_t hi = lo + W < a.n ? lo + W : a.n;
   f.g = lo + p;
@@ -113,17 +114,19 @@ __device__ __forceinline__ uint64_t feed_claim_wg(const BlockArgs& a, uint32_t l
     f.g = a.n;  // exhausted (stays so)
     f.len = 0;
   } else {
-    f.len = static_cast<uint32_t>(hi - f.g < kWgChunk ? hi - f.g : kWgChunk);
+    f.len = static_cast<uint32_t>(hi - f.g < CHUNK ? hi - f.g : CHUNK);
   }
   f.lim = f.g + f.len;
   return f.g;
 }
 
-template <bool WG>
+// WG: the workgroup feed in CHUNK-descriptor batches (16 for blocks of KiBs;
+// items of a few hundred bytes take 64: fewer batch loads per byte)
+template <bool WG, uint32_t CHUNK = kWgChunk>
 __device__ __forceinline__ uint64_t feed_first(const BlockArgs& a, uint64_t nw, uint64_t gw,
                                                uint32_t lane, BatchFeed& f) {
   f.rr = gw;
-  if (WG) return feed_claim_wg(a, lane, f);
+  if (WG) return feed_claim_wg<CHUNK>(a, lane, f);
   if (a.share1 == 0) return feed_claim_global(a, nw, lane, f);
   f.g = gw * a.share1;
   f.lim = f.g + a.share1;
@@ -131,14 +134,14 @@ __device__ __forceinline__ uint64_t feed_first(const BlockArgs& a, uint64_t nw, 
   return f.g;
 }
 
-template <bool WG>
+template <bool WG, uint32_t CHUNK = kWgChunk>
 __device__ __forceinline__ uint64_t feed_next(const BlockArgs& a, uint64_t nw, uint32_t lane,
                                               BatchFeed& f) {
   if (f.g >= a.n) {  // exhausted: stays exhausted, no more claims
     f.len = 0;
     return f.g;
   }
-  if (WG) return feed_claim_wg(a, lane, f);
+  if (WG) return feed_claim_wg<CHUNK>(a, lane, f);
   f.g += kBatch;
   if (f.g < f.lim) {
     feed_set_len(a, f);

@@ -27,6 +27,11 @@ constexpr uint32_t kThreads = kWaves * 64;
 // workgroup feed (stream_common.h) balances every wave of a CU
 constexpr uint32_t kRowsWaves = 12;
 constexpr uint32_t kRowsThreads = kRowsWaves * 64;
+// the fragment kernel (WAL records): 4-wave workgroups and the global feed
+// (the workgroup feed measured 5 % slower on C5's log-uniform records)
+constexpr bool kFragWg = false;
+constexpr uint32_t kFragWaves = kWaves;
+constexpr uint32_t kFragThreads = kFragWaves * 64;
 
 __device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
   h ^= h >> 33;
@@ -1060,13 +1065,14 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
 // WPE: waves per SIMD the register allocation targets (3, the default: 168
 // VGPRs with a few spilled dwords, C5 a14 21.5 vs 24.8 ms at 2: 181 VGPRs)
 template <int WPE>
-__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(WPE)
+__global__ void __launch_bounds__(kFragThreads) FORST_WAVES_PER_EU(WPE)
 xxh3_frag_kernel(BlockArgs a) {
   // cold per-pair constants and the accumulate keys live in LDS (registers
   // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
   __shared__ uint64_t cold[4 * kColdN];
   __shared__ uint64_t keys[24];
   __shared__ uint64_t shsec[64];
+  if (kFragWg) feed_init();
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   if (threadIdx.x < 24) keys[threadIdx.x] = sec64(8 * threadIdx.x);
   short_secrets_fill(shsec, threadIdx.x);
@@ -1078,13 +1084,13 @@ xxh3_frag_kernel(BlockArgs a) {
   // K0[k] = keys[s4 + 2p + 4k], K1[k] = keys[s4 + 2p + 4k + 1]
   // (the scramble keys sec64(128 + 16p), sec64(136 + 16p) are keys[16 + 2p],
   // keys[17 + 2p], read where used: one spilled register pair fewer)
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kWaves;
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kWaves + wave;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kFragWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kFragWaves + wave;
   BatchFeed feed;
-  uint64_t cg = feed_first<false>(a, nw, gw, lane, feed);
+  uint64_t cg = feed_first<kFragWg, 64>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
-  uint64_t ng = feed_next<false>(a, nw, lane, feed);
+  uint64_t ng = feed_next<kFragWg, 64>(a, nw, lane, feed);
   uint32_t nlen = feed.len;
   DescBatch cb, nb;
   uint64_t kbrel = 0;
@@ -1126,7 +1132,7 @@ xxh3_frag_kernel(BlockArgs a) {
         clen = nlen;
         cb = nb;
         cg = ng;
-        ng = feed_next<false>(a, nw, lane, feed);
+        ng = feed_next<kFragWg, 64>(a, nw, lane, feed);
         nlen = feed.len;
         load_batch<kModeRaw>(a, ng, a.n, lane, nb);
 #ifndef FORST_HOST_EMULATION
@@ -1461,7 +1467,7 @@ template <int WPE>
 uint32_t frag_occupancy() {
   static const uint32_t occ = [] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE>, kThreads, 0) !=
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE>, kFragThreads, 0) !=
             hipSuccess ||
         o < 1)
       o = 1;
@@ -1474,13 +1480,13 @@ template <int WPE>
 hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name) {
   const DeviceInfo& di = device_info();
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
-      1, std::min<uint64_t>((a.n + 4 * kWaves - 1) / (4 * kWaves),
+      1, std::min<uint64_t>((a.n + 4 * kFragWaves - 1) / (4 * kFragWaves),
                             uint64_t(di.num_cus) * frag_occupancy<WPE>())));
   BlockArgs b = a;
-  hipError_t e = feed_setup(b, uint64_t(grid) * kWaves, stream);
+  hipError_t e = feed_setup(b, uint64_t(grid) * kFragWaves, stream);
   if (e != hipSuccess) return e;
   *name = WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
-  hipLaunchKernelGGL(xxh3_frag_kernel<WPE>, dim3(grid), dim3(kThreads), 0, stream, b);
+  hipLaunchKernelGGL(xxh3_frag_kernel<WPE>, dim3(grid), dim3(kFragThreads), 0, stream, b);
   e = hipGetLastError();
   const hipError_t f = scratch_free(b.ticket, stream);
   return e != hipSuccess ? e : f;

@@ -1947,17 +1947,16 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream
 #endif
   // The rows kernel (one block per 16-lane row) up to 20 KiB mean block
   // size, the v2 kernel (two 4 KiB steps in flight per wave) above
-  // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2 %; v2 wins on
+  // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2-5 %; v2 wins on
   // the 4/16/64 KiB mix by 4 % and at 64 KiB by 45 %, where the rows of a
-  // wave stream addresses 64 KiB apart) ... and only with at least four
-  // 64-block chunks per wave: the rows kernel's work feed deals 64-block
-  // chunks, so with fewer the last chunk is a large part of a wave's work
-  // (C4, 512 K x 16 KiB: rows 0.645, v2 0.714).  The rows kernel indexes
-  // descriptors with 32 bits.  Buffers shorter than one 4 KiB round take the
-  // simple kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
+  // wave stream addresses 64 KiB apart).  Round 1 also required four
+  // 64-block chunks per wave (the global feed's last chunk); with the
+  // workgroup feed's 16-block batches the rows kernel wins C4 (512 K x
+  // 16 KiB) too: 0.732 vs v2 0.697.  The rows kernel indexes descriptors
+  // with 32 bits.  Buffers shorter than one 4 KiB round take the simple
+  // kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
   const uint64_t mean = a.base_len / a.n;
-  const bool small_blocks =
-      mean <= 20480 && (mean <= 8192 || a.n >= uint64_t(4) * kBatch * kWaves * grid);
+  const bool small_blocks = mean <= 20480;
   CrcKernel k = a.base_len < kRB ? CrcKernel::kSimple
                 : (a.n < 0xffffffffull && (a.kernel_hint ? a.kernel_hint == 1 : small_blocks))
                     ? CrcKernel::kRows

@@ -1945,20 +1945,17 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream
     if (e != hipSuccess) return e;
   }
 #endif
-  // The rows kernel (one block per 16-lane row) up to 20 KiB mean block
-  // size, the v2 kernel (two 4 KiB steps in flight per wave) above
-  // (measured: rows wins at 4 KiB by 10-12 %, at 16 KiB by 2-5 %; v2 wins on
-  // the 4/16/64 KiB mix by 4 % and at 64 KiB by 45 %, where the rows of a
-  // wave stream addresses 64 KiB apart).  Round 1 also required four
-  // 64-block chunks per wave (the global feed's last chunk); with the
-  // workgroup feed's 16-block batches the rows kernel wins C4 (512 K x
-  // 16 KiB) too: 0.732 vs v2 0.697.  The rows kernel indexes descriptors
-  // with 32 bits.  Buffers shorter than one 4 KiB round take the simple
+  // The rows kernel (one block per 16-lane row) for every block size.  In
+  // round 1 the v2 kernel (one block per wave, two 4 KiB steps in flight)
+  // won above 8-20 KiB; with the workgroup feed (stream_common.h) the rows
+  // kernel matches or beats it everywhere (profiles/ab_r02_late/
+  // rows_vs_v2_wgfeed.log, same box: 64 KiB 0.740 vs 0.736, the 4/16/64 KiB
+  // mix 0.726 vs 0.666, 512 K x 16 KiB 0.748 vs 0.705).  v2 remains for
+  // batches of 2^32 - 1 or more descriptors (the rows kernel indexes them
+  // with 32 bits).  Buffers shorter than one 4 KiB round take the simple
   // kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
-  const uint64_t mean = a.base_len / a.n;
-  const bool small_blocks = mean <= 20480;
   CrcKernel k = a.base_len < kRB ? CrcKernel::kSimple
-                : (a.n < 0xffffffffull && (a.kernel_hint ? a.kernel_hint == 1 : small_blocks))
+                : (a.n < 0xffffffffull && (a.kernel_hint ? a.kernel_hint == 1 : true))
                     ? CrcKernel::kRows
                     : CrcKernel::kV2;
 #ifdef FORST_DIAG

@@ -1504,15 +1504,15 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,
                               const char** name) {
   if (a.n == 0) return hipSuccess;
-  // the rows kernel indexes descriptors with 32 bits; uniform >= 48 KiB blocks
-  // go to v1 (rows of a wave streaming addresses 64 KiB apart camp on the
-  // same HBM channels: X64 rows 0.49 vs v1 0.62 of the peak; C3's 4/16/64 KiB
-  // mix stays on rows, 0.67 vs 0.53).  Buffers shorter than 4 KiB take the
-  // simple kernel (the streaming kernels' dummy loads read [0, 4 KiB)).
-  const bool big = a.base_len / a.n >= 49152;
-  XxKernel k = a.base_len < 4096                     ? XxKernel::kSimple
-               : (a.n >= 0xffffffffull || big) ? XxKernel::kV1
-                                                     : XxKernel::kRows;
+  // the rows kernel for every block size (it indexes descriptors with 32
+  // bits).  Round 1 sent uniform >= 48 KiB blocks to v1 (X64 rows 0.49 vs v1
+  // 0.62); with the workgroup feed rows win there too (X64 0.759 vs 0.644,
+  // profiles/ab_r02_late/xxh3_rows_vs_v1_wgfeed.log).  Buffers shorter than
+  // 4 KiB take the simple kernel (the streaming kernels' dummy loads read
+  // [0, 4 KiB)).
+  XxKernel k = a.base_len < 4096           ? XxKernel::kSimple
+               : a.n >= 0xffffffffull ? XxKernel::kV1
+                                           : XxKernel::kRows;
   // kernel_hint 3: one message per wave (a short list of long messages, e.g.
   // wal_hash.h's gathered records: rows would leave most rows idle while a
   // few walk 32 KiB records 1 KiB per step)

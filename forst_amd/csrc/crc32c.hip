@@ -1165,15 +1165,40 @@ constexpr uint32_t kRowChain = 512;
 constexpr uint32_t kLds3Bytes = kOffB2 + 4096;
 constexpr uint32_t kNoBlk = 0xffffffffu;
 
+// NT = the workgroup's thread count: constant trip counts, so every load of
+// the fill is issued before the first LDS store waits (a loop with a
+// blockDim trip count waited out one round of loads per iteration)
+template <uint32_t NT>
 __device__ __forceinline__ void fill_tables3(uint32_t* L) {
   const uint32_t tid = threadIdx.x;
-  const uint32_t nt = blockDim.x;
-  for (uint32_t i = tid; i < 16384; i += nt) {
-    const uint32_t e = i >> 6, d = i & 63, t = (d >> 3) & 3;
-    L[i] = d < 32 ? kCrcG[t * 256 + e] : kCrcJ3[t * 256 + e];
+  constexpr uint32_t kN1 = (16384 + NT - 1) / NT, kN2 = (15 * 1024 + NT - 1) / NT,
+                     kN3 = (1024 + NT - 1) / NT;
+  uint32_t v1[kN1], v2[kN2], v3[kN3];
+#pragma unroll
+  for (uint32_t k = 0; k < kN1; ++k) {
+    const uint32_t i = tid + k * NT;
+    const uint32_t e = (i >> 6) & 255, d = i & 63, t = (d >> 3) & 3;
+    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e] : kCrcJ3[t * 256 + e]) : 0u;
   }
-  for (uint32_t i = tid; i < 15 * 1024; i += nt) L[kOffA2 / 4 + i] = kCrcA[i];
-  for (uint32_t i = tid; i < 1024; i += nt) L[kOffB2 / 4 + i] = kCrcB[i];
+#pragma unroll
+  for (uint32_t k = 0; k < kN2; ++k) {
+    const uint32_t i = tid + k * NT;
+    v2[k] = i < 15 * 1024 ? kCrcA[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kN3; ++k) {
+    const uint32_t i = tid + k * NT;
+    v3[k] = i < 1024 ? kCrcB[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kN1; ++k)
+    if (tid + k * NT < 16384) L[tid + k * NT] = v1[k];
+#pragma unroll
+  for (uint32_t k = 0; k < kN2; ++k)
+    if (tid + k * NT < 15 * 1024) L[kOffA2 / 4 + tid + k * NT] = v2[k];
+#pragma unroll
+  for (uint32_t k = 0; k < kN3; ++k)
+    if (tid + k * NT < 1024) L[kOffB2 / 4 + tid + k * NT] = v3[k];
   __syncthreads();
 }
 
@@ -1356,7 +1381,7 @@ template <int MODE, int PROBE, int DEPTH>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
   feed_init();
-  fill_tables3(L);
+  fill_tables3<64 * (DEPTH == 2 ? kRowsD2Waves : kWaves)>(L);
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);

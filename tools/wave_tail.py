@@ -32,6 +32,8 @@ def main():
     ap.add_argument("--feed", action="append", default=[])
     ap.add_argument("--mode", default="verify", choices=["verify", "compute"])
     ap.add_argument("--reps", type=int, default=3)
+    ap.add_argument("--wal", type=int, default=0,
+                    help="also: the C5-shaped WAL verify with this many records (raw CRC rows kernel)")
     args = ap.parse_args()
     L = _lib.lib()
     fn = L.forst_diag_wave_times
@@ -51,11 +53,16 @@ def main():
                 os.environ.pop("FORST_FEED", None)
             rows = []
             for _ in range(args.reps):
+                ev0 = torch.cuda.Event(enable_timing=True)
+                ev1 = torch.cuda.Event(enable_timing=True)
+                ev0.record()
                 if args.mode == "verify":
                     engine.block_verify_batch(ct, b.base, b.offsets, b.sizes)
                 else:
                     engine.block_checksum_batch(ct, b.base, b.offsets, b.sizes, last_bytes=b.types)
+                ev1.record()
                 torch.cuda.synchronize()
+                call_us = ev0.elapsed_time(ev1) * 1e3
                 assert fn(t0.ctypes.data, t1.ctypes.data, nw) == 0
                 live = t1 > 0
                 s0 = t0[live].astype(np.int64)
@@ -71,6 +78,7 @@ def main():
                     "end_by_wg_mod8": by_xcd,
                     "waves": int(live.sum()),
                     "span_us": span / 100.0,
+                    "call_us_hip_events": round(call_us, 1),
                     "idle_mean_frac": float(idle.mean() / span),
                     "idle_p50_frac": float(np.median(idle) / span),
                     "idle_max_frac": float(idle.max() / span),
@@ -81,6 +89,24 @@ def main():
             print(json.dumps({f"{cfg}|{feed or 'default'}": rows[-1]}), flush=True)
         del b
         torch.cuda.empty_cache()
+    if args.wal:
+        w = workload.make_wal_batch(args.wal, workload.SEEDS["C5"])
+        for _ in range(args.reps):
+            engine.wal_verify_batch(w.log)
+            torch.cuda.synchronize()
+        assert fn(t0.ctypes.data, t1.ctypes.data, nw) == 0
+        live = t1 > 0
+        s0 = t0[live].astype(np.int64)
+        e = t1[live].astype(np.int64)
+        span = e.max() - s0.min()
+        idle = e.max() - e
+        gidx = np.nonzero(live)[0]
+        endf = (e - s0.min()) / span
+        r = {"end_by_wave_in_wg": [round(float(endf[(gidx % 16) == k].mean()), 3) for k in range(16)],
+             "waves": int(live.sum()), "span_us": span / 100.0,
+             "idle_mean_frac": float(idle.mean() / span), "idle_max_frac": float(idle.max() / span)}
+        res["C5_wal_verify"] = r
+        print(json.dumps({"C5_wal_verify": r}), flush=True)
     print(json.dumps(res, indent=1))
 
 

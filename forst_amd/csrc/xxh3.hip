@@ -27,6 +27,9 @@ constexpr uint32_t kThreads = kWaves * 64;
 // workgroup feed (stream_common.h) balances every wave of a CU
 constexpr uint32_t kRowsWaves = 12;
 constexpr uint32_t kRowsThreads = kRowsWaves * 64;
+// workgroup-feed batch (stream_common.h): 8 descriptors, two per row (16
+// measured 1 % slower on C3, 0.3 % on NS16X)
+constexpr uint32_t kXxWgChunk = 8;
 // the fragment kernel (WAL records): 4-wave workgroups and the global feed
 // (the workgroup feed measured 5 % slower on C5's log-uniform records)
 constexpr bool kFragWg = false;
@@ -760,10 +763,10 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
   // message cg + j (cb), ng + j (nb); a row's rel is the message's global
   // index (n < 2^32 - 1), kbrel the stream position of cb's first entry
   BatchFeed feed;
-  uint64_t cg = feed_first<MODE != kModeRaw>(a, nw, gw, lane, feed);
+  uint64_t cg = feed_first<MODE != kModeRaw, kXxWgChunk>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
-  uint64_t ng = feed_next<MODE != kModeRaw>(a, nw, lane, feed);
+  uint64_t ng = feed_next<MODE != kModeRaw, kXxWgChunk>(a, nw, lane, feed);
   uint32_t nlen = feed.len;
   const uint64_t kbeg = 0;
   DescBatch cb, nb;
@@ -808,7 +811,7 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
         clen = nlen;
         cb = nb;
         cg = ng;
-        ng = feed_next<MODE != kModeRaw>(a, nw, lane, feed);
+        ng = feed_next<MODE != kModeRaw, kXxWgChunk>(a, nw, lane, feed);
         nlen = feed.len;
         load_batch<MODE>(a, ng, a.n, lane, nb);
       }

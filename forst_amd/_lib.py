@@ -8,9 +8,7 @@ import os
 import subprocess
 
 _HERE = os.path.dirname(os.path.abspath(__file__))
-# FORST_LIB_PATH: another build of the same library (A/B of two builds in
-# separate processes, tools/gpu_build_ab.sh); the default is the in-tree build
-LIB_PATH = os.environ.get("FORST_LIB_PATH") or os.path.join(_HERE, "lib", "libforst_checksum.so")
+LIB_PATH = os.path.join(_HERE, "lib", "libforst_checksum.so")
 CSRC = os.path.join(_HERE, "csrc")
 
 _lib = None
@@ -34,6 +32,17 @@ def exported_symbols():
         text = f.read()
     return sorted(set(re.findall(r"^\s*(?:int|uint32_t|uint64_t|const char\*)\s+(forst_\w+)\(",
                                  text, re.M)))
+
+
+def use_library(path):
+    """Load another build of the same C ABI instead of the in-tree product
+    library -- for the A/B and diagnostics tools under tools/ only, which
+    call this explicitly before the first engine call.  The product reads no
+    environment variable to choose its library."""
+    global LIB_PATH
+    if _lib is not None:
+        raise ForstError(f"{LIB_PATH} is already loaded")
+    LIB_PATH = os.path.abspath(path)
 
 
 def lib():

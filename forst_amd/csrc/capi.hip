@@ -369,7 +369,7 @@ FORST_API int forst_wal_recover_batch(const uint8_t* log, uint64_t log_len, uint
                   "wal_recover launch");
   if (rc == FORST_OK && result->unsupported)
     return set_error(FORST_EUNSUPPORTED,
-                     "WAL compression / user-defined timestamp size records (types 9-11)");
+                     "WAL compression: a kSetCompressionType record names kZSTD");
   return rc;
 }
 

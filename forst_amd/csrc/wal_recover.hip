@@ -35,10 +35,29 @@
 //   hash     XXH3_64bits of every logical record (wal_hash.h): in place
 //            across the fragment headers when laid out as a writer lays them
 //            out, else from a gathered copy             (one sync: gathered bytes)
+//
+// The reader's behaviour is reproduced to the letter, as its compiled code
+// shows it (tests/golden/gen_wal_golden.py pins this file to the reference's
+// own log::Reader): a type byte is read through `const char*` into an
+// unsigned int (log_reader.cc:469), so 0x80..0xFF sign-extend; types 12..17
+// with a valid CRC are the reader's own results kEof .. kBadRecordChecksum
+// (log_reader.h:173-186), consumed without clearing the buffer; the XXH3
+// state is reset only when ReadRecord starts and at "partial record without
+// end(2)" (:73-79, :119-124), so a fragmented record's checksum covers the
+// fragments of records aborted since (use() of the fragment accessor); and
+// kSetCompressionType / timestamp-size records (types 9-11, :167-213) clear
+// scratch but keep in_fragmented_record, so a segment they head inherits
+// the previous segment's state (rw_live).  Their decode / duplicate checks
+// depend on state kept across the whole log (compression record seen,
+// recorded column families): the few such records are read back and
+// decided on the host, in reader order (ctl_* below).
 #include <hip/hip_runtime.h>
 
 #include <cstdint>
+#include <algorithm>
 #include <cstring>
+#include <unordered_map>
+#include <vector>
 
 #include "../../include/forst_checksum.h"
 #include "device_common.h"
@@ -53,6 +72,7 @@ constexpr uint32_t kLogBlock = 32768;  // db/log_format.h:45
 constexpr uint32_t kLogHdr = 7;        // :48
 constexpr uint32_t kLogRHdr = 11;      // :52
 constexpr uint32_t kLanes = 256;
+constexpr uint32_t kCtlRep = 3;        // host-decided reports per control record (at most)
 
 // block terminal events (the reader's result when it leaves the block)
 enum : uint32_t {
@@ -63,12 +83,23 @@ enum : uint32_t {
   kEvOldStop,      // kOldRecord (not skip mode): reading ends
   kEvBadHeader,    // truncated header at EOF (kBadHeader): reading ends
   kEvBadLenEof,    // kBadRecordLen at EOF: reading ends
+  kEvPseudo,       // a record of type 12..17 that ends reading (its own token)
 };
 
 // token kinds
 enum : uint8_t {
   kTkFull = 1, kTkFirst, kTkMiddle, kTkLast, kTkUnknown, kTkOldSkip, kTkZero, kTkChecksum,
   kTkBadLen, kTkStopHeader, kTkStopBadLenEof, kTkStopOld, kTkStopRecycled, kTkStopEof,
+  kTkCtlComp,  // kSetCompressionType (9)
+  kTkCtlTs,    // kUserDefinedTimestampSizeType (10) / its recyclable form (11)
+  // records whose type is one of the reader's own results (log_reader.h:173-186)
+  kTkPEof,     // 12 kEof
+  kTkPOld,     // 15 kOldRecord, not kSkipAnyCorruptedRecords: as kEof
+  kTkPBad,     // 13 kBadRecord (and 15 in kSkipAnyCorruptedRecords)
+  kTkPHeader,  // 14 kBadHeader, drop 0
+  kTkPLenEof,  // 16 kBadRecordLen while eof_, drop 0
+  kTkPLen,     // 16 kBadRecordLen, drop 0, buffer kept
+  kTkPCrc,     // 17 kBadRecordChecksum, drop 0, buffer kept
 };
 
 struct RecoverArgs {
@@ -90,6 +121,15 @@ __device__ __forceinline__ uint32_t unmask(uint32_t m) {  // util/crc32c.h:39
   const uint32_t r = m - 0xa282ead8u;
   return (r >> 17) | (r << 15);
 }
+__device__ __forceinline__ bool eof_block(const RecoverArgs& a, uint64_t b) {
+  return a.log_len - b * kLogBlock < kLogBlock;  // ReadMore read short: eof_
+}
+// a record of type 12..17 with a valid CRC that ends reading (ReadRecord
+// :236-305 reached through the aliased result)
+__device__ __forceinline__ bool pseudo_stops(uint32_t ty, bool eofb, uint32_t recycled, int mode) {
+  return ty == 12 || ty == 14 || (ty == 15 && mode != 3) ||
+         (ty == 16 && (eofb || (recycled && mode == 0))) || (ty == 17 && recycled && mode == 0);
+}
 
 // ---- walk -------------------------------------------------------------------
 // items: header offsets of the physical records the reader parses in block b
@@ -101,26 +141,26 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
                                   uint32_t* ipack) {
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
-  const bool eof_block = end - start < kLogBlock;  // ReadMore read short: eof_
+  const bool eofb = end - start < kLogBlock;
   uint64_t pos = start;
   uint32_t n = 0, e = kEvNone;
   while (true) {
     const uint64_t rem = end - pos;
     if (rem < kLogHdr) {  // trailer skipped, or a truncated header at EOF
-      if (rem > 0 && eof_block) e = kEvBadHeader;
+      if (rem > 0 && eofb) e = kEvBadHeader;
       break;
     }
     const uint8_t* h = a.log + pos;
     const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t type = h[6];
+    const uint32_t type = h[6];  // the byte; sign extension matters only in reports
     const bool recyc = recyclable_type(type);
     const uint32_t hs = recyc ? kLogRHdr : kLogHdr;
     if (rem < hs) {
-      if (eof_block) e = kEvBadHeader;
+      if (eofb) e = kEvBadHeader;
       break;
     }
     if (hs + length > rem) {
-      e = eof_block ? kEvBadLenEof : kEvBadLen;
+      e = eofb ? kEvBadLenEof : kEvBadLen;
       break;
     }
     if (recyc && ld_le32(h + 7) != a.log_number) {
@@ -179,10 +219,11 @@ __global__ void __launch_bounds__(kLanes) rw_fill_kernel(RecoverArgs a, const ui
 }
 
 // ---- per block: CRC truncation, reader position, stop -------------------------
-// acc[b] = items consumed before the first CRC mismatch; the event becomes
-// kEvChecksum at that record; rp_end[b] = reader position when leaving the
+// acc[b] = items consumed before the first CRC mismatch (a stopping pseudo
+// record included); the event becomes kEvChecksum at a mismatch, kEvPseudo
+// at a stopping pseudo record; rp_end[b] = reader position when leaving the
 // block (end of the last consumed record, or the block end after a
-// buffer-clearing event); ntok[b] = consumed items + the event token
+// buffer-clearing event)
 __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const uint64_t* cnt,
                                                           const uint64_t* base,
                                                           const uint64_t* it_off,
@@ -190,25 +231,25 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
                                                           const uint64_t* crc_off,
                                                           const uint32_t* crc_len,
                                                           const uint32_t* crc_stored,
+                                                          const uint32_t* ipack,
                                                           const uint32_t* computed, uint32_t* ev,
                                                           uint32_t* ev_pos, uint64_t* acc,
                                                           uint64_t* rp_end,
                                                           unsigned long long* first_stop,
-                                                          uint32_t recycled) {
+                                                          const uint32_t* recycled_d) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
+  const uint32_t recycled = *recycled_d;
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
+  const bool eofb = eof_block(a, b);
   const uint64_t n = cnt[b], i0 = base[b];
   uint64_t k = 0, last_end = start;
   uint32_t e = ev[b], ep = ev_pos[b];
-  // the fill's per-item arrays (stored CRC, record extent); the header is
-  // re-read only for skipped old records (kSkipAnyCorruptedRecords)
   for (; k < n; ++k) {
+    const uint32_t pk = ipack[i0 + k];
     if (it_old[i0 + k]) {
-      const uint8_t* h = a.log + it_off[i0 + k];
-      const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-      last_end = it_off[i0 + k] + (recyclable_type(h[6]) ? kLogRHdr : kLogHdr) + length;
+      last_end = it_off[i0 + k] + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr) + (pk & 0xffffu);
       continue;
     }
     if (crc_stored[i0 + k] != computed[i0 + k]) {
@@ -217,6 +258,12 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
       break;
     }
     last_end = crc_off[i0 + k] + crc_len[i0 + k];
+    if (pseudo_stops((pk >> 16) & 0xffu, eofb, recycled, a.mode)) {
+      ++k;
+      e = kEvPseudo;
+      ep = static_cast<uint32_t>(last_end - start);
+      break;
+    }
   }
   acc[b] = k;
   ev[b] = e;
@@ -227,10 +274,12 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
   rp_end[b] = clears ? end : (e == kEvOldStop ? start + ep : last_end);
   // recycled log + kTolerateCorruptedTailRecords: a checksum / length error
   // ends reading silently (log_reader.cc:288-291)
-  const bool stop = e == kEvOldStop || e == kEvBadHeader || e == kEvBadLenEof ||
+  const bool stop = e == kEvOldStop || e == kEvBadHeader || e == kEvBadLenEof || e == kEvPseudo ||
                     ((e == kEvChecksum || e == kEvBadLen) && recycled && a.mode == 0);
   if (stop) atomicMin(first_stop, static_cast<unsigned long long>(b));
 }
+
+__device__ __forceinline__ bool event_token(uint32_t e) { return e != kEvNone && e != kEvPseudo; }
 
 __global__ void __launch_bounds__(kLanes) rw_ntok_kernel(RecoverArgs a, const uint64_t* acc,
                                                          const uint32_t* ev,
@@ -242,12 +291,13 @@ __global__ void __launch_bounds__(kLanes) rw_ntok_kernel(RecoverArgs a, const ui
     ntok[b] = *first_stop == ~0ull ? 1 : 0;
     return;
   }
-  ntok[b] = b > *first_stop ? 0 : acc[b] + (ev[b] != kEvNone ? 1 : 0);
+  ntok[b] = b > *first_stop ? 0 : acc[b] + (event_token(ev[b]) ? 1 : 0);
 }
 
 // tokens: kind, item (physical record index; events: block), payload length
 // (events: dropped bytes), reader position (physical_record_offset of the
 // reference, end_of_buffer_offset_ - buffer_.size() before the read), type
+// byte (sign-extended where reported)
 struct Tokens {
   uint8_t* kind;
   uint64_t* item;
@@ -255,6 +305,26 @@ struct Tokens {
   uint64_t* pos;
   uint8_t* type;
 };
+
+__device__ __forceinline__ uint8_t record_kind(uint32_t type, bool eofb, uint32_t recycled, int mode) {
+  const uint32_t nt = (type >= 5 && type <= 8) ? type - 4 : type;  // recyclable -> legacy
+  switch (nt) {
+    case 1: return kTkFull;
+    case 2: return kTkFirst;
+    case 3: return kTkMiddle;
+    case 4: return kTkLast;
+    case 9: return kTkCtlComp;
+    case 10:
+    case 11: return kTkCtlTs;
+    case 12: return kTkPEof;
+    case 13: return kTkPBad;
+    case 14: return kTkPHeader;
+    case 15: return mode == 3 ? kTkPBad : kTkPOld;
+    case 16: return eofb ? kTkPLenEof : (recycled && mode == 0 ? kTkStopRecycled : kTkPLen);
+    case 17: return recycled && mode == 0 ? kTkStopRecycled : kTkPCrc;
+    default: return kTkUnknown;
+  }
+}
 
 __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const uint64_t* base,
                                                           const uint64_t* it_off,
@@ -265,10 +335,12 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
                                                           const uint64_t* rp_end,
                                                           const uint64_t* tok_base,
                                                           const unsigned long long* first_stop,
-                                                          uint32_t recycled, Tokens t,
-                                                          uint32_t* unsupported) {
+                                                          const uint32_t* recycled_d, Tokens t,
+                                                          uint64_t* ctl_list, uint64_t ctl_cap,
+                                                          unsigned long long* ctl_n) {
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b > a.n_blocks) return;
+  const uint32_t recycled = *recycled_d;
   uint64_t o = tok_base[b];
   if (b == a.n_blocks) {
     if (*first_stop == ~0ull) {  // kEof at the reader position after the last block
@@ -283,6 +355,7 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
   if (b > *first_stop) return;
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
+  const bool eofb = eof_block(a, b);
   uint64_t rp = b == 0 ? 0 : rp_end[b - 1];  // reader position entering the block
   const uint64_t n = acc[b], i0 = base[b];
   for (uint64_t k = 0; k < n; ++k, ++o) {
@@ -290,16 +363,11 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
     const uint32_t pk = ipack[i0 + k];  // the fill's header fields (no header re-read)
     const uint32_t length = pk & 0xffffu;
     const uint32_t type = (pk >> 16) & 0xffu;
-    const uint32_t nt = (type >= 5 && type <= 8) ? type - 4 : type;  // recyclable -> legacy
-    uint8_t kind = nt == 1   ? kTkFull
-                   : nt == 2 ? kTkFirst
-                   : nt == 3 ? kTkMiddle
-                   : nt == 4 ? kTkLast
-                             : kTkUnknown;
-    if (it_old[i0 + k]) kind = kTkOldSkip;
-    // kSetCompressionType / (recyclable) kUserDefinedTimestampSizeType records
-    // change how the reader decodes what follows: not handled on the device
-    if (kind == kTkUnknown && (type == 9 || type == 10 || type == 11)) atomicOr(unsupported, 1u);
+    const uint8_t kind = it_old[i0 + k] ? kTkOldSkip : record_kind(type, eofb, recycled, a.mode);
+    if (kind == kTkCtlComp || kind == kTkCtlTs) {  // decided on the host, in reader order
+      const unsigned long long c = atomicAdd(ctl_n, 1ull);
+      if (c < ctl_cap) ctl_list[c] = o;
+    }
     t.kind[o] = kind;
     t.item[o] = i0 + k;
     t.len[o] = length;
@@ -308,7 +376,7 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
     rp = off + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr) + length;
   }
   const uint32_t e = ev[b];
-  if (e == kEvNone) return;
+  if (!event_token(e)) return;
   const bool recyc_stop = (e == kEvChecksum || e == kEvBadLen) && recycled && a.mode == 0;
   uint8_t kind = e == kEvChecksum   ? kTkChecksum
                  : e == kEvBadLen   ? kTkBadLen
@@ -325,6 +393,7 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
 }
 
 __device__ __forceinline__ bool is_head(uint8_t k) { return k != kTkMiddle && k != kTkLast; }
+__device__ __forceinline__ bool is_ctl(uint8_t k) { return k == kTkCtlComp || k == kTkCtlTs; }
 __device__ __forceinline__ bool is_payload(uint8_t k) {
   return k == kTkFull || k == kTkFirst || k == kTkMiddle || k == kTkLast;
 }
@@ -350,44 +419,92 @@ __global__ void __launch_bounds__(kLanes) rw_seg_kernel(Tokens t, uint64_t n, co
   if (t.kind[i] == kTkLast && s > 0) atomicMin(seg_first_last + s, static_cast<unsigned long long>(i));
 }
 
+// live[s]: in_fragmented_record holds inside segment s.  A First starts a
+// fragmented record; a control record (types 9-11) keeps the state it finds
+// (log_reader.cc:167-213), i.e. that of the segment before it -- a run of
+// control-headed segments is resolved by walking back to the segment that
+// decides; every other head clears it
+__global__ void __launch_bounds__(kLanes) rw_live_kernel(Tokens t, uint64_t n, const uint64_t* head,
+                                                         const uint64_t* seg,
+                                                         const uint64_t* seg_head,
+                                                         const unsigned long long* seg_fl,
+                                                         uint8_t* live) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= n || !head[i]) return;
+  const uint8_t k = t.kind[i];
+  uint8_t l = k == kTkFirst ? 1 : 0;
+  if (is_ctl(k)) {
+    for (uint64_t x = seg[i] - 1; x > 0; --x) {
+      if (seg_fl[x] != ~0ull) break;  // a record completed there: not in a fragmented record
+      const uint8_t kx = t.kind[seg_head[x]];
+      if (kx == kTkFirst) {
+        l = 1;
+        break;
+      }
+      if (!is_ctl(kx)) break;
+    }
+  }
+  live[seg[i]] = l;
+}
+
 // reasons (forst_wal_report.reason)
 enum : uint32_t {
   kRpPartial1 = 1, kRpPartial2, kRpMissing1, kRpMissing2, kRpMiddle, kRpChecksum, kRpBadLen,
-  kRpTruncHeader, kRpTrailing, kRpTruncBody, kRpUnknown,
+  kRpTruncHeader, kRpTrailing, kRpTruncBody, kRpUnknown, kRpCompMultiple, kRpCompNotFirst,
+  kRpCompDecode, kRpTsInterspersed, kRpTsDecode, kRpTsZero, kRpTsDuplicate,
 };
 
 struct Fsm {
   const uint64_t* seg;
   const uint64_t* seg_head;
   const unsigned long long* seg_first_last;
+  const uint8_t* live;
   const uint64_t* pl;  // exclusive prefix of payload lengths
   const uint64_t* plen;
 };
 
-// the reader's fragment state entering head token i: the previous segment
-// is an unfinished First segment (in_fragmented_record), scratch = its bytes
-__device__ __forceinline__ void prev_state(const Tokens& t, const Fsm& f, uint64_t i, bool* in_frag,
+// the reader's fragment state entering head token i: in_fragmented_record
+// and the size of scratch (the previous segment's payload since its head;
+// control heads carry no payload)
+__device__ __forceinline__ void prev_state(const Fsm& f, uint64_t i, bool* in_frag,
                                            uint64_t* scratch) {
   const uint64_t s = f.seg[i];
   *in_frag = false;
   *scratch = 0;
   if (s < 2) return;
-  const uint64_t h = f.seg_head[s - 1];
-  if (t.kind[h] != kTkFirst || f.seg_first_last[s - 1] != ~0ull) return;
+  if (!f.live[s - 1] || f.seg_first_last[s - 1] != ~0ull) return;
   *in_frag = true;
-  *scratch = f.pl[i] - f.pl[h];  // B + M payloads up to this head
+  *scratch = f.pl[i] - f.pl[f.seg_head[s - 1]];
 }
 
-// per token: emitted logical records (0/1) and reports (0-2) -- or, with
-// WRITE, the records and reports themselves at their scanned positions
+// host-decided reports of the control records (ctl_list sorted by token)
+struct CtlReps {
+  const uint64_t* tok;
+  uint64_t n;
+  const uint32_t* cnt;
+  const uint32_t* reason;  // [n][kCtlRep]
+  const uint64_t* bytes;
+  __device__ uint64_t find(uint64_t i) const {
+    uint64_t lo = 0, hi = n;
+    while (lo < hi) {
+      const uint64_t mid = (lo + hi) / 2;
+      if (tok[mid] < i) lo = mid + 1; else hi = mid;
+    }
+    return lo;
+  }
+};
+
+// per token: emitted logical records (0/1) and reports -- or, with WRITE,
+// the records and reports themselves at their scanned positions
 template <bool WRITE>
 __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, Fsm f, int mode,
                                                          uint64_t* n_emit, uint64_t* n_rep,
                                                          const uint64_t* emit_at,
-                                                         const uint64_t* rep_at,
+                                                         const uint64_t* rep_at, CtlReps cr,
                                                          forst_wal_records recs, uint64_t rec_cap,
                                                          forst_wal_reports reps, uint64_t rep_cap,
-                                                         uint64_t* rec_head_tok) {
+                                                         uint64_t* rec_hash_begin,
+                                                         uint64_t* rec_last_tok) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= n) return;
   const uint8_t k = t.kind[i];
@@ -404,21 +521,20 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
   };
   const uint64_t s = f.seg[i];
   if (k == kTkMiddle || k == kTkLast) {
-    const uint64_t h = s ? f.seg_head[s] : ~0ull;
-    const bool b_seg = s && t.kind[h] == kTkFirst;
+    const bool live = s && f.live[s];
     const unsigned long long fl = s ? f.seg_first_last[s] : ~0ull;
     if (k == kTkMiddle) {
-      if (!(b_seg && (fl == ~0ull || i < fl))) rep(kRpMissing1, t.len[i]);
-    } else if (b_seg && fl == i) {
+      if (!(live && (fl == ~0ull || i < fl))) rep(kRpMissing1, t.len[i]);
+    } else if (live && fl == i) {
       emit = true;
-      first = h;
+      first = f.seg_head[s];
     } else {
       rep(kRpMissing2, t.len[i]);
     }
   } else {
     bool in_frag;
     uint64_t scratch;
-    prev_state(t, f, i, &in_frag, &scratch);
+    prev_state(f, i, &in_frag, &scratch);
     switch (k) {
       case kTkFull:
         if (in_frag && scratch) rep(kRpPartial1, scratch);
@@ -432,6 +548,7 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
         break;
       case kTkOldSkip:
       case kTkZero:
+      case kTkPBad:
         if (in_frag) rep(kRpMiddle, scratch);
         break;
       case kTkChecksum:
@@ -439,59 +556,144 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
         rep(k == kTkChecksum ? kRpChecksum : kRpBadLen, t.len[i]);
         if (in_frag) rep(kRpMiddle, scratch);
         break;
+      case kTkPLen:
+      case kTkPCrc:
+        rep(k == kTkPCrc ? kRpChecksum : kRpBadLen, 0);
+        if (in_frag) rep(kRpMiddle, scratch);
+        break;
       case kTkStopHeader:
-        if (strict) rep(kRpTruncHeader, t.len[i]);
+      case kTkPHeader:
+        if (strict) rep(kRpTruncHeader, k == kTkPHeader ? 0 : t.len[i]);
         if (strict && in_frag) rep(kRpTrailing, scratch);
         break;
       case kTkStopEof:
       case kTkStopOld:
+      case kTkPEof:
+      case kTkPOld:
         if (strict && in_frag) rep(kRpTrailing, scratch);
         break;
       case kTkStopBadLenEof:
-        if (strict) rep(kRpTruncBody, t.len[i]);
+      case kTkPLenEof:
+        if (strict) rep(kRpTruncBody, k == kTkPLenEof ? 0 : t.len[i]);
         break;
-      default:  // kTkStopRecycled: scratch cleared, no report
+      case kTkCtlTs:
+        if (in_frag && scratch) rep(kRpTsInterspersed, scratch);
+        break;
+      default:  // kTkStopRecycled: scratch cleared, no report; kTkCtlComp: host reports
         break;
     }
   }
+  uint64_t xj = 0;
+  uint32_t nx = 0;  // host-decided reports after the device's
+  if (is_ctl(k) && cr.n) {
+    xj = cr.find(i);
+    if (xj < cr.n && cr.tok[xj] == i) nx = cr.cnt[xj];
+  }
   if (!WRITE) {
     n_emit[i] = emit ? 1 : 0;
-    n_rep[i] = static_cast<uint64_t>(nr);
+    n_rep[i] = static_cast<uint64_t>(nr) + nx;
     return;
   }
   if (emit) {
     const uint64_t j = emit_at[i];
+    // the XXH3 state feeding this record was last reset where ReadRecord
+    // started (the token after the previous emitted record) or at a
+    // "partial record without end(2)" First; a Full record is hashed alone
+    uint64_t hb = i;
+    if (k == kTkLast) {
+      hb = first;
+      while (hb > 0 && !n_emit[hb - 1]) {
+        if (t.kind[hb] == kTkFirst) {
+          bool in_frag;
+          uint64_t scratch;
+          prev_state(f, hb, &in_frag, &scratch);
+          if (in_frag && scratch) break;
+        }
+        --hb;
+      }
+    }
+    rec_hash_begin[j] = hb;
+    rec_last_tok[j] = i;
     if (j < rec_cap) {
       recs.offset[j] = t.pos[first];  // Reader::LastRecordOffset
       recs.length[j] = f.pl[i] + f.plen[i] - f.pl[first];
-      recs.n_fragments[j] = static_cast<uint32_t>(i - first + 1);
-      rec_head_tok[j] = first;
+      recs.n_fragments[j] = static_cast<uint32_t>(i - first + 1 - (is_ctl(t.kind[first]) ? 1 : 0));
     }
   }
-  for (int r = 0; r < nr; ++r) {
+  // unknown record type %u: the type byte as the reader's unsigned int
+  const uint32_t ty = static_cast<uint32_t>(static_cast<int32_t>(static_cast<int8_t>(t.type[i])));
+  for (int r = 0; r < nr + static_cast<int>(nx); ++r) {
     const uint64_t j = rep_at[i] + r;
     if (j < rep_cap) {
+      const bool dev = r < nr;
       if (reps.offset) reps.offset[j] = t.pos[i];
-      if (reps.bytes) reps.bytes[j] = bytes[r];
-      if (reps.reason) reps.reason[j] = reason[r];
-      if (reps.type) reps.type[j] = t.type[i];
+      if (reps.bytes) reps.bytes[j] = dev ? bytes[r] : cr.bytes[xj * kCtlRep + (r - nr)];
+      if (reps.reason) reps.reason[j] = dev ? reason[r] : cr.reason[xj * kCtlRep + (r - nr)];
+      if (reps.type) reps.type[j] = ty;
     }
   }
 }
 
-// ---- hashing (wal_hash.h): record j = tokens head_tok[j] .. + n_frag[j] - 1 --
+// control records' fields for the host: token, kind, payload offset and
+// length, records emitted before it (first_record_read_)
+struct CtlInfo {
+  uint64_t tok;
+  uint64_t payload;
+  uint64_t emitted_before;
+  uint32_t len;
+  uint32_t kind;
+};
+__global__ void __launch_bounds__(kLanes) rw_ctl_info_kernel(Tokens t, const uint64_t* it_off,
+                                                             const uint32_t* ipack,
+                                                             const uint64_t* list, uint64_t n,
+                                                             const uint64_t* emit_at,
+                                                             CtlInfo* info) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (j >= n) return;
+  const uint64_t q = list[j];
+  const uint64_t it = t.item[q];
+  const uint32_t pk = ipack[it];
+  CtlInfo c;
+  c.tok = q;
+  c.payload = it_off[it] + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr);
+  c.emitted_before = emit_at[q];
+  c.len = pk & 0xffffu;
+  c.kind = t.kind[q];
+  info[j] = c;
+}
+
+__global__ void __launch_bounds__(kLanes) rw_ctl_add_kernel(const uint64_t* tok, const uint32_t* cnt,
+                                                            uint64_t n, uint64_t* n_rep) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (j < n) n_rep[tok[j]] += cnt[j];
+}
+
+// ---- hashing (wal_hash.h): record j = tokens hash_begin[j] .. last_tok[j],
+// the fragments the XXH3 state was fed (use) -----------------------------------
 struct RecFrags {
-  const uint64_t* head_tok;
-  const uint32_t* n_frag;
+  const uint64_t* hash_begin;
+  const uint64_t* last_tok;
+  const uint8_t* kind;
   const uint64_t* item;
   const uint64_t* it_off;
   const uint32_t* ipack;  // item: length | type << 16 | recyclable << 24 (rw_fill)
-  __device__ uint64_t begin(uint64_t j) const { return head_tok[j]; }
-  __device__ uint64_t end(uint64_t j) const { return head_tok[j] + n_frag[j]; }
+  const uint64_t* seg;
+  const uint8_t* live;
+  const unsigned long long* seg_fl;
+  __device__ uint64_t begin(uint64_t j) const { return hash_begin[j]; }
+  __device__ uint64_t end(uint64_t j) const { return last_tok[j] + 1; }
   __device__ uint64_t header(uint64_t q) const { return it_off[item[q]]; }
   __device__ uint32_t hs(uint64_t q) const { return (ipack[item[q]] >> 24) & 1u ? kLogRHdr : kLogHdr; }
   __device__ uint32_t len(uint64_t q) const { return ipack[item[q]] & 0xffffu; }
-  __device__ bool use(uint64_t) const { return true; }
+  // fed to XXH3_64bits_update: a First always; a Middle / Last while
+  // in_fragmented_record (log_reader.cc:119-157); a Full is hashed alone
+  __device__ bool use(uint64_t q) const {
+    const uint8_t k = kind[q];
+    if (k == kTkFull || k == kTkFirst) return true;
+    if (k != kTkMiddle && k != kTkLast) return false;
+    const uint64_t s = seg[q];
+    return s && live[s] && (seg_fl[s] == ~0ull || q <= seg_fl[s]);
+  }
 };
 
 __global__ void rw_recycled_kernel(RecoverArgs a, uint32_t* flag) {
@@ -504,7 +706,8 @@ size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
 dim3 grid_for(uint64_t n) { return dim3(static_cast<uint32_t>((n + kLanes - 1) / kLanes ? (n + kLanes - 1) / kLanes : 1)); }
 
-// a bump allocator over one scratch allocation
+// a bump allocator over one scratch allocation; with p == nullptr it only
+// measures (the same sequence of takes sizes the allocation)
 struct Arena {
   uint8_t* p;
   size_t used;
@@ -515,6 +718,135 @@ struct Arena {
     return r;
   }
 };
+
+// phase-1 arrays (per log block)
+struct P1 {
+  uint64_t *cnt, *ibase, *acc, *rp_end, *tiles;
+  uint32_t *ev, *ev_pos, *recycled;
+  unsigned long long *first_stop, *ctl_n;
+  void take(Arena& A, uint64_t nb) {
+    cnt = A.take<uint64_t>(nb + 1);
+    ibase = A.take<uint64_t>(nb + 1);
+    acc = A.take<uint64_t>(nb + 1);
+    rp_end = A.take<uint64_t>(nb + 1);
+    tiles = A.take<uint64_t>((nb + 1) / kScanTile + 2);
+    ev = A.take<uint32_t>(nb + 1);
+    ev_pos = A.take<uint32_t>(nb + 1);
+    recycled = A.take<uint32_t>(1);
+    first_stop = A.take<unsigned long long>(1);
+    ctl_n = A.take<unsigned long long>(1);
+  }
+};
+
+constexpr uint64_t kCtlCap = 4096;
+
+// phase-2 arrays (per item / token)
+struct P2 {
+  uint64_t *it_off, *crc_off;
+  uint8_t* it_old;
+  uint32_t *crc_len, *crc_stored, *ipack, *computed;
+  Tokens t;
+  uint64_t *ntok, *tok_base, *head, *plen, *pl, *seg, *seg_head, *n_emit, *n_rep, *emit_at, *rep_at,
+      *tiles2, *ctl_list;
+  unsigned long long* seg_fl;
+  uint8_t* live;
+  void take(Arena& A, uint64_t ni, uint64_t nb, uint64_t nt) {
+    it_off = A.take<uint64_t>(ni);
+    it_old = A.take<uint8_t>(ni);
+    crc_off = A.take<uint64_t>(ni);
+    crc_len = A.take<uint32_t>(ni);
+    crc_stored = A.take<uint32_t>(ni);
+    ipack = A.take<uint32_t>(ni);
+    computed = A.take<uint32_t>(ni);
+    t.kind = A.take<uint8_t>(nt);
+    t.item = A.take<uint64_t>(nt);
+    t.len = A.take<uint32_t>(nt);
+    t.pos = A.take<uint64_t>(nt);
+    t.type = A.take<uint8_t>(nt);
+    ntok = A.take<uint64_t>(nb + 2);
+    tok_base = A.take<uint64_t>(nb + 2);
+    head = A.take<uint64_t>(nt);
+    plen = A.take<uint64_t>(nt);
+    pl = A.take<uint64_t>(nt);
+    seg = A.take<uint64_t>(nt);
+    seg_head = A.take<uint64_t>(nt + 1);
+    seg_fl = A.take<unsigned long long>(nt + 1);
+    live = A.take<uint8_t>(nt + 1);
+    n_emit = A.take<uint64_t>(nt);
+    n_rep = A.take<uint64_t>(nt);
+    emit_at = A.take<uint64_t>(nt);
+    rep_at = A.take<uint64_t>(nt);
+    tiles2 = A.take<uint64_t>(nt / kScanTile + 2);
+    ctl_list = A.take<uint64_t>(kCtlCap);
+  }
+};
+
+// the kSetCompressionType / timestamp-size records' reports, in reader
+// order, from the state the reader keeps across the log
+// (log_reader.cc:167-213, UpdateRecordedTimestampSize)
+struct CtlHost {
+  std::vector<uint64_t> tok;
+  std::vector<uint32_t> cnt, reason;
+  std::vector<uint64_t> bytes;
+  bool unsupported = false;
+};
+
+void decide_controls(const std::vector<CtlInfo>& info, const std::vector<uint8_t>& payload,
+                     const std::vector<uint64_t>& at, CtlHost* h) {
+  bool comp_read = false;                      // compression_type_record_read_
+  std::unordered_map<uint32_t, uint32_t> ts;   // recorded_cf_to_ts_sz_
+  const size_t n = info.size();
+  h->tok.resize(n);
+  h->cnt.assign(n, 0);
+  h->reason.assign(n * kCtlRep, 0);
+  h->bytes.assign(n * kCtlRep, 0);
+  for (size_t j = 0; j < n; ++j) {
+    const CtlInfo& c = info[j];
+    const uint8_t* p = payload.data() + at[j];
+    h->tok[j] = c.tok;
+    auto rep = [&](uint32_t r, uint64_t b) {
+      h->reason[j * kCtlRep + h->cnt[j]] = r;
+      h->bytes[j * kCtlRep + h->cnt[j]] = b;
+      ++h->cnt[j];
+    };
+    if (c.kind == kTkCtlComp) {
+      if (comp_read) rep(kRpCompMultiple, c.len);
+      if (c.emitted_before) rep(kRpCompNotFirst, c.len);
+      // CompressionTypeRecord::DecodeFrom (util/compression.h:1716): GetFixed32
+      // consumes 4 bytes; CompressionType is an 8-bit enum (low byte)
+      if (c.len < 4) {
+        rep(kRpCompDecode, c.len);
+      } else if (p[0] == 0x7) {  // kZSTD: a compressed WAL, not replayed here
+        h->unsupported = true;
+      } else if (p[0] != 0) {
+        rep(kRpCompDecode, c.len - 4);
+      } else {
+        comp_read = true;  // InitCompression(kNoCompression): no decoder
+      }
+    } else {
+      // UserDefinedTimestampSizeRecord::DecodeFrom (util/udt_util.h:46)
+      if (c.len % 6) {
+        rep(kRpTsDecode, c.len);
+        continue;
+      }
+      for (uint32_t x = 0; x < c.len; x += 6) {
+        const uint32_t cf = static_cast<uint32_t>(p[x]) | (static_cast<uint32_t>(p[x + 1]) << 8) |
+                            (static_cast<uint32_t>(p[x + 2]) << 16) |
+                            (static_cast<uint32_t>(p[x + 3]) << 24);
+        const uint32_t sz = static_cast<uint32_t>(p[x + 4]) | (static_cast<uint32_t>(p[x + 5]) << 8);
+        if (sz == 0) {
+          rep(kRpTsZero, 0);
+          break;
+        }
+        if (ts.count(cf)) {
+          rep(kRpTsDuplicate, 0);
+          break;
+        }
+        ts.emplace(cf, sz);
+      }
+    }
+  }
+}
 
 }  // namespace
 
@@ -527,184 +859,221 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   const uint64_t nb = a.n_blocks;
   *name = "rw_walk";
   hipError_t e;
+  std::vector<void*> held;  // scratch allocations, freed stream-ordered on every exit
+  auto fail = [&](hipError_t x) {
+    for (auto it = held.rbegin(); it != held.rend(); ++it) (void)scratch_free(*it, st);
+    return x;
+  };
+  auto alloc = [&](size_t bytes, void** p) {
+    const hipError_t x = scratch_alloc(p, bytes, st);
+    if (x == hipSuccess) held.push_back(*p);
+    return x;
+  };
   // phase 1: per-block item counts -> item total (sync 1)
-  const size_t p1 = 4 * up256(8 * (nb + 1)) + up256(8 * (nb / kScanTile + 2)) + 4 * up256(4 * (nb + 1)) +
-                    up256(8) + 4096;
+  P1 q1;
+  Arena M1{nullptr, 0};
+  q1.take(M1, nb);
   void* s1 = nullptr;
-  if ((e = scratch_alloc(&s1, p1, st)) != hipSuccess) return e;
+  if ((e = alloc(M1.used, &s1)) != hipSuccess) return fail(e);
   Arena A1{static_cast<uint8_t*>(s1), 0};
-  uint64_t* cnt = A1.take<uint64_t>(nb + 1);
-  uint64_t* ibase = A1.take<uint64_t>(nb + 1);
-  uint64_t* acc = A1.take<uint64_t>(nb + 1);
-  uint64_t* rp_end = A1.take<uint64_t>(nb + 1);
-  uint64_t* tiles = A1.take<uint64_t>(nb / kScanTile + 2);
-  uint32_t* ev = A1.take<uint32_t>(nb + 1);
-  uint32_t* ev_pos = A1.take<uint32_t>(nb + 1);
-  uint32_t* recycled_d = A1.take<uint32_t>(1);
-  uint32_t* unsup_d = A1.take<uint32_t>(1);
-  unsigned long long* first_stop = A1.take<unsigned long long>(1);
+  q1.take(A1, nb);
   uint64_t n_items = 0;
-  uint32_t recycled = 0;
   if (nb) {
-    hipLaunchKernelGGL(rw_count_kernel, grid_for(nb), dim3(kLanes), 0, st, a, cnt);
-    scan_u64(cnt, nb, tiles, ibase, st);
+    hipLaunchKernelGGL(rw_count_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.cnt);
+    scan_u64(q1.cnt, nb, q1.tiles, q1.ibase, st);
   }
-  hipLaunchKernelGGL(rw_recycled_kernel, dim3(1), dim3(1), 0, st, a, recycled_d);
-  if ((e = hipMemsetAsync(first_stop, 0xff, 8, st)) != hipSuccess ||
-      (e = hipMemsetAsync(unsup_d, 0, 4, st)) != hipSuccess ||
-      (nb && (e = hipMemcpyAsync(&n_items, tiles + (nb + kScanTile - 1) / kScanTile, 8,
+  hipLaunchKernelGGL(rw_recycled_kernel, dim3(1), dim3(1), 0, st, a, q1.recycled);
+  if ((e = hipMemsetAsync(q1.first_stop, 0xff, 8, st)) != hipSuccess ||
+      (e = hipMemsetAsync(q1.ctl_n, 0, 8, st)) != hipSuccess ||
+      (nb && (e = hipMemcpyAsync(&n_items, q1.tiles + (nb + kScanTile - 1) / kScanTile, 8,
                                  hipMemcpyDeviceToHost, st)) != hipSuccess) ||
-      (e = hipMemcpyAsync(&recycled, recycled_d, 4, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-      (e = hipStreamSynchronize(st)) != hipSuccess) {
-    (void)scratch_free(s1, st);
-    return e;
-  }
-  // phase 2: items, CRCs, block truncation, tokens, state machine
+      (e = hipStreamSynchronize(st)) != hipSuccess)
+    return fail(e);
+  // phase 2: items, CRCs, block truncation, tokens, state machine; sized by
+  // the same sequence of takes that lays the arrays out
   const uint64_t ni = n_items, nt_max = n_items + nb + 1;
-  const size_t p2 = 3 * up256(8 * ni) + up256(ni) + 4 * up256(4 * ni) +  // items
-                    up256(nt_max) * 2 + up256(8 * nt_max) * 2 + up256(4 * nt_max) +  // tokens
-                    up256(8 * (nb + 2)) +                                          // token base
-                    up256(8 * nt_max) * 8 + up256(8 * (nt_max + 1)) * 2 +          // fsm
-                    up256(8 * (nt_max / kScanTile + 2)) + 8192;
+  P2 q;
+  Arena M2{nullptr, 0};
+  q.take(M2, ni, nb, nt_max);
   void* s2 = nullptr;
-  if ((e = scratch_alloc(&s2, p2, st)) != hipSuccess) {
-    (void)scratch_free(s1, st);
-    return e;
-  }
+  if ((e = alloc(M2.used, &s2)) != hipSuccess) return fail(e);
   Arena A{static_cast<uint8_t*>(s2), 0};
-  uint64_t* it_off = A.take<uint64_t>(ni);
-  uint8_t* it_old = A.take<uint8_t>(ni);
-  uint64_t* crc_off = A.take<uint64_t>(ni);
-  uint32_t* crc_len = A.take<uint32_t>(ni);
-  uint32_t* crc_stored = A.take<uint32_t>(ni);
-  uint32_t* ipack = A.take<uint32_t>(ni);
-  uint32_t* computed = A.take<uint32_t>(ni);
-  Tokens t{A.take<uint8_t>(nt_max), A.take<uint64_t>(nt_max), A.take<uint32_t>(nt_max),
-           A.take<uint64_t>(nt_max), A.take<uint8_t>(nt_max)};
-  uint64_t* ntok = A.take<uint64_t>(nb + 2);
-  uint64_t* tok_base = A.take<uint64_t>(nb + 2);
-  uint64_t* head = A.take<uint64_t>(nt_max);
-  uint64_t* plen = A.take<uint64_t>(nt_max);
-  uint64_t* pl = A.take<uint64_t>(nt_max);
-  uint64_t* seg = A.take<uint64_t>(nt_max);
-  uint64_t* seg_head = A.take<uint64_t>(nt_max + 1);
-  unsigned long long* seg_fl = A.take<unsigned long long>(nt_max + 1);
-  uint64_t* n_emit = A.take<uint64_t>(nt_max);
-  uint64_t* n_rep = A.take<uint64_t>(nt_max);
-  uint64_t* emit_at = A.take<uint64_t>(nt_max);
-  uint64_t* rep_at = A.take<uint64_t>(nt_max);
-  uint64_t* tiles2 = A.take<uint64_t>(nt_max / kScanTile + 2);
+  q.take(A, ni, nb, nt_max);
+  const Tokens& t = q.t;
   if (nb) {
-    hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, ibase, it_off, it_old,
-                       crc_off, crc_len, crc_stored, ipack, ev, ev_pos);
+    hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q.it_off,
+                       q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q1.ev, q1.ev_pos);
     if (ni) {
       BlockArgs cb{};
       cb.base = log;
       cb.base_len = log_len;
-      cb.offsets = crc_off;
-      cb.sizes = crc_len;
-      cb.out32 = computed;
+      cb.offsets = q.crc_off;
+      cb.sizes = q.crc_len;
+      cb.out32 = q.computed;
       cb.n = ni;
       const char* crc_name = nullptr;
-      if ((e = launch_crc32c_blocks(kModeRaw, cb, st, &crc_name)) != hipSuccess) {
-        (void)scratch_free(s2, st);
-        (void)scratch_free(s1, st);
-        return e;
-      }
+      if ((e = launch_crc32c_blocks(kModeRaw, cb, st, &crc_name)) != hipSuccess) return fail(e);
     }
-    hipLaunchKernelGGL(rw_block_kernel, grid_for(nb), dim3(kLanes), 0, st, a, cnt, ibase, it_off,
-                       it_old, crc_off, crc_len, crc_stored, computed, ev, ev_pos, acc, rp_end,
-                       first_stop, recycled);
+    hipLaunchKernelGGL(rw_block_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.cnt, q1.ibase,
+                       q.it_off, q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q.computed,
+                       q1.ev, q1.ev_pos, q1.acc, q1.rp_end, q1.first_stop, q1.recycled);
   }
-  hipLaunchKernelGGL(rw_ntok_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, acc, ev, first_stop,
-                     ntok);
-  scan_u64(ntok, nb + 1, tiles, tok_base, st);
+  hipLaunchKernelGGL(rw_ntok_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, q1.acc, q1.ev,
+                     q1.first_stop, q.ntok);
+  scan_u64(q.ntok, nb + 1, q1.tiles, q.tok_base, st);
   uint64_t n_tok = 0;
-  if ((e = hipMemcpyAsync(&n_tok, tiles + (nb + 1 + kScanTile - 1) / kScanTile, 8,
+  if ((e = hipMemcpyAsync(&n_tok, q1.tiles + (nb + 1 + kScanTile - 1) / kScanTile, 8,
                           hipMemcpyDeviceToHost, st)) != hipSuccess ||
-      (e = hipStreamSynchronize(st)) != hipSuccess) {
-    (void)scratch_free(s2, st);
-    (void)scratch_free(s1, st);
-    return e;
-  }
-  hipLaunchKernelGGL(rw_token_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, ibase, it_off,
-                     it_old, ipack, acc, ev, ev_pos, rp_end, tok_base, first_stop, recycled, t,
-                     unsup_d);
+      (e = hipStreamSynchronize(st)) != hipSuccess)
+    return fail(e);
+  hipLaunchKernelGGL(rw_token_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, q1.ibase, q.it_off,
+                     q.it_old, q.ipack, q1.acc, q1.ev, q1.ev_pos, q1.rp_end, q.tok_base,
+                     q1.first_stop, q1.recycled, t, q.ctl_list, kCtlCap, q1.ctl_n);
   const dim3 tg = grid_for(n_tok);
-  hipLaunchKernelGGL(rw_head_kernel, tg, dim3(kLanes), 0, st, t, n_tok, head, plen);
-  scan_u64(head, n_tok, tiles2, seg, st);
-  scan_u64(plen, n_tok, tiles2, pl, st);
-  (void)hipMemsetAsync(seg_fl, 0xff, 8 * (n_tok + 1), st);
-  hipLaunchKernelGGL(rw_seg_kernel, tg, dim3(kLanes), 0, st, t, n_tok, head, seg, seg_head, seg_fl);
-  const Fsm f{seg, seg_head, seg_fl, pl, plen};
+  hipLaunchKernelGGL(rw_head_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.plen);
+  scan_u64(q.head, n_tok, q.tiles2, q.seg, st);
+  scan_u64(q.plen, n_tok, q.tiles2, q.pl, st);
+  (void)hipMemsetAsync(q.seg_fl, 0xff, 8 * (n_tok + 1), st);
+  (void)hipMemsetAsync(q.live, 0, n_tok + 1, st);
+  hipLaunchKernelGGL(rw_seg_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg, q.seg_head,
+                     q.seg_fl);
+  hipLaunchKernelGGL(rw_live_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg, q.seg_head,
+                     q.seg_fl, q.live);
+  const Fsm f{q.seg, q.seg_head, q.seg_fl, q.live, q.pl, q.plen};
   forst_wal_records no_recs{};
   forst_wal_reports no_reps{};
-  hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, n_emit,
-                     n_rep, nullptr, nullptr, no_recs, 0, no_reps, 0, nullptr);
+  CtlReps cr{};
+  hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
+                     q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr);
   uint64_t tot[2] = {0, 0};
-  scan_u64(n_emit, n_tok, tiles2, emit_at, st);
-  e = hipMemcpyAsync(&tot[0], tiles2 + (n_tok + kScanTile - 1) / kScanTile, 8,
-                     hipMemcpyDeviceToHost, st);
-  scan_u64(n_rep, n_tok, tiles2, rep_at, st);  // (after the copy above, stream order)
-  if (e == hipSuccess)
-    e = hipMemcpyAsync(&tot[1], tiles2 + (n_tok + kScanTile - 1) / kScanTile, 8,
-                       hipMemcpyDeviceToHost, st);
+  unsigned long long n_ctl = 0;
+  const uint64_t ntl = (n_tok + kScanTile - 1) / kScanTile;
+  scan_u64(q.n_emit, n_tok, q.tiles2, q.emit_at, st);
+  e = hipMemcpyAsync(&tot[0], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
+  scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (after the copy above, stream order)
+  if (e == hipSuccess) e = hipMemcpyAsync(&tot[1], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
   // stop reason / offset: the last token
   uint8_t last_kind = 0;
   uint64_t last_pos = 0;
-  uint32_t unsupported = 0;
-  if (e == hipSuccess) e = hipMemcpyAsync(&unsupported, unsup_d, 4, hipMemcpyDeviceToHost, st);
+  if (e == hipSuccess) e = hipMemcpyAsync(&n_ctl, q1.ctl_n, 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && n_tok)
     e = hipMemcpyAsync(&last_kind, t.kind + n_tok - 1, 1, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess && n_tok)
     e = hipMemcpyAsync(&last_pos, t.pos + n_tok - 1, 8, hipMemcpyDeviceToHost, st);
   if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) {
-    (void)scratch_free(s2, st);
-    (void)scratch_free(s1, st);
-    return e;
-  }
-  if (unsupported) {
-    (void)scratch_free(s2, st);
-    (void)scratch_free(s1, st);
-    res->unsupported = 1;
-    return hipSuccess;
+  if (e != hipSuccess) return fail(e);
+  // control records (types 9-11): read back, decided in reader order on the
+  // host, their reports added before the report scan is taken again
+  CtlHost ch;
+  if (n_ctl) {
+    uint64_t* list = q.ctl_list;
+    if (n_ctl > kCtlCap) {  // more than the inline list holds: collect them again
+      void* big = nullptr;
+      if ((e = alloc(8 * n_ctl + 8, &big)) != hipSuccess) return fail(e);
+      list = static_cast<uint64_t*>(big);
+      if ((e = hipMemsetAsync(q1.ctl_n, 0, 8, st)) != hipSuccess) return fail(e);
+      hipLaunchKernelGGL(rw_token_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, q1.ibase,
+                         q.it_off, q.it_old, q.ipack, q1.acc, q1.ev, q1.ev_pos, q1.rp_end,
+                         q.tok_base, q1.first_stop, q1.recycled, t, list,
+                         static_cast<uint64_t>(n_ctl), q1.ctl_n);
+    }
+    void* cs = nullptr;
+    if ((e = alloc(up256(sizeof(CtlInfo) * n_ctl), &cs)) != hipSuccess) return fail(e);
+    CtlInfo* dinfo = static_cast<CtlInfo*>(cs);
+    hipLaunchKernelGGL(rw_ctl_info_kernel, grid_for(n_ctl), dim3(kLanes), 0, st, t, q.it_off,
+                       q.ipack, list, static_cast<uint64_t>(n_ctl), q.emit_at, dinfo);
+    std::vector<CtlInfo> info(n_ctl);
+    if ((e = hipMemcpyAsync(info.data(), dinfo, sizeof(CtlInfo) * n_ctl, hipMemcpyDeviceToHost,
+                            st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+      return fail(e);
+    std::sort(info.begin(), info.end(),
+              [](const CtlInfo& x, const CtlInfo& y) { return x.tok < y.tok; });
+    std::vector<uint64_t> at(n_ctl);
+    uint64_t tot_pl = 0;
+    for (uint64_t j = 0; j < n_ctl; ++j) {
+      at[j] = tot_pl;
+      tot_pl += info[j].len;
+    }
+    std::vector<uint8_t> payload(tot_pl + 1);
+    for (uint64_t j = 0; j < n_ctl; ++j)  // (few, short records)
+      if (info[j].len &&
+          (e = hipMemcpyAsync(payload.data() + at[j], log + info[j].payload, info[j].len,
+                              hipMemcpyDeviceToHost, st)) != hipSuccess)
+        return fail(e);
+    if ((e = hipStreamSynchronize(st)) != hipSuccess) return fail(e);
+    decide_controls(info, payload, at, &ch);
+    if (ch.unsupported) {
+      res->unsupported = 1;
+      return fail(hipSuccess);
+    }
+    // tok | cnt | reason | bytes, uploaded once
+    void* xs = nullptr;
+    const size_t sz_tok = up256(8 * n_ctl), sz_cnt = up256(4 * n_ctl),
+                 sz_rs = up256(4 * kCtlRep * n_ctl), sz_by = up256(8 * kCtlRep * n_ctl);
+    if ((e = alloc(sz_tok + sz_cnt + sz_rs + sz_by, &xs)) != hipSuccess) return fail(e);
+    uint8_t* xb = static_cast<uint8_t*>(xs);
+    cr.tok = reinterpret_cast<uint64_t*>(xb);
+    cr.cnt = reinterpret_cast<uint32_t*>(xb + sz_tok);
+    cr.reason = reinterpret_cast<uint32_t*>(xb + sz_tok + sz_cnt);
+    cr.bytes = reinterpret_cast<uint64_t*>(xb + sz_tok + sz_cnt + sz_rs);
+    cr.n = n_ctl;
+    if ((e = hipMemcpyAsync(const_cast<uint64_t*>(cr.tok), ch.tok.data(), 8 * n_ctl,
+                            hipMemcpyHostToDevice, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(const_cast<uint32_t*>(cr.cnt), ch.cnt.data(), 4 * n_ctl,
+                            hipMemcpyHostToDevice, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(const_cast<uint32_t*>(cr.reason), ch.reason.data(),
+                            4 * kCtlRep * n_ctl, hipMemcpyHostToDevice, st)) != hipSuccess ||
+        (e = hipMemcpyAsync(const_cast<uint64_t*>(cr.bytes), ch.bytes.data(),
+                            8 * kCtlRep * n_ctl, hipMemcpyHostToDevice, st)) != hipSuccess)
+      return fail(e);
+    hipLaunchKernelGGL(rw_ctl_add_kernel, grid_for(n_ctl), dim3(kLanes), 0, st, cr.tok, cr.cnt,
+                       static_cast<uint64_t>(n_ctl), q.n_rep);
+    scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);
+    if ((e = hipMemcpyAsync(&tot[1], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+      return fail(e);
   }
   const uint64_t n_rec = tot[0], n_rp = tot[1];
   res->n_records = n_rec;
   res->n_reports = n_rp;
   res->n_physical = ni;
-  res->stop_reason = last_kind == kTkStopEof         ? FORST_WAL_STOP_EOF
-                     : last_kind == kTkStopOld       ? FORST_WAL_STOP_OLD_RECORD
-                     : last_kind == kTkStopHeader    ? FORST_WAL_STOP_TRUNCATED_HEADER
-                     : last_kind == kTkStopBadLenEof ? FORST_WAL_STOP_TRUNCATED_BODY
-                                                     : FORST_WAL_STOP_RECYCLED_TAIL;
+  switch (last_kind) {
+    case kTkStopEof:
+    case kTkPEof: res->stop_reason = FORST_WAL_STOP_EOF; break;
+    case kTkStopOld:
+    case kTkPOld: res->stop_reason = FORST_WAL_STOP_OLD_RECORD; break;
+    case kTkStopHeader:
+    case kTkPHeader: res->stop_reason = FORST_WAL_STOP_TRUNCATED_HEADER; break;
+    case kTkStopBadLenEof:
+    case kTkPLenEof: res->stop_reason = FORST_WAL_STOP_TRUNCATED_BODY; break;
+    default: res->stop_reason = FORST_WAL_STOP_RECYCLED_TAIL; break;
+  }
   res->stop_offset = last_pos;
   res->truncated = (n_rec > rec_cap || n_rp > rep_cap) ? 1u : 0u;
   // records + reports at their positions, then the hashes
   const uint64_t nr = n_rec;
   // full record list in scratch first (the caller's capacity may be short)
   forst_wal_records full{};
-  uint64_t* head_tok = nullptr;
-  uint32_t* r_nf = nullptr;
+  uint64_t* hash_begin = nullptr;
+  uint64_t* last_tok = nullptr;
   void* s4 = nullptr;
-  if ((e = scratch_alloc(&s4, up256(8 * nr) * 4 + up256(4 * nr), st)) != hipSuccess) {
-    (void)scratch_free(s2, st);
-    (void)scratch_free(s1, st);
-    return e;
-  }
+  if ((e = alloc(up256(8 * nr) * 5 + up256(4 * nr), &s4)) != hipSuccess) return fail(e);
   {
     Arena A4{static_cast<uint8_t*>(s4), 0};
     full.offset = A4.take<uint64_t>(nr);
     full.length = A4.take<uint64_t>(nr);
     full.hash = A4.take<uint64_t>(nr);
-    full.n_fragments = r_nf = A4.take<uint32_t>(nr);
-    head_tok = A4.take<uint64_t>(nr);
+    full.n_fragments = A4.take<uint32_t>(nr);
+    hash_begin = A4.take<uint64_t>(nr);
+    last_tok = A4.take<uint64_t>(nr);
   }
-  hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, nullptr,
-                     nullptr, emit_at, rep_at, full, nr, reps, rep_cap, head_tok);
+  hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
+                     nullptr, q.emit_at, q.rep_at, cr, full, nr, reps, rep_cap, hash_begin,
+                     last_tok);
   if (nr) {
-    const RecFrags rf{head_tok, r_nf, t.item, it_off, ipack};
+    const RecFrags rf{hash_begin, last_tok, t.kind, t.item, q.it_off, q.ipack, q.seg, q.live,
+                      q.seg_fl};
     e = hash_logical_records(log, log_len, rf, nr, full.hash, st, name);
   }
   // copy the (capacity-limited) record list out
@@ -720,12 +1089,12 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   }
   if (e == hipSuccess) e = hipGetLastError();
   *name = "wal_recover";
-  const hipError_t f4 = scratch_free(s4, st), f2 = scratch_free(s2, st),
-                   f1 = scratch_free(s1, st);
-  if (e != hipSuccess) return e;
-  for (hipError_t x : {f4, f2, f1})
-    if (x != hipSuccess) return x;
-  return hipSuccess;
+  hipError_t fe = hipSuccess;
+  for (auto it = held.rbegin(); it != held.rend(); ++it) {
+    const hipError_t x = scratch_free(*it, st);
+    if (fe == hipSuccess) fe = x;
+  }
+  return e != hipSuccess ? e : fe;
 }
 
 }  // namespace forst

@@ -234,9 +234,18 @@ int forst_wal_record_xxh3_batch(const uint8_t* log, uint64_t log_len,
  * caller's (RecoverLogFiles') decision.  Output arrays are DEVICE arrays of
  * the given capacities (any member may be NULL); *result (host) has the
  * counts -- if a count exceeds its capacity, result->truncated is set and
- * only the first `capacity` entries are written.  WAL compression and
- * user-defined-timestamp-size records (types 9-11) are not handled:
- * FORST_EUNSUPPORTED.  Synchronises the stream (record counts). */
+ * only the first `capacity` entries are written.  Reader behaviour is the
+ * reference's to the letter, pinned to its compiled log::Reader
+ * (tests/golden/wal_reader.json.gz): type bytes >= 0x80 sign-extend
+ * (log_reader.cc:469); types 12..17 with a valid CRC act as the reader's own
+ * results kEof..kBadRecordChecksum (log_reader.h:173-186); the record
+ * checksum of a fragmented record covers every fragment fed to the XXH3 state
+ * since its last reset (:73-79, :119-124), aborted ones included;
+ * kSetCompressionType and user-defined-timestamp-size records (types 9-11,
+ * :167-213) are handled, except a kSetCompressionType record naming kZSTD
+ * (a compressed WAL): result->unsupported, FORST_EUNSUPPORTED.  Synchronises
+ * the stream (record counts; two more syncs when the log holds type 9-11
+ * records, whose reports depend on reader state kept across the log). */
 enum forst_wal_report_reason {
   FORST_WAL_PARTIAL_RECORD_1 = 1,   /* "partial record without end(1)" */
   FORST_WAL_PARTIAL_RECORD_2 = 2,   /* "partial record without end(2)" */
@@ -248,7 +257,18 @@ enum forst_wal_report_reason {
   FORST_WAL_TRUNCATED_HEADER = 8,   /* "truncated header" */
   FORST_WAL_TRAILING_DATA = 9,      /* "error reading trailing data" */
   FORST_WAL_TRUNCATED_BODY = 10,    /* "truncated record body" */
-  FORST_WAL_UNKNOWN_TYPE = 11       /* "unknown record type %u" */
+  FORST_WAL_UNKNOWN_TYPE = 11,      /* "unknown record type %u" (type as the
+                                       reader's unsigned int: 0xFF -> 4294967295) */
+  FORST_WAL_MULTIPLE_COMPRESSION = 12,  /* "read multiple SetCompressionType records" */
+  FORST_WAL_COMPRESSION_NOT_FIRST = 13, /* "SetCompressionType not the first record" */
+  FORST_WAL_COMPRESSION_DECODE = 14,    /* "could not decode SetCompressionType record" */
+  FORST_WAL_TS_INTERSPERSED = 15,   /* "user-defined timestamp size record interspersed
+                                       partial record" */
+  FORST_WAL_TS_DECODE = 16,         /* "could not decode user-defined timestamp size record" */
+  FORST_WAL_TS_ZERO = 17,           /* "User-defined timestamp size record contains zero
+                                       timestamp size." */
+  FORST_WAL_TS_DUPLICATE = 18       /* "User-defined timestamp size record contains update
+                                       to recorded column family." */
 };
 enum forst_wal_stop_reason {
   FORST_WAL_STOP_EOF = 0,              /* kEof */
@@ -275,7 +295,7 @@ typedef struct forst_wal_recover_result {
   uint64_t stop_offset;  /* reader position where reading ended */
   uint32_t stop_reason;  /* forst_wal_stop_reason */
   uint32_t truncated;    /* a count exceeded its capacity */
-  uint32_t unsupported;  /* types 9-11 present (the call returns FORST_EUNSUPPORTED) */
+  uint32_t unsupported;  /* a kSetCompressionType record names kZSTD (FORST_EUNSUPPORTED) */
   uint32_t reserved;
 } forst_wal_recover_result;
 int forst_wal_recover_batch(const uint8_t* log, uint64_t log_len, uint32_t log_number,

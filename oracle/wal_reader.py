@@ -2,23 +2,45 @@
 
 Serial CPU restatement of the reference WAL reader for the fused recovery
 pass (forst_wal_recover_batch): log::Reader::ReadRecord
-(db/log_reader.cc:69-320), ReadPhysicalRecord (:450-531) and ReadMore
-(:404-448), no WAL compression, with the XXH3 record checksum of every
-logical record (:95-165) and the reporter's Corruption(bytes, reason) calls in
-order.  Record types db/log_format.h:20-41; recovery modes
-include/rocksdb/options.h (WALRecoveryMode).  CRC32C and XXH3 come from the
-pinned C oracle (oracle/oracle.c).
+(db/log_reader.cc:69-320), ReadPhysicalRecord (:450-592), ReadMore
+(:404-448) and UpdateRecordedTimestampSize, with the XXH3 record checksum
+(:73-79, :95-165) and the reporter's Corruption(bytes, reason) calls in order.
+Record types db/log_format.h:20-43; recovery modes include/rocksdb/options.h
+(WALRecoveryMode).  CRC32C and XXH3 come from the pinned C oracle
+(oracle/oracle.c).
+
+Pinned against the reference reader itself: tests/golden/gen_wal_golden.py
+drives the reference's compiled log::Reader over the scenario logs of
+tests/walcases.py and commits its transcripts (tests/golden/wal_reader.json);
+tests/test_wal_golden.py checks this restatement against them.  Behaviours
+the pinning brought out, restated here as the reference has them:
+  * the record type is read from a `const char*` into `unsigned int`
+    (:466-469), so a type byte >= 0x80 sign-extends ("unknown record type
+    4294967295" for 0xFF);
+  * ReadPhysicalRecord's own results share the type space (log_reader.h:173-
+    186: kEof = kMaxRecordType + 1 = 12 ... kBadRecordChecksum = 17), so a
+    physical record of type 12..17 with a valid CRC acts as that result (with
+    drop_size 0 and the buffer NOT cleared);
+  * the XXH3 state of a fragmented record is only reset at the start of
+    ReadRecord and at "partial record without end(2)" (:73-79, :119-124), so
+    after an aborted fragmented record (error in middle, unknown type, ...)
+    the next fragmented record's checksum also covers the aborted fragments;
+  * kSetCompressionType / timestamp-size records clear scratch but keep
+    in_fragmented_record (:167-213).
+WAL compression (a kSetCompressionType record naming kZSTD) is not restated:
+it raises Unsupported, as forst_wal_recover_batch reports unsupported.
 """
 from . import oracle as O
 
 kBlockSize, kHeaderSize, kRecyclableHeaderSize = 32768, 7, 11  # log_format.h:45-52
 kZeroType, kFullType, kFirstType, kMiddleType, kLastType = 0, 1, 2, 3, 4
-kRecyclableFullType, kRecyclableLastType = 5, 8
+kRecyclableFullType, kRecyclableFirstType, kRecyclableMiddleType, kRecyclableLastType = 5, 6, 7, 8
 kSetCompressionType, kUserDefinedTimestampSizeType = 9, 10
 kRecyclableUserDefinedTimestampSizeType = 11
-# ReadPhysicalRecord's extra results (log_reader.h)
-kEof, kBadRecord, kBadHeader, kOldRecord, kBadRecordLen, kBadRecordChecksum = \
-    "eof", "bad_record", "bad_header", "old_record", "bad_record_len", "bad_record_checksum"
+kMaxRecordType = 11
+# ReadPhysicalRecord's extra results (log_reader.h:173-186)
+kEof, kBadRecord, kBadHeader, kOldRecord, kBadRecordLen, kBadRecordChecksum = range(12, 18)
+kZSTD = 7
 
 # WALRecoveryMode (include/rocksdb/options.h)
 kTolerateCorruptedTailRecords, kAbsoluteConsistency, kPointInTimeRecovery, \
@@ -27,6 +49,22 @@ kTolerateCorruptedTailRecords, kAbsoluteConsistency, kPointInTimeRecovery, \
 
 class Unsupported(Exception):
     pass
+
+
+class _Hash:
+    """XXH3_64bits streaming state as a byte accumulator (xxhash.h)"""
+
+    def __init__(self):
+        self.data = bytearray()
+
+    def reset(self):
+        self.data = bytearray()
+
+    def update(self, b):
+        self.data += b
+
+    def digest(self):
+        return O.xxh3_64(bytes(self.data))
 
 
 class Reader:
@@ -38,6 +76,11 @@ class Reader:
         self.eof = False
         self.end_of_buffer_offset = 0
         self.recycled = False
+        self.first_record_read = False
+        self.compression_type_record_read = False
+        self.recorded_ts = {}
+        self.hash = _Hash()
+        self.last_record_offset = 0
         self.reports = []  # (bytes, reason, reader position of the physical record)
         self.cur_phys = 0
 
@@ -63,7 +106,7 @@ class Reader:
         self.buf_lo = self.buf_hi
         return kEof, 0
 
-    def read_physical_record(self):  # log_reader.cc:450-531
+    def read_physical_record(self):  # log_reader.cc:450-592
         while True:
             if self._size() < kHeaderSize:
                 r, drop = self.read_more()
@@ -72,7 +115,7 @@ class Reader:
                 continue
             h = self.log[self.buf_lo:self.buf_lo + kRecyclableHeaderSize]
             length = h[4] | (h[5] << 8)
-            rtype = h[6]
+            rtype = h[6] if h[6] < 0x80 else h[6] | 0xFFFFFF00  # char -> unsigned int
             header_size = kHeaderSize
             recyc = (kRecyclableFullType <= rtype <= kRecyclableLastType) or \
                 rtype == kRecyclableUserDefinedTimestampSizeType
@@ -105,15 +148,14 @@ class Reader:
                 return kBadRecordChecksum, drop, None
             frag = self.log[self.buf_lo + header_size:self.buf_lo + header_size + length]
             self.buf_lo += header_size + length
-            if rtype in (kSetCompressionType, kUserDefinedTimestampSizeType,
-                         kRecyclableUserDefinedTimestampSizeType):
-                raise Unsupported("WAL compression / timestamp-size records")
             return rtype, 0, frag
 
     def read_record(self, mode):  # log_reader.cc:69-320
         scratch = b""
+        self.hash.reset()
         in_frag = False
         prospective = 0
+        strict = mode in (kAbsoluteConsistency, kPointInTimeRecovery)
         while True:
             phys = self.end_of_buffer_offset - self._size()
             self.cur_phys = phys
@@ -121,26 +163,80 @@ class Reader:
             if rt in (kFullType, kRecyclableFullType):
                 if in_frag and scratch:
                     self._report(len(scratch), "partial record without end(1)")
-                return phys, frag
-            if rt in (kFirstType, kFirstType + 4):
+                self.last_record_offset = phys
+                self.first_record_read = True
+                return phys, frag, O.xxh3_64(frag)
+            if rt in (kFirstType, kRecyclableFirstType):
                 if in_frag and scratch:
                     self._report(len(scratch), "partial record without end(2)")
+                    self.hash.reset()
+                self.hash.update(frag)
                 prospective = phys
                 scratch = frag
                 in_frag = True
                 continue
-            if rt in (kMiddleType, kMiddleType + 4):
+            if rt in (kMiddleType, kRecyclableMiddleType):
                 if not in_frag:
                     self._report(len(frag), "missing start of fragmented record(1)")
                 else:
+                    self.hash.update(frag)
                     scratch += frag
                 continue
-            if rt in (kLastType, kLastType + 4):
+            if rt in (kLastType, kRecyclableLastType):
                 if not in_frag:
                     self._report(len(frag), "missing start of fragmented record(2)")
                     continue
-                return prospective, scratch + frag
-            strict = mode in (kAbsoluteConsistency, kPointInTimeRecovery)
+                self.hash.update(frag)
+                self.last_record_offset = prospective
+                self.first_record_read = True
+                return prospective, scratch + frag, self.hash.digest()
+            if rt == kSetCompressionType:
+                if self.compression_type_record_read:
+                    self._report(len(frag), "read multiple SetCompressionType records")
+                if self.first_record_read:
+                    self._report(len(frag), "SetCompressionType not the first record")
+                prospective = phys
+                scratch = b""
+                self.last_record_offset = prospective
+                # CompressionTypeRecord::DecodeFrom (util/compression.h:1716):
+                # GetFixed32 consumes 4 bytes; CompressionType is an 8-bit enum
+                if len(frag) < 4:
+                    self._report(len(frag), "could not decode SetCompressionType record")
+                    continue
+                ct = frag[0]  # static_cast<CompressionType>(uint32) keeps the low byte
+                if ct == kZSTD:
+                    raise Unsupported("WAL compression (kZSTD)")
+                if ct != 0:
+                    self._report(len(frag) - 4, "could not decode SetCompressionType record")
+                    continue
+                self.compression_type_record_read = True  # InitCompression: no decoder
+                continue
+            if rt in (kUserDefinedTimestampSizeType, kRecyclableUserDefinedTimestampSizeType):
+                if in_frag and scratch:
+                    self._report(len(scratch), "user-defined timestamp size record "
+                                 "interspersed partial record")
+                prospective = phys
+                scratch = b""
+                self.last_record_offset = prospective
+                # UserDefinedTimestampSizeRecord::DecodeFrom (util/udt_util.h:46)
+                if len(frag) % 6:
+                    self._report(len(frag), "could not decode user-defined timestamp size record")
+                    continue
+                err = None
+                for k in range(0, len(frag), 6):  # UpdateRecordedTimestampSize
+                    cf = int.from_bytes(frag[k:k + 4], "little")
+                    ts = int.from_bytes(frag[k + 4:k + 6], "little")
+                    if ts == 0:
+                        err = "User-defined timestamp size record contains zero timestamp size."
+                        break
+                    if cf in self.recorded_ts:
+                        err = ("User-defined timestamp size record contains update to "
+                               "recorded column family.")
+                        break
+                    self.recorded_ts[cf] = ts
+                if err:
+                    self._report(0, err)
+                continue
             if rt == kBadHeader:
                 if strict:
                     self._report(drop, "truncated header")
@@ -182,7 +278,7 @@ class Reader:
 
 def read_all(log, log_number=0, mode=kPointInTimeRecovery):
     """Every logical record ReadRecord returns, in order: (record offset =
-    Reader::LastRecordOffset, length, XXH3_64bits), and the reporter's
+    Reader::LastRecordOffset, length, record checksum), and the reporter's
     (bytes, reason, reader position) calls."""
     r = Reader(log, log_number)
     recs = []
@@ -190,6 +286,6 @@ def read_all(log, log_number=0, mode=kPointInTimeRecovery):
         got = r.read_record(mode)
         if got is None:
             break
-        off, payload = got
-        recs.append((off, len(payload), O.xxh3_64(payload)))
+        off, payload, h = got
+        recs.append((off, len(payload), h))
     return recs, r.reports

@@ -9,92 +9,16 @@ recycled logs with old records.
 The CPU tests run the unmodified device code on the SIMT emulator
 (tests/emu); the -m gpu tests run it on the MI355X, including a C5-shaped log
 of 200 000 records with scattered corruption."""
-import struct
-
 import numpy as np
 import pytest
 
-from oracle import oracle as O
+import walcases as W
 from oracle import wal_reader as R
+from test_wal_golden import reason_text
 
 MODES = [R.kTolerateCorruptedTailRecords, R.kAbsoluteConsistency, R.kPointInTimeRecovery,
          R.kSkipAnyCorruptedRecords]
-REASONS = {1: "partial record without end(1)", 2: "partial record without end(2)",
-           3: "missing start of fragmented record(1)",
-           4: "missing start of fragmented record(2)", 5: "error in middle of record",
-           6: "checksum mismatch", 7: "bad record length", 8: "truncated header",
-           9: "error reading trailing data", 10: "truncated record body"}
-
-
-def reason_text(code, rtype):
-    return "unknown record type %u" % rtype if code == 11 else REASONS[code]
-
-
-def frame(n, seed, recyclable=False, log_number=7, hi=70000):
-    rng = np.random.default_rng(seed)
-    lens = (np.exp(rng.uniform(0, np.log(hi), n))).astype(np.uint32)
-    lens[:4] = [0, 32761, 5, 32750]
-    pay = rng.integers(0, 256, int(lens.astype(np.int64).sum()), np.uint8)
-    buf, po, pl = O.wal_frame(pay, lens, recyclable=recyclable, log_number=log_number)
-    return buf.copy(), po, pl
-
-
-def hdr_size(buf, off):
-    t = buf[off + 6]
-    return 11 if (5 <= t <= 8 or t == 11) else 7
-
-
-def set_type(buf, off, t, log_number):
-    """re-type a physical record and rewrite its CRC (log_writer.cc:240-263)"""
-    buf[off + 6] = t
-    hs = hdr_size(buf, off)
-    n = int(buf[off + 4]) | (int(buf[off + 5]) << 8)
-    c = O.mask(O.crc32c_value(bytes(buf[off + 6:off + hs + n])))
-    buf[off:off + 4] = np.frombuffer(struct.pack("<I", c), np.uint8)
-
-
-def scenarios(recyclable, seed):
-    """(name, log bytes, log_number) cases with every reader outcome"""
-    ln = 7
-    buf, po, pl = frame(600, seed, recyclable, ln)
-    rng = np.random.default_rng(seed + 1)
-    types = buf[po.astype(np.int64) + 6]
-    out = [("clean", buf, ln)]
-    b = buf.copy()  # CRC mismatches (payload flips) in a few blocks
-    for k in rng.choice(len(po), 6, replace=False):
-        if pl[k]:
-            b[int(po[k]) + hdr_size(b, int(po[k])) + int(rng.integers(0, pl[k]))] ^= 0x10
-    out.append(("crc", b, ln))
-    b = buf.copy()  # re-typed fragments: missing starts, partial records, unknown types
-    base = 4 if recyclable else 0
-    for k in rng.choice(len(po), 12, replace=False):
-        t = int(types[k]) - base
-        new = {1: 4, 2: 3, 3: 1, 4: 2}[t] if t in (1, 2, 3, 4) else 1
-        if k % 5 == 0:
-            new = 12 - base  # unknown type (12 here; 12-4 = 8 would be a valid one)
-        set_type(b, int(po[k]), new + base if new < 9 else 12, ln)
-    out.append(("retype", b, ln))
-    b = buf.copy()  # a zero-filled region (kZeroType + length 0: preallocated space)
-    z = int(po[len(po) // 3])
-    b[z:z + 300] = 0
-    out.append(("zero", b, ln))
-    for cut in (3, 9, 5000):  # truncated tail: header / recyclable header / body
-        e = int(po[-1]) + min(cut, int(pl[-1]) + 6)
-        out.append((f"trunc{cut}", buf[:e].copy(), ln))
-    b = buf.copy()  # bad length in a middle block
-    k = len(po) // 2
-    b[int(po[k]) + 4:int(po[k]) + 6] = 0xFF
-    out.append(("badlen", b, ln))
-    if recyclable:
-        b = buf.copy()  # a record of an older log incarnation
-        o = int(po[len(po) // 2])
-        b[o + 7:o + 11] = np.frombuffer(struct.pack("<I", ln + 1), np.uint8)
-        set_type(b, o, int(b[o + 6]), ln)
-        out.append(("old", b, ln))
-        b2 = b.copy()  # ... and a corrupt tail of a recycled log
-        b2[int(po[-3]) + 12] ^= 1
-        out.append(("old+crc", b2, ln))
-    return out
+scenarios = W.scenarios
 
 
 def compare(got_recs, got_reps, res, log, log_number, mode, name):
@@ -104,7 +28,8 @@ def compare(got_recs, got_reps, res, log, log_number, mode, name):
     assert [(int(a), int(b), int(c) & (2**64 - 1)) for a, b, c in zip(go, gl, gh)] == \
         [(o, n, h) for o, n, h in want_recs], (name, mode)
     po, pb, pr, pt = (np.asarray(x) for x in got_reps)
-    got = [(int(b), reason_text(int(r), int(t)), int(o)) for o, b, r, t in zip(po, pb, pr, pt)]
+    got = [(int(b), reason_text(int(r), int(t) & 0xFFFFFFFF), int(o))
+           for o, b, r, t in zip(po, pb, pr, pt)]
     assert got == [(b, r, p) for b, r, p in want_reps], (name, mode, got[:5], want_reps[:5])
 
 

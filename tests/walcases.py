@@ -11,6 +11,8 @@ the boundary at every byte of a 16-byte lane slot and of a 64-byte stripe, at
 bytes, records of 241..300 bytes across a boundary, an empty first fragment
 (leftover exactly hs), three- and four-fragment records, and short records
 (<= 240 bytes) across a boundary (gathered)."""
+import struct
+
 import numpy as np
 
 from oracle import oracle as O
@@ -105,3 +107,227 @@ def expected_hashes(payload, lens):
     starts = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
     return np.array([O.xxh3_64(payload[starts[j]:starts[j + 1]].tobytes())
                      for j in range(len(lens))], np.uint64)
+
+
+# ---- recovery scenarios (forst_wal_recover_batch; pinned to the reference's
+# own log::Reader by tests/golden/gen_wal_golden.py) --------------------------
+
+def frame(n, seed, recyclable=False, log_number=7, hi=70000):
+    rng = np.random.default_rng(seed)
+    lens = (np.exp(rng.uniform(0, np.log(hi), n))).astype(np.uint32)
+    lens[:4] = [0, 32761, 5, 32750]
+    pay = rng.integers(0, 256, int(lens.astype(np.int64).sum()), np.uint8)
+    buf, po, pl = O.wal_frame(pay, lens, recyclable=recyclable, log_number=log_number)
+    return buf.copy(), po, pl
+
+
+def hdr_size(buf, off):
+    t = buf[off + 6]
+    return 11 if (5 <= t <= 8 or t == 11) else 7
+
+
+def set_type(buf, off, t, log_number=None):
+    """re-type a physical record and rewrite its CRC (log_writer.cc:240-263)"""
+    buf[off + 6] = t
+    hs = hdr_size(buf, off)
+    n = int(buf[off + 4]) | (int(buf[off + 5]) << 8)
+    c = O.mask(O.crc32c_value(bytes(buf[off + 6:off + hs + n])))
+    buf[off:off + 4] = np.frombuffer(struct.pack("<I", c), np.uint8)
+
+
+def set_payload(buf, off, data):
+    """overwrite a physical record's leading payload bytes and re-CRC it"""
+    hs = hdr_size(buf, off)
+    buf[off + hs:off + hs + len(data)] = np.frombuffer(bytes(data), np.uint8)
+    set_type(buf, off, int(buf[off + 6]))
+
+
+def scenarios(recyclable, seed, n=600):
+    """(name, log bytes, log_number) cases with every reader outcome"""
+    ln = 7
+    buf, po, pl = frame(n, seed, recyclable, ln)
+    rng = np.random.default_rng(seed + 1)
+    types = buf[po.astype(np.int64) + 6]
+    out = [("clean", buf, ln)]
+    b = buf.copy()  # CRC mismatches (payload flips) in a few blocks
+    for k in rng.choice(len(po), 6, replace=False):
+        if pl[k]:
+            b[int(po[k]) + hdr_size(b, int(po[k])) + int(rng.integers(0, pl[k]))] ^= 0x10
+    out.append(("crc", b, ln))
+    b = buf.copy()  # re-typed fragments: missing starts, partial records, unknown types
+    base = 4 if recyclable else 0
+    for k in rng.choice(len(po), 12, replace=False):
+        t = int(types[k]) - base
+        new = {1: 4, 2: 3, 3: 1, 4: 2}[t] if t in (1, 2, 3, 4) else 1
+        if k % 5 == 0:
+            new = 12 - base  # 12 = the reader's kEof (log_reader.h:173): reading ends
+        set_type(b, int(po[k]), new + base if new < 9 else 12, ln)
+    out.append(("retype", b, ln))
+    b = buf.copy()  # a zero-filled region (kZeroType + length 0: preallocated space)
+    z = int(po[len(po) // 3])
+    b[z:z + 300] = 0
+    out.append(("zero", b, ln))
+    for cut in (3, 9, 5000):  # truncated tail: header / recyclable header / body
+        e = int(po[-1]) + min(cut, int(pl[-1]) + 6)
+        out.append((f"trunc{cut}", buf[:e].copy(), ln))
+    b = buf.copy()  # bad length in a middle block
+    k = len(po) // 2
+    b[int(po[k]) + 4:int(po[k]) + 6] = 0xFF
+    out.append(("badlen", b, ln))
+    if recyclable:
+        b = buf.copy()  # a record of an older log incarnation
+        o = int(po[len(po) // 2])
+        b[o + 7:o + 11] = np.frombuffer(struct.pack("<I", ln + 1), np.uint8)
+        set_type(b, o, int(b[o + 6]), ln)
+        out.append(("old", b, ln))
+        b2 = b.copy()  # ... and a corrupt tail of a recycled log
+        b2[int(po[-3]) + 12] ^= 1
+        out.append(("old+crc", b2, ln))
+    return out
+
+
+def pseudo_type_scenarios(recyclable, seed, n=300):
+    """records re-typed (valid CRC) into the reader's own result codes
+    12..17 (log_reader.h:173-186), unknown types 18 / 0x7F, and type bytes
+    >= 0x80 (sign-extended, log_reader.cc:469), one kind per log, plus a mix
+    in which re-typed fragments sit inside fragmented records"""
+    ln = 7
+    buf, po, pl = frame(n, seed, recyclable, ln)
+    rng = np.random.default_rng(seed + 2)
+    out = []
+    for t in (12, 13, 14, 15, 16, 17, 18, 0x7F, 0x80, 0xFF):
+        b = buf.copy()
+        for k in sorted(rng.choice(np.arange(8, len(po)), 3, replace=False)):
+            set_type(b, int(po[k]), t, ln)
+        out.append((f"type{t}", b, ln))
+    # a pseudo type in the last (short) log block: kBadRecordLen at eof_
+    b = buf.copy()
+    set_type(b, int(po[-2]), 16, ln)
+    out.append(("type16eof", b, ln))
+    b = buf.copy()
+    for k, t in zip(sorted(rng.choice(np.arange(8, len(po)), 6, replace=False)),
+                    (13, 16, 17, 0x80, 0xFF, 13)):
+        set_type(b, int(po[k]), t, ln)
+    out.append(("mixed", b, ln))
+    # partial records: a First whose Last is re-typed Full (partial ...(1)) or
+    # First (partial ...(2) at the following First)
+    base = 4 if recyclable else 0
+    types = buf[po.astype(np.int64) + 6].astype(int) - base
+    two = [k for k in range(len(po) - 1) if types[k] == 2 and types[k + 1] == 4 and pl[k]]
+    b = buf.copy()
+    for i, k in enumerate(two[1:7]):
+        set_type(b, int(po[k + 1]), (1 if i % 2 else 2) + base, ln)
+    out.append(("partials", b, ln))
+    return out
+
+
+def frame_lens(lens, seed, recyclable=False, log_number=7):
+    rng = np.random.default_rng(seed)
+    lens = np.asarray(lens, np.uint32)
+    pay = rng.integers(0, 256, int(lens.astype(np.int64).sum()), np.uint8)
+    buf, po, pl = O.wal_frame(pay, lens, recyclable=recyclable, log_number=log_number)
+    return buf.copy(), po, pl
+
+
+def make_control(buf, off, rtype, payload):
+    """rewrite the Full physical record at `off` as a control record the way
+    log::Writer emits one (log_writer.cc:228-263: kSetCompressionType always
+    with the 7-byte header, the recyclable timestamp-size type with the
+    11-byte one); the record must span exactly header + len(payload)"""
+    old_hs = hdr_size(buf, off)
+    old_n = int(buf[off + 4]) | (int(buf[off + 5]) << 8)
+    hs = 11 if rtype == 11 else 7
+    assert old_hs + old_n == hs + len(payload), (old_hs, old_n, hs, len(payload))
+    buf[off + 4:off + 6] = np.frombuffer(struct.pack("<H", len(payload)), np.uint8)
+    buf[off + hs:off + hs + len(payload)] = np.frombuffer(bytes(payload), np.uint8)
+    set_type(buf, off, rtype)
+
+
+def control_scenarios(recyclable, seed, n=300):
+    """kSetCompressionType and user-defined-timestamp-size records
+    (log_format.h:37-41) written where a writer puts them and where it never
+    does: first in the log, repeated, mid-log, between the fragments of a
+    record, with undecodable payloads, zero timestamp sizes and repeated
+    column families (log_reader.cc:167-213, UpdateRecordedTimestampSize)"""
+    ln = 7
+    rng = np.random.default_rng(seed)
+    lens = (np.exp(rng.uniform(0, np.log(70000), n))).astype(np.uint32)
+    ts_type = 11 if recyclable else 10
+
+    def ts(pairs):
+        return b"".join(struct.pack("<IH", cf, t) for cf, t in pairs)
+
+    plan = {
+        "ctl_ok": [(0, 9, struct.pack("<I", 0)), (3, ts_type, ts([(1, 8), (2, 16)])),
+                   (9, ts_type, ts([(3, 8)])), (40, ts_type, ts([(4, 8), (5, 8), (6, 24)]))],
+        "ctl_comp": [(0, 9, struct.pack("<I", 0)), (2, 9, struct.pack("<I", 0)),
+                     (5, 9, struct.pack("<I", 0x100)), (8, 9, struct.pack("<I", 3)),
+                     (11, 9, struct.pack("<I", 0x205))],
+        "ctl_ts": [(1, ts_type, ts([(1, 8)])), (4, ts_type, ts([(2, 0)])),
+                   (7, ts_type, ts([(3, 4), (1, 8)])), (10, ts_type, b"\x01" * 7),
+                   (13, ts_type, b""), (16, ts_type, ts([(9, 2), (10, 0), (11, 4)]))],
+    }
+    out = []
+    for name, items in plan.items():
+        L = lens.copy()
+        for k, t, p in items:  # a Full record of the control record's span
+            L[k] = len(p) - 4 if (t == 9 and recyclable) else len(p)
+        buf, po, pl = frame_lens(L, seed + 1, recyclable, ln)
+        first_phys = {}
+        j = 0
+        types = buf[po.astype(np.int64) + 6]
+        for q in range(len(po)):  # logical record -> its first physical record
+            t = int(types[q]) - (4 if recyclable else 0)
+            if t in (1, 2):
+                first_phys[j] = q
+                j += 1
+        for k, t, p in items:
+            q = first_phys[k]
+            if int(types[q]) - (4 if recyclable else 0) != 1:
+                continue  # (straddles a block: not a single Full record)
+            make_control(buf, int(po[q]), t, p)
+        out.append((name, buf, ln))
+    # control records in place of Middle / Last fragments (a writer never
+    # does this; the reader keeps in_fragmented_record across them)
+    buf, po, pl = frame(n, seed + 2, recyclable, ln)
+    base = 4 if recyclable else 0
+    types = buf[po.astype(np.int64) + 6].astype(int) - base
+    mids = [k for k in range(len(po)) if types[k] in (3, 4) and pl[k] >= 12]
+    b = buf.copy()
+    for i, k in enumerate(sorted(np.random.default_rng(seed + 3).choice(mids, 8, replace=False))):
+        o = int(po[k])
+        n_ = int(pl[k])
+        if i % 2:  # a timestamp-size record of the fragment's own length (ragged or not)
+            b[o + 6] = ts_type if recyclable else 10
+            if n_ % 6 == 0:
+                b[o + hdr_size(b, o):o + hdr_size(b, o) + n_] = np.frombuffer(
+                    ts([(200 + i * 1000 + x, 8) for x in range(n_ // 6)]), np.uint8)
+            set_type(b, o, int(b[o + 6]))
+        else:  # a compression record (7-byte header) over the fragment's span
+            hs = hdr_size(b, o)
+            pay = struct.pack("<I", 0) + bytes(n_ + hs - 7 - 4)
+            b[o + 4:o + 6] = np.frombuffer(struct.pack("<H", len(pay)), np.uint8)
+            b[o + 7:o + 7 + len(pay)] = np.frombuffer(pay, np.uint8)
+            set_type(b, o, 9)
+    out.append(("ctl_frag", b, ln))
+    return out
+
+
+def zero_tail_log(recyclable, total=64 << 20, n=40, seed=31):
+    """a few records followed by a zero-filled (preallocated) tail"""
+    buf, po, pl = frame(n, seed, recyclable, 7, hi=20000)
+    out = np.zeros(total, np.uint8)
+    out[:len(buf)] = buf
+    return out
+
+
+def old_tail_log(total_blocks=600, seed=33):
+    """a recycled log: this incarnation's records followed by an older
+    incarnation's (other log number) in the remaining blocks"""
+    new, _, _ = frame(200, seed, True, 8, hi=20000)
+    old, _, _ = frame(3000, seed + 1, True, 5, hi=20000)
+    n = total_blocks * 32768
+    out = old[:n].copy() if len(old) >= n else np.concatenate([old, np.zeros(n - len(old), np.uint8)])
+    cut = (len(new) // 32768) * 32768 + 32768
+    out[:len(new)] = new
+    return out[:max(n, cut)]

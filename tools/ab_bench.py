@@ -16,13 +16,14 @@ ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
 
 # kernel variants live only in the diagnostics build (make -C forst_amd/csrc diag)
-os.environ.setdefault("FORST_LIB_PATH", os.path.join(ROOT, "forst_amd", "lib",
-                                                     "libforst_checksum_diag.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
-from forst_amd import engine, workload  # noqa: E402
+from forst_amd import _lib, engine, workload  # noqa: E402
+
+_lib.use_library(os.environ.get("FORST_AB_LIB") or
+                 os.path.join(ROOT, "forst_amd", "lib", "libforst_checksum_diag.so"))
 
 CONFIGS = {
     "C2": (1 << 20, 4096, 1), "NS16": (1 << 20, 16384, 1), "NS16X": (1 << 20, 16384, 4),

@@ -10,13 +10,13 @@ variants = sys.argv[1:] or ["FORST_WAL_VARIANT=", "FORST_WAL_VARIANT=wave"]
 for v in variants:
     env = dict(os.environ)
     # variants exist only in the diagnostics build (make -C forst_amd/csrc diag)
-    env.setdefault("FORST_LIB_PATH", os.path.join(ROOT, "forst_amd", "lib",
-                                                  "libforst_checksum_diag.so"))
     k, _, val = v.partition("=")
     env[k] = val
     code = ("import sys, json; sys.path.insert(0, %r); import bench; "
-            "from forst_amd import engine; engine.init_device(); "
-            "print(json.dumps(bench.run_wal(5, 1)))" % ROOT)
+            "from forst_amd import _lib, engine; "
+            "_lib.use_library(%r); engine.init_device(); "
+            "print(json.dumps(bench.run_wal(5, 1)))" % (ROOT, os.path.join(
+                ROOT, "forst_amd", "lib", "libforst_checksum_diag.so")))
     out = subprocess.run([sys.executable, "-c", code], env=env, capture_output=True, text=True,
                          timeout=300)
     line = out.stdout.strip().splitlines()[-1] if out.returncode == 0 else out.stderr[-2000:]

@@ -16,13 +16,14 @@ import sys
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 sys.path.insert(0, ROOT)
-os.environ.setdefault("FORST_LIB_PATH", os.path.join(ROOT, "forst_amd", "lib",
-                                                     "libforst_checksum_diag.so"))
 
 import numpy as np  # noqa: E402
 import torch  # noqa: E402
 
 from forst_amd import _lib, engine, workload  # noqa: E402
+
+_lib.use_library(os.environ.get("FORST_AB_LIB") or
+                 os.path.join(ROOT, "forst_amd", "lib", "libforst_checksum_diag.so"))
 from tools.ab_bench import CONFIGS  # noqa: E402
 
 

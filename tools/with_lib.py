@@ -1,0 +1,14 @@
+#!/usr/bin/env python3
+"""tools/with_lib.py <library.so> <script.py> [args...] -- run a script with
+another build of the C ABI loaded (A/B of two builds, tools/ab_libs.sh)."""
+import os
+import runpy
+import sys
+
+ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
+sys.path.insert(0, ROOT)
+from forst_amd import _lib  # noqa: E402
+
+_lib.use_library(sys.argv[1])
+sys.argv = sys.argv[2:]
+runpy.run_path(sys.argv[0], run_name="__main__")

@@ -1,4 +1,4 @@
-// forst_amd/csrc/forstdb_shim.cc -- C++ host shim (namespace forstdb) over the
+// forst_amd/csrc/engine_shim.cc -- C++ host shim (namespace forst_gpu) over the
 // C ABI; see include/forst/checksum_engine.h for the reference mapping.
 #include "../../include/forst/checksum_engine.h"
 
@@ -8,7 +8,7 @@
 #include <string>
 #include <vector>
 
-namespace forstdb {
+namespace forst_gpu {
 
 std::string Status::ToString() const {
   switch (code_) {
@@ -173,4 +173,4 @@ Status BlockChecksumEngine::VerifyBlocks(ChecksumType type, uint32_t base_contex
   return first;
 }
 
-}  // namespace forstdb
+}  // namespace forst_gpu

@@ -288,7 +288,7 @@ static int footer_decode(const uint8_t* tail, uint64_t tail_len, uint64_t file_s
       return corrupt("Bad extended magic number: 0x" + hex(in, 4));
     f->stored_footer_checksum = fixed32(in + 4);
     f->base_context_checksum = fixed32(in + 8);
-    if (forstdb::ChecksumModifierForContext(f->base_context_checksum, 0) == 0)
+    if (forst_gpu::ChecksumModifierForContext(f->base_context_checksum, 0) == 0)
       return corrupt("Invalid base context checksum");
     const uint32_t metaindex_size = fixed32(in + 12);
     const uint64_t metaindex_end = f->footer_offset - kBlockTrailer;
@@ -298,7 +298,7 @@ static int footer_decode(const uint8_t* tail, uint64_t tail_len, uint64_t file_s
     // format.cc:440-448: checked after the footer checksum (by the caller)
     f->future_feature = fixed64(in + 32) != 0 ? 1u : 0u;
     f->footer_checksum_modifier =
-        forstdb::ChecksumModifierForContext(f->base_context_checksum, f->footer_offset);
+        forst_gpu::ChecksumModifierForContext(f->base_context_checksum, f->footer_offset);
   } else {
     const uint8_t* p = in;
     const uint8_t* lim = in + 2 * kHandleMax;
@@ -340,7 +340,7 @@ __attribute__((visibility("default"))) int forst_sst_properties_decode(const uin
 // ---------------------------------------------------------------------------
 // BlockBasedTable::VerifyChecksum over a file staged in device memory
 // ---------------------------------------------------------------------------
-namespace forstdb {
+namespace forst_gpu {
 namespace {
 
 // Footer errors carry Status::CopyAppendMessage(s, " in ", file) of
@@ -698,11 +698,11 @@ std::vector<Status> VerifySstFilesChecksums(BlockChecksumEngine& eng,
   return out;
 }
 
-}  // namespace forstdb
+}  // namespace forst_gpu
 
 namespace {
-void fill_result(forst_sst_verify_result* out, const forstdb::Status& s,
-                 const forstdb::SstVerifyReport& rep) {
+void fill_result(forst_sst_verify_result* out, const forst_gpu::Status& s,
+                 const forst_gpu::SstVerifyReport& rep) {
   std::memset(out, 0, sizeof(*out));
   out->status = s.code();
   out->blocks_verified = rep.blocks_verified;
@@ -723,7 +723,7 @@ extern "C" __attribute__((visibility("default"))) int forst_sst_verify_files(
     forst_sst_verify_result* out, void* stream) {
   if (n_files == 0) return FORST_OK;
   if (!host_files || !file_sizes || !dev_offsets || !dev_arena || !out) return FORST_EINVAL;
-  std::vector<forstdb::SstFileRef> files(n_files);
+  std::vector<forst_gpu::SstFileRef> files(n_files);
   for (uint64_t i = 0; i < n_files; ++i) {
     if (!host_files[i]) return FORST_EINVAL;
     files[i].host_file = host_files[i];
@@ -731,10 +731,10 @@ extern "C" __attribute__((visibility("default"))) int forst_sst_verify_files(
     files[i].dev_offset = dev_offsets[i];
     files[i].file_name = (file_names && file_names[i]) ? file_names[i] : "";
   }
-  forstdb::BlockChecksumEngine eng(stream);
-  std::vector<forstdb::SstVerifyReport> reps;
-  std::vector<forstdb::Status> st =
-      forstdb::VerifySstFilesChecksums(eng, files, dev_arena, arena_len, &reps);
+  forst_gpu::BlockChecksumEngine eng(stream);
+  std::vector<forst_gpu::SstVerifyReport> reps;
+  std::vector<forst_gpu::Status> st =
+      forst_gpu::VerifySstFilesChecksums(eng, files, dev_arena, arena_len, &reps);
   for (uint64_t i = 0; i < n_files; ++i) fill_result(&out[i], st[i], reps[i]);
   return FORST_OK;
 }
@@ -743,9 +743,9 @@ extern "C" __attribute__((visibility("default"))) int forst_sst_verify_file(
     const uint8_t* host_file, uint64_t file_size, const uint8_t* dev_file, const char* file_name,
     forst_sst_verify_result* out, void* stream) {
   if (!host_file || !dev_file || !out) return FORST_EINVAL;
-  forstdb::BlockChecksumEngine eng(stream);
-  forstdb::SstVerifyReport rep;
-  forstdb::Status s = forstdb::VerifySstFileChecksums(eng, host_file, file_size, dev_file,
+  forst_gpu::BlockChecksumEngine eng(stream);
+  forst_gpu::SstVerifyReport rep;
+  forst_gpu::Status s = forst_gpu::VerifySstFileChecksums(eng, host_file, file_size, dev_file,
                                                       file_name ? file_name : "", &rep);
   fill_result(out, s, rep);
   return FORST_OK;

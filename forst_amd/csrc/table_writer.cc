@@ -30,7 +30,7 @@
 #include "../../include/forst/checksum_engine.h"
 #include "../../include/forst_checksum.h"
 
-namespace forstdb {
+namespace forst_gpu {
 
 namespace {
 constexpr uint32_t kTrailer = 5;                                     // block_based_table_reader.h:75
@@ -250,7 +250,7 @@ Status GpuTrailerWriter::WriteFooter(uint32_t format_version, uint64_t metaindex
   return s;
 }
 
-}  // namespace forstdb
+}  // namespace forst_gpu
 
 // ---------------------------------------------------------------------------
 // C ABI
@@ -259,17 +259,17 @@ Status GpuTrailerWriter::WriteFooter(uint32_t format_version, uint64_t metaindex
 
 namespace {
 thread_local std::string g_tw_err;
-int tw_fail(const forstdb::Status& s) {
+int tw_fail(const forst_gpu::Status& s) {
   g_tw_err = s.ToString();
   return s.IsCorruption() ? FORST_ECORRUPT
-         : s.code() == forstdb::Status::kInvalidArgument ? FORST_EINVAL
-         : s.code() == forstdb::Status::kNotSupported    ? FORST_EUNSUPPORTED
+         : s.code() == forst_gpu::Status::kInvalidArgument ? FORST_EINVAL
+         : s.code() == forst_gpu::Status::kNotSupported    ? FORST_EUNSUPPORTED
                                                          : FORST_EHIP;
 }
 }  // namespace
 
 struct forst_trailer_writer {
-  forstdb::GpuTrailerWriter* w;
+  forst_gpu::GpuTrailerWriter* w;
 };
 
 FORST_API const char* forst_trailer_writer_last_error(void) { return g_tw_err.c_str(); }
@@ -278,14 +278,14 @@ FORST_API int forst_trailer_writer_open(int checksum_type, uint32_t base_context
                                         uint64_t start_offset, uint32_t block_align,
                                         uint64_t window_bytes, forst_sink_fn sink, void* sink_arg,
                                         void* stream, forst_trailer_writer** out) {
-  if (!out || !sink) return tw_fail(forstdb::Status::InvalidArgument("null sink / out"));
+  if (!out || !sink) return tw_fail(forst_gpu::Status::InvalidArgument("null sink / out"));
   if (checksum_type < FORST_kNoChecksum || checksum_type > FORST_kXXH3)
-    return tw_fail(forstdb::Status::InvalidArgument("unknown ChecksumType " +
+    return tw_fail(forst_gpu::Status::InvalidArgument("unknown ChecksumType " +
                                                     std::to_string(checksum_type)));
   if (block_align && (block_align & (block_align - 1)))
-    return tw_fail(forstdb::Status::InvalidArgument("alignment must be a power of 2"));
-  forstdb::GpuTrailerWriter::Options o;
-  o.checksum = static_cast<forstdb::ChecksumType>(checksum_type);
+    return tw_fail(forst_gpu::Status::InvalidArgument("alignment must be a power of 2"));
+  forst_gpu::GpuTrailerWriter::Options o;
+  o.checksum = static_cast<forst_gpu::ChecksumType>(checksum_type);
   o.base_context_checksum = base_context_checksum;
   o.start_offset = start_offset;
   o.block_align = block_align != 0;
@@ -293,10 +293,10 @@ FORST_API int forst_trailer_writer_open(int checksum_type, uint32_t base_context
   if (window_bytes) o.window_bytes = window_bytes;
   auto fn = [sink, sink_arg](const char* d, size_t n) {
     return sink(sink_arg, reinterpret_cast<const uint8_t*>(d), n) == 0
-               ? forstdb::Status::OK()
-               : forstdb::Status::IOError("sink failed");
+               ? forst_gpu::Status::OK()
+               : forst_gpu::Status::IOError("sink failed");
   };
-  *out = new forst_trailer_writer{new forstdb::GpuTrailerWriter(o, fn, stream)};
+  *out = new forst_trailer_writer{new forst_gpu::GpuTrailerWriter(o, fn, stream)};
   return FORST_OK;
 }
 
@@ -305,23 +305,23 @@ FORST_API int forst_trailer_writer_add(forst_trailer_writer* w, const uint8_t* b
                                        int is_data_block, uint64_t* handle_offset,
                                        uint64_t* handle_size) {
   if (!w || (!block && size) || !handle_offset || !handle_size)
-    return tw_fail(forstdb::Status::InvalidArgument("null argument"));
-  forstdb::Status s = w->w->AddBlock(reinterpret_cast<const char*>(block), size, compression_type,
+    return tw_fail(forst_gpu::Status::InvalidArgument("null argument"));
+  forst_gpu::Status s = w->w->AddBlock(reinterpret_cast<const char*>(block), size, compression_type,
                                      is_data_block != 0, handle_offset, handle_size);
   return s.ok() ? FORST_OK : tw_fail(s);
 }
 
 FORST_API int forst_trailer_writer_flush(forst_trailer_writer* w) {
-  if (!w) return tw_fail(forstdb::Status::InvalidArgument("null writer"));
-  forstdb::Status s = w->w->Flush();
+  if (!w) return tw_fail(forst_gpu::Status::InvalidArgument("null writer"));
+  forst_gpu::Status s = w->w->Flush();
   return s.ok() ? FORST_OK : tw_fail(s);
 }
 
 FORST_API int forst_trailer_writer_footer(forst_trailer_writer* w, uint32_t format_version,
                                           uint64_t metaindex_offset, uint64_t metaindex_size,
                                           uint64_t index_offset, uint64_t index_size) {
-  if (!w) return tw_fail(forstdb::Status::InvalidArgument("null writer"));
-  forstdb::Status s = w->w->WriteFooter(format_version, metaindex_offset, metaindex_size,
+  if (!w) return tw_fail(forst_gpu::Status::InvalidArgument("null writer"));
+  forst_gpu::Status s = w->w->WriteFooter(format_version, metaindex_offset, metaindex_size,
                                         index_offset, index_size);
   return s.ok() ? FORST_OK : tw_fail(s);
 }
@@ -332,7 +332,7 @@ FORST_API uint64_t forst_trailer_writer_offset(const forst_trailer_writer* w) {
 
 FORST_API int forst_trailer_writer_close(forst_trailer_writer* w) {
   if (!w) return FORST_OK;
-  forstdb::Status s = w->w->Flush();
+  forst_gpu::Status s = w->w->Flush();
   delete w->w;
   delete w;
   return s.ok() ? FORST_OK : tw_fail(s);
@@ -347,36 +347,36 @@ FORST_API int forst_sst_footer_build(uint32_t format_version, int checksum_type,
                                      uint64_t metaindex_offset, uint64_t metaindex_size,
                                      uint64_t index_offset, uint64_t index_size, uint8_t* out,
                                      uint32_t* out_len, void* stream) {
-  using forstdb::PutFixed32;
-  using forstdb::PutFixed64;
+  using forst_gpu::PutFixed32;
+  using forst_gpu::PutFixed64;
   if (!out || !out_len) return FORST_EINVAL;
   if (format_version > 6 || checksum_type < 0 || checksum_type > 4) return FORST_EINVAL;
-  uint8_t f[forstdb::kFooterLen];
+  uint8_t f[forst_gpu::kFooterLen];
   std::memset(f, 0, sizeof(f));
   if (format_version == 0) {  // legacy: part2 + legacy magic, kCRC32c implied
     if (checksum_type != FORST_kCRC32c && checksum_type != FORST_kNoChecksum) return FORST_EINVAL;
-    uint8_t* cur = forstdb::PutVarint64(f, metaindex_offset);
-    cur = forstdb::PutVarint64(cur, metaindex_size);
-    cur = forstdb::PutVarint64(cur, index_offset);
-    forstdb::PutVarint64(cur, index_size);
-    PutFixed64(f + 40, forstdb::kLegacyBlockBasedTableMagicNumber);
-    std::memcpy(out, f, forstdb::kVersion0Len);
-    *out_len = forstdb::kVersion0Len;
+    uint8_t* cur = forst_gpu::PutVarint64(f, metaindex_offset);
+    cur = forst_gpu::PutVarint64(cur, metaindex_size);
+    cur = forst_gpu::PutVarint64(cur, index_offset);
+    forst_gpu::PutVarint64(cur, index_size);
+    PutFixed64(f + 40, forst_gpu::kLegacyBlockBasedTableMagicNumber);
+    std::memcpy(out, f, forst_gpu::kVersion0Len);
+    *out_len = forst_gpu::kVersion0Len;
     return FORST_OK;
   }
   f[0] = static_cast<uint8_t>(checksum_type);
   PutFixed32(f + 41, format_version);
-  PutFixed64(f + 45, forstdb::kBlockBasedTableMagicNumber);
+  PutFixed64(f + 45, forst_gpu::kBlockBasedTableMagicNumber);
   if (format_version < 6) {
-    uint8_t* cur = forstdb::PutVarint64(f + 1, metaindex_offset);
-    cur = forstdb::PutVarint64(cur, metaindex_size);
-    cur = forstdb::PutVarint64(cur, index_offset);
-    forstdb::PutVarint64(cur, index_size);
-    std::memcpy(out, f, forstdb::kFooterLen);
-    *out_len = forstdb::kFooterLen;
+    uint8_t* cur = forst_gpu::PutVarint64(f + 1, metaindex_offset);
+    cur = forst_gpu::PutVarint64(cur, metaindex_size);
+    cur = forst_gpu::PutVarint64(cur, index_offset);
+    forst_gpu::PutVarint64(cur, index_size);
+    std::memcpy(out, f, forst_gpu::kFooterLen);
+    *out_len = forst_gpu::kFooterLen;
     return FORST_OK;
   }
-  if (forstdb::ChecksumModifierForContext(base_context_checksum, 0) == 0) return FORST_EINVAL;
+  if (forst_gpu::ChecksumModifierForContext(base_context_checksum, 0) == 0) return FORST_EINVAL;
   if (metaindex_size > 0xffffffffull) return FORST_EUNSUPPORTED;  // "Metaindex block size > 4GB"
   static const uint8_t kExt[4] = {0x3e, 0x00, 0x7a, 0x00};
   std::memcpy(f + 1, kExt, 4);
@@ -392,14 +392,14 @@ FORST_API int forst_sst_footer_build(uint32_t format_version, int checksum_type,
   uint32_t* dmod = reinterpret_cast<uint32_t*>(dz + 76);
   uint32_t* dout = reinterpret_cast<uint32_t*>(dz + 80);
   const uint64_t zero = 0;
-  const uint32_t n52 = forstdb::kFooterLen - 1;
-  const uint32_t mod = forstdb::ChecksumModifierForContext(base_context_checksum, footer_offset);
+  const uint32_t n52 = forst_gpu::kFooterLen - 1;
+  const uint32_t mod = forst_gpu::ChecksumModifierForContext(base_context_checksum, footer_offset);
   uint32_t c = 0;
-  bool ok = hipMemcpyAsync(dz, f, forstdb::kFooterLen, hipMemcpyHostToDevice, st) == hipSuccess &&
+  bool ok = hipMemcpyAsync(dz, f, forst_gpu::kFooterLen, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(doff, &zero, 8, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(dsz, &n52, 4, hipMemcpyHostToDevice, st) == hipSuccess &&
             hipMemcpyAsync(dmod, &mod, 4, hipMemcpyHostToDevice, st) == hipSuccess;
-  int rc = ok ? forst_block_checksum_batch(checksum_type, dz, forstdb::kFooterLen, doff, dsz,
+  int rc = ok ? forst_block_checksum_batch(checksum_type, dz, forst_gpu::kFooterLen, doff, dsz,
                                            nullptr, dmod, dout, 1, stream)
               : FORST_EHIP;
   if (rc == FORST_OK)
@@ -410,7 +410,7 @@ FORST_API int forst_sst_footer_build(uint32_t format_version, int checksum_type,
   (void)hipFree(d);
   if (rc != FORST_OK) return rc;
   PutFixed32(f + 5, c);
-  std::memcpy(out, f, forstdb::kFooterLen);
-  *out_len = forstdb::kFooterLen;
+  std::memcpy(out, f, forst_gpu::kFooterLen);
+  *out_len = forst_gpu::kFooterLen;
   return FORST_OK;
 }

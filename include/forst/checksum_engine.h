@@ -1,7 +1,11 @@
 // include/forst/checksum_engine.h -- C++ host shim over the C ABI, in the
-// reference's own vocabulary (namespace forstdb, ChecksumType, Status), so a
-// ForSt call site can switch from the per-block CPU functions to batched GPU
-// launches without changing types:
+// reference's vocabulary (ChecksumType, Status with the reference's codes and
+// message texts), so a ForSt call site can switch from the per-block CPU
+// functions to batched GPU launches.  Its types live in namespace forst_gpu,
+// NOT forstdb: the header compiles inside a ForSt translation unit next to
+// include/rocksdb/table.h, status.h, table/format.h and util/crc32c.h, and
+// forst/forstdb_adapter.h converts forst_gpu::Status / ChecksumType to and
+// from ROCKSDB_NAMESPACE's there:
 //
 //   reference (per block, CPU)                      this shim (per batch, GPU)
 //   ComputeBuiltinChecksumWithLastByte + modifier   BlockChecksumEngine::ComputeChecksums
@@ -9,8 +13,10 @@
 //   WriteMaybeCompressedBlock trailer               BlockChecksumEngine::WriteTrailers
 //     (block_based_table_builder.cc:1340-1360)
 //   VerifyBlockChecksum (reader_common.cc:26)       BlockChecksumEngine::VerifyBlocks
-//   crc32c::Mask/Unmask (util/crc32c.h:44-53),      forstdb::crc32c::Mask/Unmask,
-//   ChecksumModifierForContext (format.h:119)       forstdb::ChecksumModifierForContext
+//   crc32c::Mask/Unmask (util/crc32c.h:44-53),      forst_gpu::crc32c::Mask/Unmask,
+//   ChecksumModifierForContext (format.h:119)       forst_gpu::ChecksumModifierForContext
+//     (the shim's own copies for code outside ForSt; ForSt call sites keep
+//     the reference's)
 //
 // Statistics hooks mirror BLOCK_CHECKSUM_COMPUTE_COUNT / _MISMATCH_COUNT
 // (include/rocksdb/statistics.h:440,444).
@@ -23,7 +29,7 @@
 
 #include "../forst_checksum.h"
 
-namespace forstdb {
+namespace forst_gpu {
 
 // include/rocksdb/table.h:54-60
 enum ChecksumType : char {
@@ -229,4 +235,4 @@ class GpuTrailerWriter {
   ChecksumStats stats_;
 };
 
-}  // namespace forstdb
+}  // namespace forst_gpu

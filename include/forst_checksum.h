@@ -481,7 +481,7 @@ typedef struct forst_sst_properties {
 } forst_sst_properties;
 
 typedef struct forst_sst_verify_result {
-  int32_t status; /* forstdb::Status::Code: 0 OK, 2 Corruption, 3 NotSupported, ... */
+  int32_t status; /* forst_gpu::Status::Code (= the reference Status::Code): 0 OK, 2 Corruption, 3 NotSupported, ... */
   uint32_t format_version;
   int32_t checksum_type;
   uint32_t index_type;

@@ -17,7 +17,7 @@
 
 #include "forst/checksum_engine.h"
 
-using namespace forstdb;
+using namespace forst_gpu;
 
 static int g_fail = 0;
 #define CHECK(c)                                                  \

@@ -1,4 +1,4 @@
-"""The C++ host shim (namespace forstdb) end to end on the GPU: write trailers,
+"""The C++ host shim (namespace forst_gpu) end to end on the GPU: write trailers,
 verify clean, detect a corrupted block with the reference's exact
 Corruption message (reader_common.cc:55-60)."""
 import os

@@ -6,20 +6,34 @@
 // host memory (the table builder's buffer, a FilePrefetchBuffer, an mmap'd
 // file -- env/io_posix.cc:958).  These entry points take such a host batch and
 // a device list, cut the blocks into contiguous byte-balanced ranges (one per
-// device, forst_partition_bytes) and give every device its own host thread,
-// HIP stream and pinned staging: the thread streams its range through two
+// device, forst_partition_bytes) and give every device its own worker thread,
+// HIP stream and pinned staging: the worker streams its range through two
 // device windows (copy of window k+1 overlaps the kernel on window k), runs
 // the block kernels on them and brings back 4-5 B per block.  No data crosses
-// between devices; the only join is the host threads'.
+// between devices; the only join is the caller's wait for the workers.
 //
-// Host memory that is pinned or registered (hipHostRegister, e.g. an mmap'd
-// SST file: forst_host_register) is copied by DMA straight from the caller's
-// pages; pageable memory is first memcpy'd into the thread's pinned staging.
+// The per-device resources -- worker thread, non-blocking stream, two device
+// windows with descriptor / result arrays, their pinned mirrors and staging
+// -- live in a context that is created once and reused by every later call
+// (a pool per device: concurrent callers each take a free context, so flush,
+// compaction and verify threads never share one).  Buffers only grow; nothing
+// is allocated or freed on the steady-state path, and an error leaves the
+// context intact (nothing to leak).  forst_host_context_stats reports what the
+// pool holds.
+//
+// Host memory that is pinned or registered over the whole batch
+// (hipHostRegister, e.g. an mmap'd SST file: forst_host_register) is copied by
+// DMA straight from the caller's pages; otherwise it is first memcpy'd into the
+// context's pinned staging.
 #include <hip/hip_runtime.h>
 
 #include <algorithm>
+#include <condition_variable>
 #include <cstdint>
 #include <cstring>
+#include <functional>
+#include <map>
+#include <mutex>
 #include <string>
 #include <thread>
 #include <vector>
@@ -36,7 +50,9 @@ int fail(int code, const std::string& m) {
 }
 
 constexpr uint64_t kWindowBytes = 64ull << 20;  // device window per copy (two per device)
-constexpr uint32_t kTrailer = 5;               // block_based_table_reader.h:75
+constexpr uint64_t kWindowBlocks = 1u << 20;    // descriptors per window
+constexpr uint32_t kTrailer = 5;                // block_based_table_reader.h:75
+constexpr uint64_t kPerBlock = 26;              // descriptor + result bytes per block
 
 // [cuts[p], cuts[p+1]) = part p: contiguous, byte-balanced (part p starts at
 // the first block whose byte prefix reaches p/parts of the total) -- the same
@@ -65,6 +81,13 @@ bool is_device_readable_host(const void* p) {
   return at.type == hipMemoryTypeHost;  // pinned or registered
 }
 
+// DMA straight from the caller's pages only if the whole range is pinned or
+// registered: the first and the last byte (a registration that covers part of
+// the range, or was dropped, falls back to staging)
+bool range_device_readable(const uint8_t* base, uint64_t len) {
+  return len && is_device_readable_host(base) && is_device_readable_host(base + len - 1);
+}
+
 enum class Op { kVerify, kChecksum };
 
 struct HostBatch {
@@ -81,16 +104,6 @@ struct HostBatch {
   uint8_t* ok;        // verify, nullable
 };
 
-// One device's share [lo, hi) of the blocks, in windows of at most
-// kWindowBytes (a block larger than that gets a window of its own).
-struct DeviceRun {
-  int device = 0;
-  uint64_t lo = 0, hi = 0;
-  uint64_t mismatches = 0;
-  int rc = FORST_OK;
-  std::string err;
-};
-
 // bytes a block needs in host memory: payload + trailer (verify), payload +
 // type byte (compute without last_bytes), payload (compute with last_bytes)
 uint64_t block_end(const HostBatch& b, uint64_t i) {
@@ -98,107 +111,235 @@ uint64_t block_end(const HostBatch& b, uint64_t i) {
   return b.offsets[i] + b.sizes[i] + extra;
 }
 
-void run_device(const HostBatch& b, bool direct, DeviceRun& r) {
+// one device window: device bytes + descriptors + results, and their pinned
+// mirrors (+ staging for pageable input)
+struct Slot {
+  uint64_t dbytes = 0, blocks = 0, hbytes = 0;  // capacities
+  uint8_t* d = nullptr;
+  uint64_t* d_off = nullptr;
+  uint32_t *d_size = nullptr, *d_mod = nullptr, *d_out = nullptr, *d_st = nullptr;
+  uint8_t *d_last = nullptr, *d_ok = nullptr;
+  unsigned long long* d_bad = nullptr;
+  uint8_t* hbase = nullptr;
+  uint8_t* h = nullptr;  // pinned staging (pageable input)
+  uint64_t* h_off = nullptr;
+  uint32_t *h_size = nullptr, *h_mod = nullptr, *h_out = nullptr, *h_st = nullptr;
+  uint8_t *h_last = nullptr, *h_ok = nullptr;
+  unsigned long long* h_bad = nullptr;
+  hipEvent_t done = nullptr;
+  int64_t win = -1;  // window whose results are pending in this slot
+
+  void release() {
+    (void)hipFree(d);
+    (void)hipHostFree(hbase);
+    d = nullptr;
+    hbase = nullptr;
+    dbytes = blocks = hbytes = 0;
+  }
+  // grow-only: (re)allocate when a call needs more than the slot holds
+  hipError_t reserve(uint64_t need_bytes, uint64_t need_blocks, bool staging) {
+    const uint64_t nb = (need_bytes + 255) & ~255ull;
+    const uint64_t hb = staging ? nb : 0;
+    if (nb <= dbytes && need_blocks <= blocks && hb <= hbytes && d) return hipSuccess;
+    const uint64_t db = std::max(nb, dbytes), m = std::max(need_blocks, blocks),
+                   hs = std::max(hb, hbytes);
+    release();
+    void* p = nullptr;
+    hipError_t e = hipMalloc(&p, db + m * kPerBlock + 64);
+    if (e != hipSuccess) return e;
+    d = static_cast<uint8_t*>(p);
+    d_off = reinterpret_cast<uint64_t*>(d + db);
+    d_size = reinterpret_cast<uint32_t*>(d_off + m);
+    d_mod = d_size + m;
+    d_out = d_mod + m;
+    d_st = d_out + m;
+    d_bad = reinterpret_cast<unsigned long long*>(d_st + m);  // 24 m bytes in: aligned
+    d_last = reinterpret_cast<uint8_t*>(d_bad + 1);
+    d_ok = d_last + m;
+    if ((e = hipHostMalloc(&p, m * kPerBlock + 128 + hs)) != hipSuccess) {
+      (void)hipFree(d);
+      d = nullptr;
+      return e;
+    }
+    hbase = static_cast<uint8_t*>(p);
+    h_off = reinterpret_cast<uint64_t*>(hbase);
+    h_size = reinterpret_cast<uint32_t*>(h_off + m);
+    h_mod = h_size + m;
+    h_out = h_mod + m;
+    h_st = h_out + m;
+    h_bad = reinterpret_cast<unsigned long long*>(h_st + m);
+    h_last = reinterpret_cast<uint8_t*>(h_bad + 1);
+    h_ok = h_last + m;
+    h = hs ? h_ok + m + 64 - ((reinterpret_cast<uintptr_t>(h_ok + m)) & 63) : nullptr;
+    dbytes = db;
+    blocks = m;
+    hbytes = hs;
+    return hipSuccess;
+  }
+};
+
+// a per-device context: worker thread + stream + two slots, reused by every
+// call that takes it from the pool
+struct DeviceCtx {
+  int device = 0;
+  hipStream_t st = nullptr;
+  Slot slot[2];
+  std::thread worker;
+  std::mutex mu;
+  std::condition_variable cv;
+  std::function<void()> job;
+  bool busy = false;
+
+  explicit DeviceCtx(int dev) : device(dev) {
+    worker = std::thread([this] { loop(); });
+    worker.detach();  // contexts live for the whole process
+  }
+  void loop() {
+    (void)hipSetDevice(device);
+    for (;;) {
+      std::function<void()> j;
+      {
+        std::unique_lock<std::mutex> lk(mu);
+        cv.wait(lk, [this] { return static_cast<bool>(job); });
+        j = std::move(job);
+      }
+      j();
+      {
+        std::lock_guard<std::mutex> lk(mu);
+        busy = false;
+      }
+      cv.notify_all();
+    }
+  }
+  void run(std::function<void()> j) {
+    std::lock_guard<std::mutex> lk(mu);
+    busy = true;
+    job = std::move(j);
+    cv.notify_all();
+  }
+  void wait() {
+    std::unique_lock<std::mutex> lk(mu);
+    cv.wait(lk, [this] { return !busy; });
+  }
+  // stream and events, once (on the worker's device)
+  hipError_t init() {
+    if (st) return hipSuccess;
+    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
+    if (e != hipSuccess) {
+      st = nullptr;
+      return e;
+    }
+    for (Slot& s : slot) {
+      if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
+        s.done = nullptr;
+        return e;
+      }
+    }
+    return hipSuccess;
+  }
+};
+
+std::mutex g_pool_mu;
+std::map<int, std::vector<DeviceCtx*>>* g_free = new std::map<int, std::vector<DeviceCtx*>>();
+std::vector<DeviceCtx*>* g_all = new std::vector<DeviceCtx*>();  // never destroyed
+
+DeviceCtx* acquire_ctx(int dev) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  auto& v = (*g_free)[dev];
+  if (!v.empty()) {
+    DeviceCtx* c = v.back();
+    v.pop_back();
+    return c;
+  }
+  DeviceCtx* c = new DeviceCtx(dev);
+  g_all->push_back(c);
+  return c;
+}
+
+void release_ctx(DeviceCtx* c) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  (*g_free)[c->device].push_back(c);
+}
+
+// One device's share [lo, hi) of the blocks, in windows of at most
+// kWindowBytes (a block larger than that gets a window of its own).
+struct DeviceRun {
+  uint64_t lo = 0, hi = 0;
+  uint64_t mismatches = 0;
+  int rc = FORST_OK;
+  std::string err;
+};
+
+struct Window {
+  uint64_t c0, c1, base0, end;  // blocks [c0, c1) in host bytes [base0, end)
+};
+
+void run_device(const HostBatch& b, bool direct, DeviceCtx& cx, DeviceRun& r) {
   auto bail = [&](hipError_t e, const char* what) {
     r.rc = FORST_EHIP;
     r.err = std::string(what) + ": " + hipGetErrorString(e);
   };
-  hipError_t e = hipSetDevice(r.device);
-  if (e != hipSuccess) return bail(e, "hipSetDevice");
   if (r.hi <= r.lo) return;
-  // windows: contiguous block runs whose bytes fit one device window
-  std::vector<std::pair<uint64_t, uint64_t>> win;
+  hipError_t e = cx.init();
+  if (e != hipSuccess) return bail(e, "hipStreamCreate / hipEventCreate");
+  // windows: contiguous block runs whose bytes fit one device window; a
+  // window spans [min offset, max end) of its blocks, so descriptors need not
+  // ascend
+  std::vector<Window> win;
   uint64_t max_bytes = 0, max_blocks = 0;
   for (uint64_t c0 = r.lo; c0 < r.hi;) {
-    const uint64_t base0 = b.offsets[c0] & ~3ull;
-    uint64_t c1 = c0 + 1;
-    while (c1 < r.hi && block_end(b, c1) - base0 <= kWindowBytes && c1 - c0 < (1u << 20)) ++c1;
-    uint64_t end = 0;
-    for (uint64_t i = c0; i < c1; ++i) end = std::max(end, block_end(b, i));
-    max_bytes = std::max(max_bytes, end - base0);
+    uint64_t lo = b.offsets[c0], hi = block_end(b, c0), c1 = c0 + 1;
+    while (c1 < r.hi && c1 - c0 < kWindowBlocks) {
+      const uint64_t nlo = std::min(lo, b.offsets[c1]), nhi = std::max(hi, block_end(b, c1));
+      if (nhi - (nlo & ~3ull) > kWindowBytes) break;
+      lo = nlo;
+      hi = nhi;
+      ++c1;
+    }
+    const uint64_t base0 = lo & ~3ull;
+    max_bytes = std::max(max_bytes, hi - base0);
     max_blocks = std::max(max_blocks, c1 - c0);
-    win.emplace_back(c0, c1);
+    win.push_back({c0, c1, base0, hi});
     c0 = c1;
   }
-  hipStream_t st;
-  if ((e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking)) != hipSuccess)
-    return bail(e, "hipStreamCreate");
-  const uint64_t dbytes = (max_bytes + 255) & ~255ull;
-  // per slot: device window + descriptors + outputs; pinned descriptors,
-  // outputs and (pageable input only) the staged window
-  struct Slot {
-    uint8_t* d = nullptr;
-    uint64_t* d_off = nullptr;
-    uint32_t *d_size = nullptr, *d_mod = nullptr, *d_out = nullptr, *d_st = nullptr;
-    uint8_t *d_last = nullptr, *d_ok = nullptr;
-    unsigned long long* d_bad = nullptr;
-    uint8_t* h = nullptr;  // pinned staging (pageable input)
-    uint64_t* h_off = nullptr;
-    uint32_t *h_size = nullptr, *h_mod = nullptr, *h_out = nullptr, *h_st = nullptr;
-    uint8_t *h_last = nullptr, *h_ok = nullptr;
-    unsigned long long* h_bad = nullptr;
-    hipEvent_t done;
-    int64_t win = -1;  // window whose results are pending in this slot
-  } slot[2];
-  const uint64_t m = max_blocks;
-  for (Slot& s : slot) {
-    void* p = nullptr;
-    if ((e = hipMalloc(&p, dbytes + m * 26 + 64)) != hipSuccess) return bail(e, "hipMalloc");
-    s.d = static_cast<uint8_t*>(p);
-    s.d_off = reinterpret_cast<uint64_t*>(s.d + dbytes);
-    s.d_size = reinterpret_cast<uint32_t*>(s.d_off + m);
-    s.d_mod = s.d_size + m;
-    s.d_out = s.d_mod + m;
-    s.d_st = s.d_out + m;
-    s.d_bad = reinterpret_cast<unsigned long long*>(s.d_st + m);  // 24 m bytes in: aligned
-    s.d_last = reinterpret_cast<uint8_t*>(s.d_bad + 1);
-    s.d_ok = s.d_last + m;
-    if ((e = hipHostMalloc(&p, m * 26 + 128 + (direct ? 0 : dbytes))) != hipSuccess)
-      return bail(e, "hipHostMalloc");
-    s.h_off = static_cast<uint64_t*>(p);
-    s.h_size = reinterpret_cast<uint32_t*>(s.h_off + m);
-    s.h_mod = s.h_size + m;
-    s.h_out = s.h_mod + m;
-    s.h_st = s.h_out + m;
-    s.h_bad = reinterpret_cast<unsigned long long*>(s.h_st + m);
-    s.h_last = reinterpret_cast<uint8_t*>(s.h_bad + 1);
-    s.h_ok = s.h_last + m;
-    s.h = direct ? nullptr : s.h_ok + m + 64 - ((reinterpret_cast<uintptr_t>(s.h_ok + m)) & 63);
-    if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess)
-      return bail(e, "hipEventCreate");
+  for (Slot& s : cx.slot) {
+    if ((e = s.reserve(max_bytes, max_blocks, !direct)) != hipSuccess)
+      return bail(e, "window allocation");
+    s.win = -1;
   }
+  hipStream_t st = cx.st;
   auto collect = [&](Slot& s) -> bool {
     if (s.win < 0) return true;
     hipError_t w = hipEventSynchronize(s.done);
     if (w != hipSuccess) {
       bail(w, "hipEventSynchronize");
+      s.win = -1;
       return false;
     }
-    const uint64_t c0 = win[s.win].first, c1 = win[s.win].second, k = c1 - c0;
-    std::memcpy(b.out + c0, s.h_out, k * 4);
+    const Window& wd = win[s.win];
+    const uint64_t k = wd.c1 - wd.c0;
+    std::memcpy(b.out + wd.c0, s.h_out, k * 4);
     if (b.op == Op::kVerify) {
-      if (b.stored) std::memcpy(b.stored + c0, s.h_st, k * 4);
-      if (b.ok) std::memcpy(b.ok + c0, s.h_ok, k);
+      if (b.stored) std::memcpy(b.stored + wd.c0, s.h_st, k * 4);
+      if (b.ok) std::memcpy(b.ok + wd.c0, s.h_ok, k);
       r.mismatches += *s.h_bad;
     }
     s.win = -1;
     return true;
   };
   for (uint64_t w = 0; w < win.size() && r.rc == FORST_OK; ++w) {
-    Slot& s = slot[w & 1];
+    Slot& s = cx.slot[w & 1];
     if (!collect(s)) break;  // the slot's previous window is done: reuse it
-    const uint64_t c0 = win[w].first, c1 = win[w].second, k = c1 - c0;
-    const uint64_t base0 = b.offsets[c0] & ~3ull;
-    uint64_t end = 0;
-    for (uint64_t i = c0; i < c1; ++i) {
-      end = std::max(end, block_end(b, i));
-      s.h_off[i - c0] = b.offsets[i] - base0;
-      s.h_size[i - c0] = b.sizes[i];
-      if (b.modifiers) s.h_mod[i - c0] = b.modifiers[i];
-      if (b.last_bytes) s.h_last[i - c0] = b.last_bytes[i];
+    const Window& wd = win[w];
+    const uint64_t k = wd.c1 - wd.c0;
+    for (uint64_t i = wd.c0; i < wd.c1; ++i) {
+      s.h_off[i - wd.c0] = b.offsets[i] - wd.base0;
+      s.h_size[i - wd.c0] = b.sizes[i];
+      if (b.modifiers) s.h_mod[i - wd.c0] = b.modifiers[i];
+      if (b.last_bytes) s.h_last[i - wd.c0] = b.last_bytes[i];
     }
-    const uint64_t nbytes = std::min(end, b.base_len) - base0;
-    const uint8_t* src = b.base + base0;
+    const uint64_t nbytes = std::min(wd.end, b.base_len) - wd.base0;
+    const uint8_t* src = b.base + wd.base0;
     if (!direct) {
       std::memcpy(s.h, src, nbytes);
       src = s.h;
@@ -216,7 +357,10 @@ void run_device(const HostBatch& b, bool direct, DeviceRun& r) {
     }
     int rc;
     if (b.op == Op::kVerify) {
-      okc = (e = hipMemsetAsync(s.d_bad, 0, 8, st)) == hipSuccess;
+      if ((e = hipMemsetAsync(s.d_bad, 0, 8, st)) != hipSuccess) {
+        bail(e, "hipMemsetAsync");
+        break;
+      }
       rc = forst_block_verify_batch(b.type, s.d, nbytes, s.d_off, s.d_size,
                                     b.modifiers ? s.d_mod : nullptr, s.d_out, s.d_st, s.d_ok,
                                     s.d_bad, k, st);
@@ -244,16 +388,12 @@ void run_device(const HostBatch& b, bool direct, DeviceRun& r) {
     s.win = static_cast<int64_t>(w);
   }
   if (r.rc == FORST_OK) {
-    collect(slot[0]);
-    if (r.rc == FORST_OK) collect(slot[1]);
+    collect(cx.slot[0]);
+    if (r.rc == FORST_OK) collect(cx.slot[1]);
   }
+  // the context goes back to the pool idle: nothing of this call in flight
   (void)hipStreamSynchronize(st);
-  for (Slot& s : slot) {
-    (void)hipFree(s.d);
-    (void)hipHostFree(s.h_off);
-    (void)hipEventDestroy(s.done);
-  }
-  (void)hipStreamDestroy(st);
+  cx.slot[0].win = cx.slot[1].win = -1;
 }
 
 int run_host_batch(const HostBatch& b, uint64_t n, const int* devices, int n_devices,
@@ -267,22 +407,33 @@ int run_host_batch(const HostBatch& b, uint64_t n, const int* devices, int n_dev
   for (uint64_t i = 0; i < n; ++i)
     if (b.offsets[i] > b.base_len || block_end(b, i) > b.base_len)
       return fail(FORST_EINVAL, "block " + std::to_string(i) + " reaches past base_len");
+  int n_dev_total = 0;
+  if (hipGetDeviceCount(&n_dev_total) != hipSuccess) n_dev_total = 0;
+  for (int d = 0; d < n_devices; ++d)
+    if (devices[d] < 0 || devices[d] >= n_dev_total)
+      return fail(FORST_ENODEV, "no HIP device " + std::to_string(devices[d]));
   std::vector<uint64_t> cuts(n_devices + 1);
   partition(b.sizes, n, static_cast<uint32_t>(n_devices), cuts.data());
-  const bool direct = is_device_readable_host(b.base);
+  const bool direct = range_device_readable(b.base, b.base_len);
   std::vector<DeviceRun> runs(n_devices);
-  std::vector<std::thread> th;
+  std::vector<DeviceCtx*> ctx(n_devices);
   for (int d = 0; d < n_devices; ++d) {
-    runs[d].device = devices[d];
     runs[d].lo = cuts[d];
     runs[d].hi = cuts[d + 1];
-    th.emplace_back(run_device, std::cref(b), direct, std::ref(runs[d]));
+    ctx[d] = acquire_ctx(devices[d]);
+    DeviceCtx* c = ctx[d];
+    DeviceRun* r = &runs[d];
+    c->run([&b, direct, c, r] { run_device(b, direct, *c, *r); });
   }
-  for (auto& t : th) t.join();
+  for (DeviceCtx* c : ctx) {
+    c->wait();
+    release_ctx(c);
+  }
   uint64_t bad = 0;
-  for (const DeviceRun& r : runs) {
-    if (r.rc != FORST_OK) return fail(r.rc, "device " + std::to_string(r.device) + ": " + r.err);
-    bad += r.mismatches;
+  for (int d = 0; d < n_devices; ++d) {
+    if (runs[d].rc != FORST_OK)
+      return fail(runs[d].rc, "device " + std::to_string(devices[d]) + ": " + runs[d].err);
+    bad += runs[d].mismatches;
   }
   if (mismatches) *mismatches = bad;
   return FORST_OK;
@@ -325,6 +476,21 @@ FORST_API int forst_block_checksum_host(int checksum_type, const uint8_t* host_b
   const HostBatch b{Op::kChecksum, checksum_type, host_base, base_len, offsets, sizes, last_bytes,
                     modifiers,     out,           nullptr,   nullptr};
   return run_host_batch(b, n_blocks, devices, n_devices, nullptr);
+}
+
+FORST_API int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
+                                       uint64_t* pinned_bytes) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  uint64_t db = 0, pb = 0;
+  for (const DeviceCtx* c : *g_all)
+    for (const Slot& s : c->slot) {
+      if (s.d) db += s.dbytes + s.blocks * kPerBlock + 64;
+      if (s.hbase) pb += s.blocks * kPerBlock + 128 + s.hbytes;
+    }
+  if (contexts) *contexts = static_cast<uint32_t>(g_all->size());
+  if (device_bytes) *device_bytes = db;
+  if (pinned_bytes) *pinned_bytes = pb;
+  return FORST_OK;
 }
 
 FORST_API int forst_host_register(void* p, uint64_t len) {

@@ -30,6 +30,11 @@
 #include "../../include/forst/checksum_engine.h"
 #include "../../include/forst_checksum.h"
 
+namespace forst {  // the engine's stream-ordered scratch pool (capi.hip)
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream);
+hipError_t scratch_free(void* p, hipStream_t stream);
+}  // namespace forst
+
 namespace forst_gpu {
 
 namespace {
@@ -382,10 +387,11 @@ FORST_API int forst_sst_footer_build(uint32_t format_version, int checksum_type,
   std::memcpy(f + 1, kExt, 4);
   PutFixed32(f + 9, base_context_checksum);
   PutFixed32(f + 13, static_cast<uint32_t>(metaindex_size));
-  // checksum field (f + 5) zero; compute on the GPU
+  // checksum field (f + 5) zero; compute on the GPU, in scratch from the
+  // engine's stream-ordered pool (no driver allocation per footer)
   hipStream_t st = static_cast<hipStream_t>(stream);
   void* d = nullptr;
-  if (hipMalloc(&d, 256) != hipSuccess) return FORST_EHIP;
+  if (forst::scratch_alloc(&d, 256, st) != hipSuccess) return FORST_EHIP;
   uint8_t* dz = static_cast<uint8_t*>(d);
   uint64_t* doff = reinterpret_cast<uint64_t*>(dz + 64);
   uint32_t* dsz = reinterpret_cast<uint32_t*>(dz + 72);
@@ -407,7 +413,7 @@ FORST_API int forst_sst_footer_build(uint32_t format_version, int checksum_type,
                  hipStreamSynchronize(st) == hipSuccess
              ? FORST_OK
              : FORST_EHIP;
-  (void)hipFree(d);
+  (void)forst::scratch_free(d, st);
   if (rc != FORST_OK) return rc;
   PutFixed32(f + 5, c);
   std::memcpy(out, f, forst_gpu::kFooterLen);

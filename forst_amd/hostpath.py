@@ -111,3 +111,11 @@ class MappedFile:
         self._view = None
         self._mm.close()
         os.close(self._fd)
+
+
+def context_stats():
+    """(contexts, device bytes, pinned bytes) held by the host path's
+    per-device context pool (forst_host_context_stats)"""
+    c, d, p = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
+    _check(lib().forst_host_context_stats(ctypes.byref(c), ctypes.byref(d), ctypes.byref(p)))
+    return c.value, d.value, p.value

@@ -397,6 +397,12 @@ int forst_block_checksum_host(int checksum_type, const uint8_t* host_base, uint6
 int forst_host_register(void* p, uint64_t len);
 int forst_host_unregister(void* p);
 const char* forst_host_last_error(void);
+/* The host-memory calls keep one context per device and caller -- worker
+ * thread, HIP stream, two device windows, pinned mirrors and staging --
+ * created on first use and reused by every later call (buffers only grow).
+ * Reports how many contexts exist and the device / pinned bytes they hold. */
+int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
+                             uint64_t* pinned_bytes);
 
 /* ---- Write side of flush / compaction with deferred trailers (§8f-3) --------
  * BlockBasedTableBuilder::WriteMaybeCompressedBlock

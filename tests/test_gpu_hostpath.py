@@ -86,3 +86,51 @@ def test_host_args_rejected():
         hostpath.block_verify_host(9, hb, [0], [10])
     with pytest.raises(ForstError):
         hostpath.block_verify_host(CT.kCRC32c, hb, [0], [10], devices=())
+
+
+def test_back_to_back_calls_reuse_the_context():
+    """1000 forst_block_verify_host calls in a row: after the first, the
+    context pool holds the same contexts and bytes, and free device memory
+    does not move (no per-call hipMalloc / hipHostMalloc / stream)"""
+    b, hb, offs, sizes = batch(2000, (4096, 16384), CT.kCRC32c, 0xF0E57000AE)
+    want = hostpath.block_verify_host(CT.kCRC32c, hb, offs, sizes, devices=(0,))
+    torch.cuda.synchronize()
+    s0 = hostpath.context_stats()
+    free0 = torch.cuda.mem_get_info()[0]
+    for k in range(1000):
+        got = hostpath.block_verify_host(CT.kCRC32c, hb, offs, sizes, devices=(0,))
+        if k % 250 == 0:
+            assert (got[0] == want[0]).all() and got[3] == 0
+    assert hostpath.context_stats() == s0, (s0, hostpath.context_stats())
+    assert torch.cuda.mem_get_info()[0] == free0
+    assert s0[0] >= 1 and s0[1] > 0 and s0[2] > 0
+
+
+def test_out_of_order_descriptors_and_partial_registration():
+    """descriptors that do not ascend (a window spans its blocks' minimum
+    offset) and a pinned buffer of which only the first part is pinned (the
+    batch is staged instead of DMA'd from unpinned pages)"""
+    b, hb, offs, sizes = batch(6000, 4096, CT.kXXH3, 0xF0E57000AF)
+    perm = np.random.default_rng(8).permutation(b.n)
+    comp, _, ok, bad = hostpath.block_verify_host(CT.kXXH3, hb, offs[perm], sizes[perm],
+                                                  devices=(0,))
+    assert bad == 0 and ok.all()
+    want = engine.block_verify_batch(CT.kXXH3, b.base, b.offsets, b.sizes)[0].cpu().numpy()
+    assert (comp == want[perm]).all()
+    import ctypes
+    import mmap
+    from forst_amd._lib import lib
+    mm = mmap.mmap(-1, (len(hb) + 4095) // 4096 * 4096)
+    buf = np.frombuffer(mm, np.uint8)
+    buf[:len(hb)] = hb
+    ptr = ctypes.addressof(ctypes.c_char.from_buffer(mm))
+    half = (len(buf) // 2) // 4096 * 4096
+    assert lib().forst_host_register(ptr, half) == 0  # only the first half pinned
+    try:
+        comp2, _, ok2, bad2 = hostpath.block_verify_host(CT.kXXH3, buf[:len(hb)], offs, sizes,
+                                                         devices=(0,))
+        assert bad2 == 0 and (comp2 == want).all()
+    finally:
+        lib().forst_host_unregister(ptr)
+        del buf
+        mm.close()

@@ -1,0 +1,260 @@
+// forst_amd/csrc/block_codecs.cc -- decompression of the structural blocks
+// the whole-file verify must decode (metaindex, index, index partitions), as
+// BlockFetcher::ReadBlockContents does after the checksum check
+// (table/block_fetcher.cc:242-350 -> UncompressSerializedBlock,
+// table/format.cc:637-700 -> UncompressData, util/compression.h).
+//
+// Block format (util/compression.h): compress_format_version 2 (format_version
+// >= 2, GetCompressFormatForVersion) puts the uncompressed size as a varint32
+// in front of the codec's stream; version 1 (format_version 0-1) does not
+// (Zlib / BZip2: size unknown, output grown; LZ4: an 8-byte legacy header).
+// Codecs: Zlib = raw deflate, windowBits -14 (Zlib_Uncompress); LZ4 / LZ4HC =
+// LZ4 block (LZ4_decompress_safe); ZSTD = a zstd frame; BZip2.  zlib is
+// linked; liblz4 / libzstd / libbz2 are opened at run time when present (the
+// image ships their runtime libraries, not their headers: the few entry points
+// used are declared here with their published C signatures).  Snappy and
+// XPRESS have no library on the image: NotSupported, as a reference build
+// without them reports.  Data blocks are never decompressed -- their checksum
+// covers the compressed bytes.
+#include <dlfcn.h>
+#include <zlib.h>
+
+#include <algorithm>
+#include <cstdint>
+#include <cstring>
+#include <mutex>
+#include <string>
+#include <vector>
+
+#include "../../include/forst_checksum.h"
+
+namespace forst {
+
+namespace {
+
+const char* codec_name(uint8_t t) {  // CompressionTypeToString (util/compression.h)
+  switch (t) {
+    case 0: return "NoCompression";
+    case 1: return "Snappy";
+    case 2: return "Zlib";
+    case 3: return "BZip2";
+    case 4: return "LZ4";
+    case 5: return "LZ4HC";
+    case 6: return "Xpress";
+    case 7: return "ZSTD";
+    default: return "Unknown";
+  }
+}
+
+bool get_varint32(const uint8_t*& p, const uint8_t* lim, uint32_t* v) {
+  uint32_t r = 0;
+  for (uint32_t shift = 0; shift <= 28 && p < lim; shift += 7) {
+    const uint32_t b = *p++;
+    r |= (b & 127) << shift;
+    if (!(b & 128)) {
+      *v = r;
+      return true;
+    }
+  }
+  return false;
+}
+
+// runtime-loaded codec libraries
+struct Libs {
+  int (*lz4_decompress_safe)(const char*, char*, int, int) = nullptr;
+  size_t (*zstd_decompress)(void*, size_t, const void*, size_t) = nullptr;
+  unsigned (*zstd_is_error)(size_t) = nullptr;
+  const char* (*zstd_error_name)(size_t) = nullptr;
+  int (*bz_decompress_init)(void*, int, int) = nullptr;
+  int (*bz_decompress)(void*) = nullptr;
+  int (*bz_decompress_end)(void*) = nullptr;
+};
+
+const Libs& libs() {
+  static Libs L;
+  static std::once_flag once;
+  std::call_once(once, [] {
+    if (void* h = dlopen("liblz4.so.1", RTLD_NOW | RTLD_LOCAL))
+      L.lz4_decompress_safe =
+          reinterpret_cast<int (*)(const char*, char*, int, int)>(dlsym(h, "LZ4_decompress_safe"));
+    if (void* h = dlopen("libzstd.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      L.zstd_decompress = reinterpret_cast<size_t (*)(void*, size_t, const void*, size_t)>(
+          dlsym(h, "ZSTD_decompress"));
+      L.zstd_is_error = reinterpret_cast<unsigned (*)(size_t)>(dlsym(h, "ZSTD_isError"));
+      L.zstd_error_name = reinterpret_cast<const char* (*)(size_t)>(dlsym(h, "ZSTD_getErrorName"));
+      if (!L.zstd_is_error || !L.zstd_error_name) L.zstd_decompress = nullptr;
+    }
+    if (void* h = dlopen("libbz2.so.1", RTLD_NOW | RTLD_LOCAL)) {
+      L.bz_decompress_init =
+          reinterpret_cast<int (*)(void*, int, int)>(dlsym(h, "BZ2_bzDecompressInit"));
+      L.bz_decompress = reinterpret_cast<int (*)(void*)>(dlsym(h, "BZ2_bzDecompress"));
+      L.bz_decompress_end = reinterpret_cast<int (*)(void*)>(dlsym(h, "BZ2_bzDecompressEnd"));
+      if (!L.bz_decompress || !L.bz_decompress_end) L.bz_decompress_init = nullptr;
+    }
+  });
+  return L;
+}
+
+// bz_stream of bzlib.h 1.0.x (the layout its ABI fixes)
+struct BzStream {
+  char* next_in;
+  unsigned int avail_in;
+  unsigned int total_in_lo32, total_in_hi32;
+  char* next_out;
+  unsigned int avail_out;
+  unsigned int total_out_lo32, total_out_hi32;
+  void* state;
+  void* (*bzalloc)(void*, int, int);
+  void (*bzfree)(void*, void*);
+  void* opaque;
+};
+
+// Zlib_Uncompress (util/compression.h:871-960): Z_SYNC_FLUSH steps; Z_OK
+// means the output is full, grown by 20% (at least 10 bytes); any other
+// status than Z_STREAM_END fails
+bool zlib_inflate(const uint8_t* in, size_t n, uint32_t size, bool known,
+                  std::vector<uint8_t>* out) {
+  size_t len = known ? size : std::min<size_t>(((n * 5) & ~size_t(4095)) + 4096, 0xffffffffu);
+  z_stream z;
+  std::memset(&z, 0, sizeof(z));
+  if (inflateInit2(&z, -14) != Z_OK) return false;
+  out->assign(len, 0);
+  z.next_in = const_cast<Bytef*>(in);
+  z.avail_in = static_cast<uInt>(n);
+  z.next_out = out->data();
+  z.avail_out = static_cast<uInt>(len);
+  for (;;) {
+    const int st = inflate(&z, Z_SYNC_FLUSH);
+    if (st == Z_STREAM_END) break;
+    if (st != Z_OK) {
+      inflateEnd(&z);
+      return false;
+    }
+    const size_t old = len;
+    const size_t delta = len / 5;
+    len += delta < 10 ? 10 : delta;
+    out->resize(len);
+    z.next_out = out->data() + old;
+    z.avail_out = static_cast<uInt>(len - old);
+  }
+  out->resize(len - z.avail_out);
+  inflateEnd(&z);
+  return true;
+}
+
+}  // namespace
+
+// BlockFetcher's decompression of one serialized block (contents of type
+// `type`, `n` bytes before the trailer).  FORST_OK with *out = contents;
+// FORST_ECORRUPT / FORST_EUNSUPPORTED with *err = the reference's Status text
+// (UncompressBlockData, table/format.cc:651-668).
+int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, size_t n,
+                     std::vector<uint8_t>* out, std::string* err) {
+  const bool v2 = format_version >= 2;  // GetCompressFormatForVersion
+  const Libs& L = libs();
+  const bool supported = type == 2 || ((type == 4 || type == 5) && L.lz4_decompress_safe) ||
+                         (type == 7 && L.zstd_decompress) || (type == 3 && L.bz_decompress_init);
+  if (!supported) {
+    *err = std::string("Unsupported compression method for this build: ") + codec_name(type);
+    return FORST_EUNSUPPORTED;
+  }
+  const uint8_t* p = in;
+  const uint8_t* lim = in + n;
+  uint32_t size = 0;
+  const char* detail = nullptr;
+  bool ok = false;
+  if (v2 && !get_varint32(p, lim, &size)) {
+    ok = false;
+  } else if (type == 2) {
+    ok = zlib_inflate(p, static_cast<size_t>(lim - p), size, v2, out);
+  } else if (type == 4 || type == 5) {
+    bool hdr = true;
+    if (!v2) {  // legacy: 8-byte header, the low 32 bits the size (Lz4_Uncompress)
+      hdr = lim - p >= 8;
+      if (hdr) {
+        std::memcpy(&size, p, 4);
+        p += 8;
+      }
+    }
+    if (hdr) {
+      out->assign(size, 0);
+      const int r = L.lz4_decompress_safe(reinterpret_cast<const char*>(p),
+                                          reinterpret_cast<char*>(out->data()),
+                                          static_cast<int>(lim - p), static_cast<int>(size));
+      ok = r >= 0 && static_cast<uint32_t>(r) == size;
+    }
+  } else if (type == 7) {
+    if (!v2) {
+      ok = false;  // ZSTD requires format 2 (ZSTD_Uncompress)
+    } else {
+      out->assign(size, 0);
+      const size_t r = L.zstd_decompress(out->data(), size, p, static_cast<size_t>(lim - p));
+      if (L.zstd_is_error(r)) {
+        detail = L.zstd_error_name(r);
+      } else {
+        ok = r == size;
+      }
+    }
+  } else if (type == 3) {
+    BzStream s;
+    std::memset(&s, 0, sizeof(s));
+    if (L.bz_decompress_init(&s, 0, 0) == 0) {
+      out->assign(v2 ? size : (n * 5 + 4095) / 4096 * 4096 + 4096, 0);
+      s.next_in = const_cast<char*>(reinterpret_cast<const char*>(p));
+      s.avail_in = static_cast<unsigned>(lim - p);
+      s.next_out = reinterpret_cast<char*>(out->data());
+      s.avail_out = static_cast<unsigned>(out->size());
+      for (;;) {
+        const int st = L.bz_decompress(&s);
+        if (st == 4) {  // BZ_STREAM_END
+          ok = true;
+          break;
+        }
+        if (st != 0) break;  // BZ_OK
+        if (s.avail_out == 0) {
+          if (v2) break;
+          const size_t used = out->size();
+          out->resize(used * 2);
+          s.next_out = reinterpret_cast<char*>(out->data() + used);
+          s.avail_out = static_cast<unsigned>(out->size() - used);
+        }
+      }
+      const size_t produced = out->size() - s.avail_out;
+      L.bz_decompress_end(&s);
+      if (ok) out->resize(produced);
+    }
+  }
+  if (!ok) {
+    *err = std::string("Corrupted compressed block contents") + (detail ? std::string(": ") + detail : "") +
+           ": " + codec_name(type);
+    return FORST_ECORRUPT;
+  }
+  return FORST_OK;
+}
+
+}  // namespace forst
+
+// ---------------------------------------------------------------------------
+// C ABI: one block's contents as BlockFetcher decompresses them
+// ---------------------------------------------------------------------------
+thread_local std::string g_codec_err;
+
+extern "C" __attribute__((visibility("default"))) int forst_block_uncompress(
+    uint8_t compression_type, uint32_t format_version, const uint8_t* in, uint64_t n, uint8_t* out,
+    uint64_t capacity, uint64_t* out_len, const char** err) {
+  if ((!in && n) || !out_len) return FORST_EINVAL;
+  std::vector<uint8_t> buf;
+  int rc;
+  if (compression_type == 0) {
+    buf.assign(in, in + n);
+    rc = FORST_OK;
+  } else {
+    rc = forst::uncompress_block(compression_type, format_version, in, n, &buf, &g_codec_err);
+  }
+  if (err) *err = rc == FORST_OK ? "" : g_codec_err.c_str();
+  if (rc != FORST_OK) return rc;
+  *out_len = buf.size();
+  if (buf.size() > capacity || (!out && !buf.empty())) return FORST_EINVAL;
+  if (!buf.empty()) std::memcpy(out, buf.data(), buf.size());
+  return FORST_OK;
+}

@@ -27,6 +27,13 @@
 #include "../../include/forst/checksum_engine.h"
 #include "../../include/forst_checksum.h"
 
+namespace forst {
+int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, size_t n,
+                     std::vector<uint8_t>* out, std::string* err);  // block_codecs.cc
+hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream);  // capi.hip
+hipError_t scratch_free(void* p, hipStream_t stream);
+}  // namespace forst
+
 namespace {
 
 constexpr uint64_t kBlockBasedTableMagicNumber = 0x88e241b785f4cff7ull;        // builder.cc:201
@@ -387,7 +394,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   // on the GPU (compute mode: 52 bytes + the last one from memory)
   if (f.format_version >= 6) {  // (kNoChecksum: computed = 0 + modifier)
     void* d = nullptr;
-    Status s = hip_status(hipMalloc(&d, 256), "hipMalloc");
+    Status s = hip_status(forst::scratch_alloc(&d, 256, st), "scratch_alloc");
     if (!s.ok()) return s;
     uint8_t* dz = static_cast<uint8_t*>(d);
     uint64_t* doff = reinterpret_cast<uint64_t*>(dz + 64);
@@ -408,7 +415,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
     }
     if (s.ok()) s = hip_status(hipMemcpyAsync(&got, dout, 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
     if (s.ok()) s = hip_status(hipStreamSynchronize(st), "hipStreamSynchronize");
-    (void)hipFree(d);
+    (void)forst::scratch_free(d, st);
     if (!s.ok()) return s;
     if (got != f.stored_footer_checksum)  // format.cc:425-428
       return Status::Corruption("Footer at " + std::to_string(f.footer_offset) +
@@ -431,7 +438,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       sz[i] = static_cast<uint32_t>(hs[i].size);
     }
     void* d = nullptr;
-    Status s = hip_status(hipMalloc(&d, hs.size() * 12 + 256), "hipMalloc");
+    Status s = hip_status(forst::scratch_alloc(&d, hs.size() * 12 + 256, st), "scratch_alloc");
     if (!s.ok()) return s;
     uint64_t* doffs = static_cast<uint64_t*>(d);
     uint32_t* dsz = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(d) + hs.size() * 8);
@@ -448,7 +455,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       rep.blocks_verified += hs.size();
     }
     (void)hipStreamSynchronize(st);
-    (void)hipFree(d);
+    (void)forst::scratch_free(d, st);
     return s;
   };
   // VerifyBlockChecksum over a host copy of block h (+ trailer) whose 8 bytes
@@ -458,7 +465,7 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
     std::vector<uint8_t> tmp(host_file + h.off, host_file + h.off + len);
     std::memset(tmp.data() + zero_at, 0, 8);
     void* d = nullptr;
-    Status s2 = hip_status(hipMalloc(&d, len + 256), "hipMalloc");
+    Status s2 = hip_status(forst::scratch_alloc(&d, len + 256, st), "scratch_alloc");
     if (!s2.ok()) return s2;
     uint8_t* dblk = static_cast<uint8_t*>(d);
     uint64_t* doff = reinterpret_cast<uint64_t*>(dblk + ((len + 15) & ~uint64_t(15)));
@@ -478,14 +485,31 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       s2 = eng.VerifyBlocks(type, bcc, b, file_name, {h.off}, nullptr);
     }
     (void)hipStreamSynchronize(st);
-    (void)hipFree(d);
+    (void)forst::scratch_free(d, st);
     return s2;
   };
-  auto host_block = [&](const Handle& h, const char* what) -> Status {
+  // the contents BlockFetcher hands the reader after the checksum check:
+  // decompressed when the trailer's type byte says so (block_fetcher.cc:
+  // 333-345, UncompressSerializedBlock) -- metaindex, index and index
+  // partitions; the properties block is read raw (meta_blocks.cc:258-262,
+  // decompress = false)
+  std::vector<std::vector<uint8_t>> keep;  // decompressed contents in use
+  auto host_block = [&](const Handle& h, const char* what, bool decompress, const uint8_t** data,
+                        uint64_t* size) -> Status {
     if (h.off > file_size || h.size > file_size - h.off || file_size - h.off - h.size < kBlockTrailer)
       return Status::Corruption(std::string(what) + " block handle past end of file in " + file_name);
-    if (host_file[h.off + h.size] != 0)  // kNoCompression: structural blocks we decode
-      return Status::NotSupported(std::string("compressed ") + what + " block");
+    *data = host_file + h.off;
+    *size = h.size;
+    const uint8_t t = host_file[h.off + h.size];
+    if (!decompress || t == 0) return Status::OK();
+    keep.emplace_back();
+    std::string err;
+    const int rc2 = forst::uncompress_block(t, f.format_version, host_file + h.off, h.size,
+                                            &keep.back(), &err);
+    if (rc2 == FORST_EUNSUPPORTED) return Status::NotSupported(err);
+    if (rc2 != FORST_OK) return Status::Corruption(err);
+    *data = keep.back().data();
+    *size = keep.back().size();
     return Status::OK();
   };
   // 2. metaindex (+ index when the footer holds it) read with checksum verify
@@ -496,10 +520,12 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
   if (index_in_footer) first.push_back(ix);
   Status s = verify(first, nullptr);
   if (!s.ok()) return s;
-  s = host_block(mi, "metaindex");
+  const uint8_t* blk = nullptr;
+  uint64_t blk_size = 0;
+  s = host_block(mi, "metaindex", true, &blk, &blk_size);
   if (!s.ok()) return s;
   std::vector<MetaEntry> meta;
-  rc = metaindex_entries(host_file + mi.off, mi.size, &meta);
+  rc = metaindex_entries(blk, blk_size, &meta);
   if (rc) return from_sst_rc(rc, file_name, false);
   // 3. properties (ReadTablePropertiesHelper) and the index handle (fv >= 6)
   forst_sst_properties props;
@@ -510,9 +536,9 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
     if (e.name == "rocksdb.properties" || e.name == "rocksdb.stats") {
       // ReadTablePropertiesHelper (meta_blocks.cc:250-417): decode, then the
       // checksum -- retried with an ingested file's global seqno zeroed
-      s = host_block(e.h, "properties");
+      s = host_block(e.h, "properties", false, &blk, &blk_size);
       if (!s.ok()) return s;
-      rc = properties(host_file + e.h.off, e.h.size, &props);
+      rc = properties(blk, blk_size, &props);
       if (rc) return from_sst_rc(rc, file_name, false);
       s = verify({e.h}, nullptr);
       if (s.IsCorruption() && props.global_seqno_value_offset != 0 &&
@@ -528,28 +554,29 @@ static Status WalkSstFile(BlockChecksumEngine& eng, const uint8_t* host_file, ui
       meta_blocks.push_back(e.h);
     }
   }
-  if (!have_index) return Status::Corruption("index block handle missing in " + file_name);
+  // FindMetaBlock (meta_blocks.cc:478-486)
+  if (!have_index) return Status::Corruption("Cannot find the meta block: rocksdb.index");
   rep.index_type = props.index_type;
   // 4. index (and partitions) -> data block handles
   if (!index_in_footer) {
     s = verify({ix}, nullptr);
     if (!s.ok()) return s;
   }
-  s = host_block(ix, "index");
+  s = host_block(ix, "index", true, &blk, &blk_size);
   if (!s.ok()) return s;
   const bool delta = props.index_value_is_delta_encoded != 0;
   const bool first_key = props.index_type == 3;  // kBinarySearchWithFirstKey
   std::vector<Handle> top, data;
-  rc = index_handles(host_file + ix.off, ix.size, delta, first_key, &top);
+  rc = index_handles(blk, blk_size, delta, first_key, &top);
   if (rc) return from_sst_rc(rc, file_name, false);
   if (props.index_type == 2) {  // kTwoLevelIndexSearch: top level -> partitions
     rep.index_partitions = top.size();
     s = verify(top, nullptr);
     if (!s.ok()) return s;
     for (const Handle& p : top) {
-      s = host_block(p, "index partition");
+      s = host_block(p, "index partition", true, &blk, &blk_size);
       if (!s.ok()) return s;
-      rc = index_handles(host_file + p.off, p.size, delta, first_key, &data);
+      rc = index_handles(blk, blk_size, delta, first_key, &data);
       if (rc) return from_sst_rc(rc, file_name, false);
     }
   } else {

@@ -401,6 +401,19 @@ const char* forst_host_last_error(void);
  * thread, HIP stream, two device windows, pinned mirrors and staging --
  * created on first use and reused by every later call (buffers only grow).
  * Reports how many contexts exist and the device / pinned bytes they hold. */
+/* BlockFetcher's decompression of one block (table/block_fetcher.cc:333-345,
+ * UncompressSerializedBlock, table/format.cc:637-700), host only: the
+ * structural blocks the whole-file verify decodes.  compression_type =
+ * CompressionType (0 none, 2 Zlib, 3 BZip2, 4 LZ4, 5 LZ4HC, 7 ZSTD; zlib is
+ * linked, the others are opened from the system's runtime libraries;
+ * 1 Snappy / 6 XPRESS: FORST_EUNSUPPORTED).  format_version >= 2 blocks carry
+ * a varint32 size in front (compress_format_version 2).  FORST_ECORRUPT /
+ * FORST_EUNSUPPORTED set *err to the reference's message ("Corrupted
+ * compressed block contents: Zlib", "Unsupported compression method for this
+ * build: Snappy"); FORST_EINVAL if capacity is short (*out_len = size). */
+int forst_block_uncompress(uint8_t compression_type, uint32_t format_version,
+                           const uint8_t* in, uint64_t n, uint8_t* out, uint64_t capacity,
+                           uint64_t* out_len, const char** err);
 int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
                              uint64_t* pinned_bytes);
 

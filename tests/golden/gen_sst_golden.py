@@ -17,7 +17,18 @@ output for format_version 0-6 x the 5 checksum types as ref_footers.json.
 tests/test_sst_pinned.py then checks that sstgen's own restated encodings
 write the same bytes, and the GPU verify / writer paths run on these files.
 
-Re-run:  python tests/golden/gen_sst_golden.py   (needs /root/reference + g++)
+Second family (round 3): whole files from the reference's own
+SstFileWriter -> BlockBasedTableBuilder (tests/golden/ref_sstwriter_shim.cc,
+linked against the reference archive of tests/golden/refbuild.py), so block
+ORDER, filter blocks and partitions, index partitions, range-deletion and
+compression-dictionary blocks, and zlib-compressed data AND index blocks
+(enable_index_compression, include/rocksdb/table.h:526) are all the
+reference's: tests/golden/sst/builder_*.sst + builder_manifest.json.  For
+each file, single-byte corruptions of chosen blocks (located with
+tests/sstwalk.py) are run through the reference's SstFileReader::
+VerifyChecksum, and its Status text is recorded ("{file}" stands for the path).
+
+Re-run:  python tests/golden/gen_sst_golden.py [--builder]   (needs /root/reference + g++)
 """
 import ctypes
 import json
@@ -154,8 +165,94 @@ class RefCodec:
                      mi[0], mi[1], ix[0], ix[1], bcc)
 
 
+# SstFileWriter configurations: (format_version, checksum, index type, filter
+# (0 none, 1 full bloom, 2 partitioned), compression (0 none, 2 zlib), index
+# compression, block_size, restart interval, keys, value length, range
+# deletions, compression dictionary bytes, seed)
+BUILDER_CONFIGS = [
+    (5, 1, 0, 1, 2, 1, 1024, 16, 700, 60, 0, 0, 201),
+    (6, 4, 2, 2, 2, 1, 1024, 16, 1100, 60, 2, 0, 202),
+    (6, 1, 3, 1, 2, 1, 2048, 4, 800, 80, 0, 4096, 203),
+    (5, 4, 0, 0, 0, 0, 4096, 16, 500, 100, 1, 0, 204),
+    (4, 3, 2, 1, 2, 1, 1024, 16, 700, 60, 0, 0, 205),
+    (3, 2, 0, 1, 2, 0, 1024, 16, 500, 60, 0, 0, 206),
+    (6, 0, 0, 1, 2, 1, 1024, 16, 400, 60, 0, 0, 207),
+    (2, 1, 2, 2, 2, 1, 512, 1, 900, 40, 1, 0, 208),
+    (5, 1, 2, 2, 2, 1, 512, 16, 1400, 40, 0, 0, 209),
+    (1, 1, 0, 1, 2, 1, 1024, 16, 600, 60, 0, 0, 210),  # compress_format_version 1
+    (0, 1, 2, 0, 2, 1, 1024, 16, 600, 60, 0, 0, 211),
+]
+FLIP_KINDS = ("data", "index", "index_partition", "metaindex", "properties", "filter",
+              "filter_index", "filter_partition", "rangedel", "dict")
+
+
+def gen_builder_files(tmp):
+    import sstwalk
+    so = os.path.join(tmp, "libref_sstw.so")
+    sys.path.insert(0, HERE)
+    import refbuild
+    refbuild.link_veneer([os.path.join(HERE, "ref_sstwriter_shim.cc")], so)
+    L = ctypes.CDLL(so)
+    L.ref_sst_write.restype = ctypes.c_int
+    L.ref_sst_verify.restype = ctypes.c_int
+    err = ctypes.create_string_buffer(1024)
+    files = []
+    for i, (fv, ct, it, flt, comp, icomp, bs, ri, nk, vl, rd, db, seed) in enumerate(BUILDER_CONFIGS):
+        name = f"builder_fv{fv}_ct{ct}_ix{it}_f{flt}_c{comp}.sst"
+        path = os.path.join(tmp, name)
+        rc = L.ref_sst_write(path.encode(), fv, ct, it, flt, comp, icomp, bs, ri, nk, vl,
+                             ctypes.c_ulonglong(seed), rd, db, err, 1024)
+        assert rc == 0, err.value
+        data = open(path, "rb").read()
+        blocks, f = sstwalk.walk(data)
+        assert sstwalk.tiles(blocks, f), name
+        rc = L.ref_sst_verify(path.encode(), err, 1024)
+        assert rc == 0, err.value
+        flips = []
+        for kind in FLIP_KINDS:
+            ks = [b for b in blocks if b[0] == kind]
+            for b in (ks[:1] + ks[len(ks) // 2:len(ks) // 2 + 1] if kind == "data" else ks[:1]):
+                _, o, n, _ = b
+                at = o + n // 2
+                bad = bytearray(data)
+                bad[at] ^= 0x20
+                cpath = os.path.join(tmp, "corrupt_" + name)
+                open(cpath, "wb").write(bad)
+                L.ref_sst_verify(cpath.encode(), err, 1024)
+                flips.append({"kind": kind, "block": [o, n], "offset": at,
+                              "status": err.value.decode().replace(cpath, "{file}")})
+        if f["fv"] >= 6:  # the footer checksum field
+            bad = bytearray(data)
+            bad[f["footer_offset"] + 6] ^= 0x01
+            cpath = os.path.join(tmp, "corrupt_" + name)
+            open(cpath, "wb").write(bad)
+            L.ref_sst_verify(cpath.encode(), err, 1024)
+            flips.append({"kind": "footer", "block": [f["footer_offset"], 53],
+                          "offset": f["footer_offset"] + 6,
+                          "status": err.value.decode().replace(cpath, "{file}")})
+        with open(os.path.join(OUT_DIR, name), "wb") as fh:
+            fh.write(data)
+        files.append({"file": name, "format_version": fv, "checksum": ct, "index_type": it,
+                      "filter": flt, "compression": comp, "index_compression": icomp,
+                      "block_size": bs, "restart_interval": ri, "keys": nk, "value_len": vl,
+                      "range_dels": rd, "dict_bytes": db, "seed": seed, "size": len(data),
+                      "blocks": [[k, o, n, t] for k, o, n, t in blocks],
+                      "footer_offset": f["footer_offset"], "flips": flips})
+        print(name, len(data), len(blocks), [x["status"][:60] for x in flips][:3])
+    with open(os.path.join(OUT_DIR, "builder_manifest.json"), "w") as fh:
+        json.dump({"generator": "tests/golden/gen_sst_golden.py (SstFileWriter, "
+                                "table/sst_file_writer.cc; SstFileReader::VerifyChecksum)",
+                   "files": files}, fh, indent=0)
+
+
 def main():
     tmp = tempfile.mkdtemp(prefix="forst_ref_sst_")
+    if "--builder" in sys.argv:
+        try:
+            gen_builder_files(tmp)
+        finally:
+            shutil.rmtree(tmp, ignore_errors=True)
+        return
     try:
         L = build_reference(tmp)
         codec = RefCodec(L)
@@ -191,6 +288,7 @@ def main():
             json.dump({"generator": "tests/golden/gen_sst_golden.py (FooterBuilder::Build, "
                                     "table/format.cc:231)", "footers": footers}, fh, indent=0)
         print(f"{len(manifest)} SST files, {len(footers)} footers")
+        gen_builder_files(tmp)
     finally:
         shutil.rmtree(tmp, ignore_errors=True)
 

@@ -56,9 +56,11 @@ CONFIGS = {
     "C4": (1 << 19, 16384, 1, "compaction-shaped 8 GiB/GPU of 16 KiB kCRC32c compute+verify"),
     "NS16": (1 << 20, 16384, 1, "north-star 1 M x 16 KiB kCRC32c compute+verify"),
     "NS16X": (1 << 20, 16384, 4, "north-star 1 M x 16 KiB kXXH3 compute+verify"),
+    "C3S": (1 << 20, ("sorted", (4096, 16384, 65536)), 4,
+            "C3's blocks sorted by size (64 KiB, then 16 KiB, then 4 KiB) kXXH3 compute+verify"),
 }
 SEEDS = {"C2": 0xF0E5700002, "C3": 0xF0E5700003, "C4": 0xF0E5700004,
-         "NS16": 0xF0E5700002, "NS16X": 0xF0E5700002}
+         "NS16": 0xF0E5700002, "NS16X": 0xF0E5700002, "C3S": 0xF0E5700003}
 
 
 def algorithmic_bytes(kind, payload_bytes, n):
@@ -518,8 +520,10 @@ def main():
     del b
     torch.cuda.empty_cache()
     if world == 1 and not args.no_extras and args.config == "C2":
-        for nm in ("NS16", "NS16X", "C3", "C4"):
-            r = run_config(nm, max(3, args.steps // 2), 1, rank, world)
+        for nm in ("NS16", "NS16X", "C3", "C3S", "C4"):
+            # the north-star points with the headline's step and warmup counts
+            r = run_config(nm, args.steps if nm.startswith("NS") else max(3, args.steps // 2),
+                           args.warmup if nm.startswith("NS") else 1, rank, world)
             r.pop("batch")
             torch.cuda.empty_cache()
             kv, kt = r["kernels"]["verify"], r["kernels"]["trailer"]

@@ -47,6 +47,7 @@ struct BatchFeed {
   uint64_t g;    // start of the last batch handed out
   uint64_t lim;  // end of the static share / chunk it belongs to
   uint64_t rr;   // round-robin ticket (no counter)
+  uint64_t wlo, whi;  // workgroup feed: this workgroup's descriptor range
   uint32_t len;  // entries of the last batch handed out (0 once exhausted)
 };
 
@@ -77,19 +78,20 @@ __device__ __forceinline__ uint64_t feed_claim_global(const BlockArgs& a, uint64
   return f.g;
 }
 
-// Workgroup feed (WG = true; the CRC rows kernel's block modes): workgroup b
-// owns the contiguous range [b * W, (b + 1) * W) of descriptors (W = n / grid
-// rounded up to 16), and its waves take 16-descriptor batches of it from an
-// LDS counter.
+// Workgroup feed (WG = true; the rows kernels' block modes): workgroup b owns
+// a contiguous descriptor range [L(b), L(b + 1)) of about 1/G of the batch's
+// BYTES (wg_range below), and its waves take CHUNK-descriptor batches of it
+// from an LDS counter.
 // - An LDS atomic waits on lgkmcnt only, so a claim does not drain the
 //   wave's loads in flight (a global claim does: vmcnt(0)).
-// - The 16-descriptor grain lets the fast and slow waves of a SIMD finish
-//   together. The four waves of a SIMD progress at different rates
-//   (age-ordered), and the global feed's last 64-descriptor chunk left them
-//   idle for 7-13 % of a C2 launch (tools/wave_tail.py).
-// Workgroups are not balanced against each other: measured, the spread of
-// their finish times is a few per cent on uniform blocks.  Mixed sizes
-// (XXH3 C3, WAL records) keep the global feed.
+// - The small grain lets the fast and slow waves of a SIMD finish together.
+//   The four waves of a SIMD progress at different rates (age-ordered), and
+//   the global feed's last 64-descriptor chunk left them idle for 7-13 % of a
+//   C2 launch (tools/wave_tail.py).
+// - Ranges by bytes, not by count (round 3): a batch sorted or clustered by
+//   block size (64 KiB blocks, then 4 KiB; an arena of SST files with
+//   different block sizes) would otherwise give some workgroups many times
+//   the bytes of others.
 constexpr uint32_t kWgChunk = 16;
 __device__ __forceinline__ uint32_t* feed_lds_ctr() {
   __shared__ uint32_t ctr;
@@ -99,22 +101,74 @@ __device__ __forceinline__ uint32_t* feed_lds_ctr() {
 __device__ __forceinline__ void feed_init() {
   if (threadIdx.x == 0) *feed_lds_ctr() = 0;
 }
+
+// off0 + floor(span * b / G) without 128-bit arithmetic
+__device__ __forceinline__ uint64_t frac_point(uint64_t off0, uint64_t span, uint64_t b,
+                                               uint64_t G) {
+  return off0 + (span / G) * b + ((span % G) * b) / G;
+}
+
+// L(b): the number of descriptors "before" byte target t, by a 64-ary
+// COUNTING search over offsets[] -- at each level the next segment is chosen
+// by how many of the 63 probes lie below t, which is non-decreasing in t for
+// any order of the array.  So L is monotone in b and [L(b), L(b+1)) tiles
+// [0, n) exactly whatever the descriptors; when they are in file order (an
+// SST, an arena of SSTs) it is lower_bound and the ranges are byte-balanced.
+// Both bounds of the workgroup are searched together (their loads overlap):
+// ceil(log64 n) dependent rounds, 4 for 1 M descriptors.
+__device__ __forceinline__ void wg_range(const BlockArgs& a, uint32_t lane, uint64_t* lo_out,
+                                         uint64_t* hi_out) {
+  const uint64_t n = a.n, G = gridDim.x, b = blockIdx.x;
+  const uint64_t off0 = a.offsets[0];
+  const uint64_t last = a.offsets[n - 1] + a.sizes[n - 1];
+  if (last <= off0 || G == 1) {  // no byte span to split: by count
+    const uint64_t W = (n + G - 1) / G;
+    *lo_out = b * W < n ? b * W : n;
+    *hi_out = (b + 1) * W < n ? (b + 1) * W : n;
+    return;
+  }
+  const uint64_t span = last - off0;
+  const uint64_t t0 = frac_point(off0, span, b, G), t1 = frac_point(off0, span, b + 1, G);
+  uint64_t lo0 = 0, len0 = n, lo1 = 0, len1 = n;
+  while (len0 > 64 || len1 > 64) {
+    const uint64_t st0 = (len0 + 63) / 64, st1 = (len1 + 63) / 64;
+    const uint64_t q0 = lo0 + lane * st0, q1 = lo1 + lane * st1;
+    const bool v0 = len0 > 64 && lane > 0 && q0 < lo0 + len0;
+    const bool v1 = len1 > 64 && lane > 0 && q1 < lo1 + len1;
+    const uint64_t k0 = a.offsets[v0 ? q0 : 0], k1 = a.offsets[v1 ? q1 : 0];
+    const uint64_t c0 = static_cast<uint64_t>(__popcll(__ballot(v0 && k0 < t0)));
+    const uint64_t c1 = static_cast<uint64_t>(__popcll(__ballot(v1 && k1 < t1)));
+    if (len0 > 64) {
+      const uint64_t e = lo0 + len0;
+      lo0 += c0 * st0;
+      len0 = e - lo0 < st0 ? e - lo0 : st0;
+    }
+    if (len1 > 64) {
+      const uint64_t e = lo1 + len1;
+      lo1 += c1 * st1;
+      len1 = e - lo1 < st1 ? e - lo1 : st1;
+    }
+  }
+  const bool f0 = lane < len0, f1 = lane < len1;
+  const uint64_t k0 = a.offsets[f0 ? lo0 + lane : 0], k1 = a.offsets[f1 ? lo1 + lane : 0];
+  const uint64_t L0 = lo0 + static_cast<uint64_t>(__popcll(__ballot(f0 && k0 < t0)));
+  const uint64_t L1 = lo1 + static_cast<uint64_t>(__popcll(__ballot(f1 && k1 < t1)));
+  *lo_out = b == 0 ? 0 : uniform64(L0);
+  *hi_out = b + 1 == G ? n : uniform64(L1);
+}
+
 template <uint32_t CHUNK>
 __device__ __forceinline__ uint64_t feed_claim_wg(const BlockArgs& a, uint32_t lane,
                                                   BatchFeed& f) {
   uint32_t p = 0;
   if (lane == 0) p = atomicAdd(feed_lds_ctr(), CHUNK);
   p = readlane32(p, 0);
-  const uint64_t G = gridDim.x;
-  const uint64_t W = ((a.n + G - 1) / G + CHUNK - 1) / CHUNK * CHUNK;
-  const uint64_t lo = blockIdx.x * W < a.n ? blockIdx.x * W : a.n;
-  const uint64_t hi = lo + W < a.n ? lo + W : a.n;
-  f.g = lo + p;
-  if (f.g >= hi) {
+  f.g = f.wlo + p;
+  if (f.g >= f.whi) {
     f.g = a.n;  // exhausted (stays so)
     f.len = 0;
   } else {
-    f.len = static_cast<uint32_t>(hi - f.g < CHUNK ? hi - f.g : CHUNK);
+    f.len = static_cast<uint32_t>(f.whi - f.g < CHUNK ? f.whi - f.g : CHUNK);
   }
   f.lim = f.g + f.len;
   return f.g;
@@ -126,7 +180,10 @@ template <bool WG, uint32_t CHUNK = kWgChunk>
 __device__ __forceinline__ uint64_t feed_first(const BlockArgs& a, uint64_t nw, uint64_t gw,
                                                uint32_t lane, BatchFeed& f) {
   f.rr = gw;
-  if (WG) return feed_claim_wg<CHUNK>(a, lane, f);
+  if (WG) {
+    wg_range(a, lane, &f.wlo, &f.whi);
+    return feed_claim_wg<CHUNK>(a, lane, f);
+  }
   if (a.share1 == 0) return feed_claim_global(a, nw, lane, f);
   f.g = gw * a.share1;
   f.lim = f.g + a.share1;

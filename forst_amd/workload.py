@@ -37,6 +37,8 @@ def block_sizes(n, spec, seed):
           tuple of ints  -> equal shares of each class, shuffled (C3)
           ("dev", b)     -> uniform in [0.9 b, b] (block_size_deviation=10, C3b)
           ("logu", lo, hi) -> log-uniform in [lo, hi] (the C5 record mix)
+          ("sorted", (a, b, ..)) -> the shuffled mix sorted largest first (C3S:
+                             the same blocks as C3, clustered by size)
     """
     idx = np.arange(n, dtype=np.uint64)
     with np.errstate(over="ignore"):
@@ -45,6 +47,8 @@ def block_sizes(n, spec, seed):
         return np.full(n, spec, dtype=np.uint32)
     if isinstance(spec, tuple) and spec and spec[0] == "logu":  # log-uniform [lo, hi] (C5-like)
         return log_uniform_lengths(n, int(spec[1]), int(spec[2]), seed)
+    if isinstance(spec, tuple) and spec and spec[0] == "sorted":
+        return np.sort(block_sizes(n, tuple(spec[1]), seed))[::-1].copy()
     if isinstance(spec, tuple) and spec and spec[0] == "dev":
         b = int(spec[1])
         lo = (b * 9) // 10

@@ -341,6 +341,9 @@ FULL_SIZE = {  # bench.py CONFIGS: (blocks, size spec, checksum type, seed)
     "C4": (1 << 19, 16384, CT.kCRC32c, workload.SEEDS["C4"]),
     "NS16": (1 << 20, 16384, CT.kCRC32c, workload.SEEDS["C2"]),
     "NS16X": (1 << 20, 16384, CT.kXXH3, workload.SEEDS["C2"]),
+    # C3's blocks sorted by size: the byte-balanced workgroup ranges
+    "C3S": (1 << 20, ("sorted", (4096, 16384, 65536)), CT.kXXH3, workload.SEEDS["C3"]),
+    "C3S_CRC": (1 << 20, ("sorted", (4096, 16384, 65536)), CT.kCRC32c, workload.SEEDS["C3"]),
 }
 
 
@@ -375,6 +378,22 @@ def test_full_size_properties(cfg):
     _, _, ok, bad = engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes)
     assert int(host(bad)[0]) == 64
     assert set(np.nonzero(host(ok) == 0)[0].tolist()) == set(victims.tolist())
+
+
+@pytest.mark.parametrize("ctype", [CT.kCRC32c, CT.kXXH3])
+def test_descriptors_in_any_order(ctype):
+    """the workgroup ranges come from a counting search over offsets[]: exact
+    cover for descriptors in any order (a random permutation of a mixed batch,
+    and a reversed one) -- every block verified once, results in place"""
+    n = 200_000
+    b = workload.make_sst_batch(n, (4096, 16384, 65536), 0xF0E57000C1, ctype=ctype)
+    want = host(engine.block_verify_batch(ctype, b.base, b.offsets, b.sizes)[0])
+    for perm in (np.random.default_rng(2).permutation(n), np.arange(n)[::-1].copy()):
+        p = torch.from_numpy(perm).to(DEV)
+        comp, _, ok, bad = engine.block_verify_batch(ctype, b.base, b.offsets[p].contiguous(),
+                                                     b.sizes[p].contiguous())
+        assert int(host(bad)[0]) == 0 and host(ok).all()
+        assert (host(comp) == want[perm]).all()
 
 
 # ---- a15: Hash64 (XXPH3) and per-KV protection (db/kv_checksum.h) ---------

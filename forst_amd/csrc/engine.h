@@ -38,6 +38,11 @@ struct BlockArgs {
   unsigned long long* ticket;
   uint64_t share1;
   int kernel_hint;  // CRC: 0 by mean block size, 1 rows kernel, 2 v2 kernel; XXH3: 3 v1 kernel
+  // fused WAL-recovery CRC (launch_xxh3_frag_crc): per physical record, the
+  // constants (E | Z << 32) and the CRC verdict; modifiers = the record's
+  // first physical record index
+  const uint64_t* crc_ez;
+  uint8_t* crc_ok;
 };
 
 struct WalArgs {
@@ -118,6 +123,9 @@ hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a,
 // (xxh3.hip xxh3_frag_kernel): offsets = first payload byte, sizes = record
 // length, init_crcs = frag_info (hs | j_last << 8); needs base_len >= 4096
 hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char** kernel_name);
+// the fragment kernel with every physical record's CRC32C checked from the
+// same loads (wal_recover.hip): long records (> 240 B) only
+hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const char** kernel_name);
 hipError_t launch_noop_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
 // kxxHash (x64 = false, XXH32) / kxxHash64 (x64 = true, Lower32 of XXH64)

@@ -60,6 +60,7 @@
 #include <vector>
 
 #include "../../include/forst_checksum.h"
+#include "crc32c_tables.h"
 #include "device_common.h"
 #include "engine.h"
 #include "scan_common.h"
@@ -108,6 +109,7 @@ struct RecoverArgs {
   uint64_t n_blocks;
   uint32_t log_number;
   int mode;  // WALRecoveryMode
+  int fuse;  // candidates through the fused CRC + XXH3 kernel
 };
 
 __device__ __forceinline__ bool recyclable_type(uint32_t t) {  // log_format.h:20-41
@@ -218,6 +220,180 @@ __global__ void __launch_bounds__(kLanes) rw_fill_kernel(RecoverArgs a, const ui
                       crc_stored, ipack);
 }
 
+// ---- candidates: records laid out as log::Writer lays them out ---------------
+// The reader's records are only known after the CRCs (the state machine
+// below), but a log written by log::Writer::AddRecord (log_writer.cc:65-160)
+// is a run of such records: a Full, or a First whose fragments fill their
+// blocks, the next one right after the next block's header, up to a Last.
+// Every such run is a CANDIDATE: one pass of the fragment kernel with the
+// fused CRC (xxh3.hip xxh3_frag_kernel<3, true>) reads its bytes ONCE for both
+// the XXH3 record checksum and the CRC32C of each physical record.  Records
+// the state machine emits that are exactly a candidate (same first and last
+// physical record, XXH3 state reset at its head) take the candidate's hash;
+// everything else -- corrupted, re-typed, recycled or zero-filled logs -- is
+// CRC'd by the rows kernel (raw) and hashed by hash_logical_records.
+__device__ __forceinline__ uint32_t ct_shift(const uint32_t* T, uint32_t v) {  // 4 x 256 table
+  return T[v & 0xffu] ^ T[256 + ((v >> 8) & 0xffu)] ^ T[512 + ((v >> 16) & 0xffu)] ^
+         T[768 + (v >> 24)];
+}
+// v * x^(8n) mod P (raw CRC32C state moved over n zero bytes), n <= 1024
+__device__ __forceinline__ uint32_t crc_shift_bytes(uint32_t v, uint32_t n) {
+  const uint32_t a6 = n >> 6, b4 = (n >> 2) & 15u, r = n & 3u;
+  if (a6) v = ct_shift(kCrcS64 + 1024 * (a6 - 1), v);
+  if (b4) v = ct_shift(kCrcS4 + 1024 * (b4 - 1), v);
+  for (uint32_t i = 0; i < r; ++i) v = (v >> 8) ^ kCrcG[3 * 256 + (v & 0xffu)];  // Sarwate
+  return v;
+}
+// the CRC32C state after header bytes [6, hs) from ~0 (log_writer.cc:240-258)
+__device__ __forceinline__ uint32_t crc_header_state(const uint8_t* h, uint32_t hs) {
+  uint32_t v = 0xffffffffu;
+  for (uint32_t i = 6; i < hs; ++i) v = (v >> 8) ^ kCrcG[3 * 256 + ((v ^ h[i]) & 0xffu)];
+  return v;
+}
+
+struct Cand {
+  uint8_t* head;       // per item: 1 = a candidate starts here
+  uint8_t* fused;      // per item: its CRC comes from the fused kernel
+  uint64_t* ez;        // per item: E | Z << 32
+  uint64_t* p0;        // per item (heads): payload start of the first non-empty fragment
+  uint32_t* len;       //   logical length
+  uint32_t* info;      //   hs | j_last << 8 (0: one fragment)
+  uint32_t* first;     //   item of the first non-empty fragment
+  uint32_t* last;      //   last item
+};
+
+__global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t ni,
+                                                         const uint64_t* it_off,
+                                                         const uint8_t* it_old,
+                                                         const uint32_t* ipack,
+                                                         const uint32_t* crc_stored, Cand c) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= ni) return;
+  c.head[i] = 0;
+  c.fused[i] = 0;
+  if (!a.fuse) return;  // (logs under 4 KiB: the rows kernels' dummy loads need 4 KiB)
+  auto ltype = [&](uint64_t q) {  // legacy type of item q (0: none of Full..Last)
+    const uint32_t ty = (ipack[q] >> 16) & 0xffu;
+    const uint32_t nt = (ty >= 5 && ty <= 8) ? ty - 4 : ty;
+    return it_old[q] || nt < 1 || nt > 4 ? 0u : nt;
+  };
+  const uint32_t t0 = ltype(i);
+  if (t0 != 1 && t0 != 2) return;
+  const uint32_t pk0 = ipack[i];
+  const uint32_t rec0 = (pk0 >> 24) & 1u;
+  const uint32_t hs = rec0 ? kLogRHdr : kLogHdr;
+  uint64_t q = i, prev_end = 0, total = 0, start = 0, first = i;
+  uint32_t nz = 0, last_len = 0;
+  bool ok = true;
+  for (;; ++q) {  // the run i .. q (wh_prep_kernel's regularity, wal_hash.h)
+    if (q >= ni) {
+      ok = false;
+      break;
+    }
+    const uint32_t tq = ltype(q);
+    const uint32_t pk = ipack[q];
+    const uint64_t h = it_off[q];
+    const uint32_t l = pk & 0xffffu;
+    if (q > i && (tq != 3 && tq != 4)) {
+      ok = false;
+      break;
+    }
+    if (((pk >> 24) & 1u) != rec0) ok = false;
+    if (q > i && (h != prev_end || (h & (kLogBlock - 1)) != 0)) ok = false;
+    if (l && nz && last_len == 0) ok = false;  // (an empty fragment only first)
+    if (l) {
+      if (!nz) {
+        start = h + hs;
+        first = q;
+      }
+      ++nz;
+    }
+    total += l;
+    last_len = l;
+    prev_end = h + hs + l;
+    if (t0 == 1 || tq == 4) break;
+    if ((prev_end & (kLogBlock - 1)) != 0) ok = false;  // a First / Middle fills its block
+    if (!ok) break;
+  }
+  const bool multi = nz > 1;
+  if (multi && (total <= 240 || last_len < 64)) ok = false;
+  if (total > 0xffffffffull) ok = false;
+  // (the fused kernel loads whole 16-byte chunks up to the record end)
+  if (total > 240 && prev_end + 32 > a.log_len) ok = false;
+  if (!ok) return;
+  if (nz == 0) start = it_off[i] + hs;
+  c.head[i] = 1;
+  c.p0[i] = start;
+  c.len[i] = static_cast<uint32_t>(total);
+  c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
+  c.first[i] = static_cast<uint32_t>(first);
+  c.last[i] = static_cast<uint32_t>(q);
+  if (total <= 240) return;  // short records: the rows kernel's CRC
+  // E / Z of every non-empty fragment (xxh3.hip, the fused CRC)
+  uint32_t b = 0;
+  for (uint64_t r = first; r <= q; ++r) {
+    const uint32_t l = ipack[r] & 0xffffu;
+    if (l == 0) continue;  // (an empty trailing fragment: the rows kernel's CRC)
+    const uint32_t H = crc_header_state(a.log + it_off[r], hs);
+    const uint32_t e = b + l;
+    const uint32_t ws = b >> 10, we = (e - 1) >> 10;
+    const uint32_t E = crc_shift_bytes(H, 1024u * (ws + 1) - b);
+    const uint32_t Z = crc_shift_bytes(~crc_stored[r], 1024u * (we + 1) - e);
+    c.ez[r] = static_cast<uint64_t>(E) | (static_cast<uint64_t>(Z) << 32);
+    c.fused[r] = 1;
+    b = e;
+  }
+}
+
+// compact lists: candidates (item order) and the physical records the rows
+// kernel CRCs (not fused)
+__global__ void __launch_bounds__(kLanes) rw_cand_flags_kernel(const Cand c, uint64_t ni,
+                                                               const uint8_t* it_old,
+                                                               uint64_t* fc, uint64_t* fr) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= ni) return;
+  fc[i] = c.head[i];
+  fr[i] = c.fused[i] || it_old[i] ? 0u : 1u;  // (skipped old records need no CRC)
+}
+
+__global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint64_t ni,
+                                                              const uint8_t* it_old,
+                                                              const uint64_t* cpos,
+                                                              const uint64_t* rpos,
+                                                              const uint64_t* crc_off,
+                                                              const uint32_t* crc_len,
+                                                              uint64_t* l_p0, uint32_t* l_len,
+                                                              uint32_t* l_info, uint32_t* l_first,
+                                                              uint64_t* r_off, uint32_t* r_len,
+                                                              uint64_t* r_item) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= ni) return;
+  if (c.head[i]) {
+    const uint64_t k = cpos[i];
+    l_p0[k] = c.p0[i];
+    l_len[k] = c.len[i];
+    l_info[k] = c.info[i];
+    l_first[k] = c.first[i];
+  }
+  if (!c.fused[i] && !it_old[i]) {
+    const uint64_t k = rpos[i];
+    r_off[k] = crc_off[i];
+    r_len[k] = crc_len[i];
+    r_item[k] = i;
+  }
+}
+
+// the rows kernel's CRCs -> the verdicts of the non-fused records
+__global__ void __launch_bounds__(kLanes) rw_raw_ok_kernel(const uint64_t* r_item,
+                                                           const uint32_t* computed, uint64_t nr,
+                                                           const uint32_t* crc_stored,
+                                                           uint8_t* crc_ok) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (k >= nr) return;
+  const uint64_t i = r_item[k];
+  crc_ok[i] = computed[k] == crc_stored[i] ? 1 : 0;
+}
+
 // ---- per block: CRC truncation, reader position, stop -------------------------
 // acc[b] = items consumed before the first CRC mismatch (a stopping pseudo
 // record included); the event becomes kEvChecksum at a mismatch, kEvPseudo
@@ -232,7 +408,7 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
                                                           const uint32_t* crc_len,
                                                           const uint32_t* crc_stored,
                                                           const uint32_t* ipack,
-                                                          const uint32_t* computed, uint32_t* ev,
+                                                          const uint8_t* crc_ok, uint32_t* ev,
                                                           uint32_t* ev_pos, uint64_t* acc,
                                                           uint64_t* rp_end,
                                                           unsigned long long* first_stop,
@@ -252,7 +428,7 @@ __global__ void __launch_bounds__(kLanes) rw_block_kernel(RecoverArgs a, const u
       last_end = it_off[i0 + k] + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr) + (pk & 0xffffu);
       continue;
     }
-    if (crc_stored[i0 + k] != computed[i0 + k]) {
+    if (!crc_ok[i0 + k]) {
       e = kEvChecksum;
       ep = static_cast<uint32_t>(crc_off[i0 + k] - 6 - start);
       break;
@@ -696,6 +872,51 @@ struct RecFrags {
   }
 };
 
+// an emitted record that is exactly a candidate takes the fused kernel's hash;
+// need[j] = 1 for the others (hashed by hash_logical_records)
+__global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const uint64_t* hb,
+                                                          const uint64_t* lt, uint64_t nr,
+                                                          const Cand c, const uint64_t* cpos,
+                                                          const uint64_t* cand_hash,
+                                                          uint64_t* hash_out, uint64_t* need) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (j >= nr) return;
+  const uint64_t i = lt[j];
+  const uint64_t h = t.kind[i] == kTkFull ? i : f.seg_head[f.seg[i]];
+  bool m = c.head != nullptr && hb[j] == h && (t.kind[h] == kTkFull || t.kind[h] == kTkFirst);
+  if (m) {
+    const uint64_t ih = t.item[h];
+    m = c.head[ih] && c.last[ih] == t.item[i];
+    if (m) hash_out[j] = cand_hash[cpos[ih]];
+  }
+  need[j] = m ? 0u : 1u;
+}
+
+__global__ void __launch_bounds__(kLanes) rw_need_list_kernel(const uint64_t* need,
+                                                              const uint64_t* npos, uint64_t nr,
+                                                              uint64_t* sub) {
+  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (j < nr && need[j]) sub[npos[j]] = j;
+}
+
+__global__ void __launch_bounds__(kLanes) rw_scatter_kernel(const uint64_t* sub, const uint64_t* h,
+                                                            uint64_t n, uint64_t* out) {
+  const uint64_t k = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (k < n) out[sub[k]] = h[k];
+}
+
+// RecFrags over a sub-list of the records (the ones no candidate covers)
+struct RecFragsSub {
+  RecFrags r;
+  const uint64_t* sub;
+  __device__ uint64_t begin(uint64_t j) const { return r.begin(sub[j]); }
+  __device__ uint64_t end(uint64_t j) const { return r.end(sub[j]); }
+  __device__ uint64_t header(uint64_t q) const { return r.header(q); }
+  __device__ uint32_t hs(uint64_t q) const { return r.hs(q); }
+  __device__ uint32_t len(uint64_t q) const { return r.len(q); }
+  __device__ bool use(uint64_t q) const { return r.use(q); }
+};
+
 __global__ void rw_recycled_kernel(RecoverArgs a, uint32_t* flag) {
   // Reader::recycled_: the first header of the file has a recyclable type
   // (log_reader.cc:480-483)
@@ -745,6 +966,11 @@ struct P2 {
   uint64_t *it_off, *crc_off;
   uint8_t* it_old;
   uint32_t *crc_len, *crc_stored, *ipack, *computed;
+  // candidates (fused CRC + XXH3) and the rows kernel's list
+  uint8_t* crc_ok;
+  Cand c;
+  uint64_t *fc, *fr, *cpos, *rpos, *l_p0, *cand_hash, *r_off, *r_item;
+  uint32_t *l_len, *l_info, *l_first, *r_len;
   Tokens t;
   uint64_t *ntok, *tok_base, *head, *plen, *pl, *seg, *seg_head, *n_emit, *n_rep, *emit_at, *rep_at,
       *tiles2, *ctl_list;
@@ -758,6 +984,27 @@ struct P2 {
     crc_stored = A.take<uint32_t>(ni);
     ipack = A.take<uint32_t>(ni);
     computed = A.take<uint32_t>(ni);
+    crc_ok = A.take<uint8_t>(ni);
+    c.head = A.take<uint8_t>(ni);
+    c.fused = A.take<uint8_t>(ni);
+    c.ez = A.take<uint64_t>(ni);
+    c.p0 = A.take<uint64_t>(ni);
+    c.len = A.take<uint32_t>(ni);
+    c.info = A.take<uint32_t>(ni);
+    c.first = A.take<uint32_t>(ni);
+    c.last = A.take<uint32_t>(ni);
+    fc = A.take<uint64_t>(ni);
+    fr = A.take<uint64_t>(ni);
+    cpos = A.take<uint64_t>(ni);
+    rpos = A.take<uint64_t>(ni);
+    l_p0 = A.take<uint64_t>(ni);
+    cand_hash = A.take<uint64_t>(ni);
+    r_off = A.take<uint64_t>(ni);
+    r_item = A.take<uint64_t>(ni);
+    l_len = A.take<uint32_t>(ni);
+    l_info = A.take<uint32_t>(ni);
+    l_first = A.take<uint32_t>(ni);
+    r_len = A.take<uint32_t>(ni);
     t.kind = A.take<uint8_t>(nt);
     t.item = A.take<uint64_t>(nt);
     t.len = A.take<uint32_t>(nt);
@@ -855,7 +1102,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
                               uint64_t rep_cap, forst_wal_recover_result* res, hipStream_t st,
                               const char** name) {
   std::memset(res, 0, sizeof(*res));
-  RecoverArgs a{log, log_len, (log_len + kLogBlock - 1) / kLogBlock, log_number, mode};
+  RecoverArgs a{log, log_len, (log_len + kLogBlock - 1) / kLogBlock, log_number, mode, 0};
   const uint64_t nb = a.n_blocks;
   *name = "rw_walk";
   hipError_t e;
@@ -892,6 +1139,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   // phase 2: items, CRCs, block truncation, tokens, state machine; sized by
   // the same sequence of takes that lays the arrays out
   const uint64_t ni = n_items, nt_max = n_items + nb + 1;
+  a.fuse = log_len >= 4096 && ni < 0xffffffffull ? 1 : 0;
   P2 q;
   Arena M2{nullptr, 0};
   q.take(M2, ni, nb, nt_max);
@@ -900,22 +1148,62 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   Arena A{static_cast<uint8_t*>(s2), 0};
   q.take(A, ni, nb, nt_max);
   const Tokens& t = q.t;
+  uint64_t n_cand = 0;
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q.it_off,
                        q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q1.ev, q1.ev_pos);
     if (ni) {
-      BlockArgs cb{};
-      cb.base = log;
-      cb.base_len = log_len;
-      cb.offsets = q.crc_off;
-      cb.sizes = q.crc_len;
-      cb.out32 = q.computed;
-      cb.n = ni;
-      const char* crc_name = nullptr;
-      if ((e = launch_crc32c_blocks(kModeRaw, cb, st, &crc_name)) != hipSuccess) return fail(e);
+      // candidates: the records a writer lays out, CRC'd and hashed by ONE
+      // read of their bytes (the fused kernel); the other physical records
+      // go to the rows kernel's CRC (sync: the two list sizes)
+      hipLaunchKernelGGL(rw_cand_kernel, grid_for(ni), dim3(kLanes), 0, st, a, ni, q.it_off,
+                         q.it_old, q.ipack, q.crc_stored, q.c);
+      hipLaunchKernelGGL(rw_cand_flags_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni,
+                         q.it_old, q.fc, q.fr);
+      const uint64_t nti = (ni + kScanTile - 1) / kScanTile;
+      uint64_t cnt2[2] = {0, 0};
+      scan_u64(q.fc, ni, q.tiles2, q.cpos, st);
+      e = hipMemcpyAsync(&cnt2[0], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      if (e == hipSuccess) e = hipStreamSynchronize(st);
+      if (e != hipSuccess) return fail(e);
+      n_cand = cnt2[0];
+      const uint64_t n_raw = cnt2[1];
+      hipLaunchKernelGGL(rw_cand_list_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni, q.it_old,
+                         q.cpos, q.rpos, q.crc_off, q.crc_len, q.l_p0, q.l_len, q.l_info,
+                         q.l_first, q.r_off, q.r_len, q.r_item);
+      if (n_cand) {
+        BlockArgs fa{};
+        fa.base = log;
+        fa.base_len = log_len;
+        fa.offsets = q.l_p0;
+        fa.sizes = q.l_len;
+        fa.init_crcs = q.l_info;
+        fa.modifiers = q.l_first;
+        fa.crc_ez = q.c.ez;
+        fa.crc_ok = q.crc_ok;
+        fa.out64 = q.cand_hash;
+        fa.n = n_cand;
+        const char* fname = nullptr;
+        if ((e = launch_xxh3_frag_crc(fa, st, &fname)) != hipSuccess) return fail(e);
+      }
+      if (n_raw) {
+        BlockArgs cb{};
+        cb.base = log;
+        cb.base_len = log_len;
+        cb.offsets = q.r_off;
+        cb.sizes = q.r_len;
+        cb.out32 = q.computed;
+        cb.n = n_raw;
+        const char* crc_name = nullptr;
+        if ((e = launch_crc32c_blocks(kModeRaw, cb, st, &crc_name)) != hipSuccess) return fail(e);
+        hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_raw), dim3(kLanes), 0, st, q.r_item,
+                           q.computed, n_raw, q.crc_stored, q.crc_ok);
+      }
     }
     hipLaunchKernelGGL(rw_block_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.cnt, q1.ibase,
-                       q.it_off, q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q.computed,
+                       q.it_off, q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q.crc_ok,
                        q1.ev, q1.ev_pos, q1.acc, q1.rp_end, q1.first_stop, q1.recycled);
   }
   hipLaunchKernelGGL(rw_ntok_kernel, grid_for(nb + 1), dim3(kLanes), 0, st, a, q1.acc, q1.ev,
@@ -1072,9 +1360,38 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
                      nullptr, q.emit_at, q.rep_at, cr, full, nr, reps, rep_cap, hash_begin,
                      last_tok);
   if (nr) {
-    const RecFrags rf{hash_begin, last_tok, t.kind, t.item, q.it_off, q.ipack, q.seg, q.live,
-                      q.seg_fl};
-    e = hash_logical_records(log, log_len, rf, nr, full.hash, st, name);
+    // records that are exactly a candidate already have their hash (the
+    // fused kernel); the rest are hashed here (sync: how many)
+    void* s5 = nullptr;
+    if ((e = alloc(up256(8 * nr) * 4 + up256(8 * (nr / kScanTile + 2)), &s5)) != hipSuccess)
+      return fail(e);
+    Arena A5{static_cast<uint8_t*>(s5), 0};
+    uint64_t* need = A5.take<uint64_t>(nr);
+    uint64_t* npos = A5.take<uint64_t>(nr);
+    uint64_t* sub = A5.take<uint64_t>(nr);
+    uint64_t* hsub = A5.take<uint64_t>(nr);
+    uint64_t* tiles5 = A5.take<uint64_t>(nr / kScanTile + 2);
+    Cand cm = q.c;
+    if (!n_cand) cm.head = nullptr;
+    hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,
+                       last_tok, nr, cm, q.cpos, q.cand_hash, full.hash, need);
+    scan_u64(need, nr, tiles5, npos, st);
+    uint64_t n_need = 0;
+    if ((e = hipMemcpyAsync(&n_need, tiles5 + (nr + kScanTile - 1) / kScanTile, 8,
+                            hipMemcpyDeviceToHost, st)) != hipSuccess ||
+        (e = hipStreamSynchronize(st)) != hipSuccess)
+      return fail(e);
+    if (n_need) {
+      hipLaunchKernelGGL(rw_need_list_kernel, grid_for(nr), dim3(kLanes), 0, st, need, npos, nr,
+                         sub);
+      const RecFrags rf{hash_begin, last_tok, t.kind, t.item, q.it_off, q.ipack, q.seg, q.live,
+                        q.seg_fl};
+      const RecFragsSub rs{rf, sub};
+      e = hash_logical_records(log, log_len, rs, n_need, hsub, st, name);
+      if (e == hipSuccess)
+        hipLaunchKernelGGL(rw_scatter_kernel, grid_for(n_need), dim3(kLanes), 0, st, sub, hsub,
+                           n_need, full.hash);
+    }
   }
   // copy the (capacity-limited) record list out
   const uint64_t nc = nr < rec_cap ? nr : rec_cap;

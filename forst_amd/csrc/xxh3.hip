@@ -13,6 +13,8 @@
 #include <cstdlib>
 #include <string>
 
+#include "crc32c_tables.h"
+#include "crc_lds.h"
 #include "device_common.h"
 #include "engine.h"
 #include "stream_common.h"
@@ -35,6 +37,12 @@ constexpr uint32_t kXxWgChunk = 8;
 constexpr bool kFragWg = false;
 constexpr uint32_t kFragWaves = kWaves;
 constexpr uint32_t kFragThreads = kFragWaves * 64;
+// ... with the fused physical-record CRC (WAL recovery): 124 KiB of CRC
+// tables in LDS, so one 12-wave workgroup per CU
+constexpr uint32_t kFragCrcWaves = 8;
+constexpr uint32_t kFragCrcThreads = kFragCrcWaves * 64;
+constexpr uint32_t kFcOffA16 = 65536;                  // A16[1..15], 4 KiB each
+constexpr uint32_t kFcLds = kFcOffA16 + 15 * 4096;     // 124 KiB
 
 __device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
   h ^= h >> 33;
@@ -955,6 +963,7 @@ constexpr uint32_t kNoBound = 0xffffffffu;
 
 struct FRow {
   uint32_t off_lo, off_hi, size, rel, g;
+  uint32_t item;  // (fused CRC) the physical record of the first non-empty fragment
   uint32_t info;  // hs | j_last << 8
   uint32_t jc;    // fragment of the window start
   uint32_t bn;    // next boundary (logical offset), kNoBound
@@ -968,6 +977,7 @@ struct FStep {
   uint32_t x[4][5];
   uint32_t l[5];
   uint32_t alt[5];
+  uint32_t ez[4];  // (fused CRC) E, Z of the window's fragment and of the next one
   uint32_t fm;  // m0..m3 (2 bits each) | has_alt:1 @8 | kk:2 @9 | cut:4 @11 | m_alt:2 @15
 };
 
@@ -988,6 +998,7 @@ __device__ __forceinline__ void frow_next(FRow& P) {  // window g -> g + 1
   }
 }
 
+template <bool CRC>
 __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, const FRow& P,
                                            FStep& d) {
   const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
@@ -1014,11 +1025,17 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t dA = ((static_cast<uint32_t>(B) + hs) & ~3u) - (static_cast<uint32_t>(B) & ~3u);
   const uint8_t* R = a.base + (B & ~3ull);
   const uint32_t lim = P.g < nb ? 4u : (nbS > s4 ? (nbS - s4 + 3) >> 2 : 0u);  // chunks k < lim
+  // (fused CRC) the last window's chunks up to the record end, past the
+  // stripes XXH3 accumulates (its last stripe is loaded apart): a chunk
+  // starting before the end is loaded whole (the candidate kernel keeps
+  // records that end within 32 bytes of the log end out of this kernel)
+  const uint32_t crem = CRC && P.g == nb ? P.size - wpos : 0u;
+  auto needk = [&](uint32_t k) { return lng && (k < lim || lof + 256 * k < crem); };
   uint32_t fm = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
     const bool past = static_cast<int32_t>(256 * k) >= dl;
-    const bool need = lng && k < lim;
+    const bool need = needk(k);
     const uint8_t* q = R + (256 * k + (past ? dA : 0u));
     const uint32_t m = past ? m1 : m0;
     const uint8_t* pq = need ? q : a.base;
@@ -1041,7 +1058,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   // the one chunk of the lane that straddles the boundary (0 < dl - 256k < 16)
   // takes the bytes past it from the shifted frame: the same chunk hs on
   const uint32_t ks = static_cast<uint32_t>(dl) >> 8, cut = static_cast<uint32_t>(dl) & 255u;
-  const bool straddle = lng && dl > 0 && dl < 1024 && cut != 0 && cut < 16 && ks < lim;
+  const bool straddle = dl > 0 && dl < 1024 && cut != 0 && cut < 16 && needk(ks);
   const uint8_t* qa = straddle ? R + (256 * ks + dA) : a.base;
   const u32x4a4 av = ld16_a4(qa);
   d.alt[0] = av.x;
@@ -1063,23 +1080,79 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   d.l[2] = lv.z;
   d.l[3] = lv.w;
   d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
+  if (CRC) {  // E, Z of the window's fragment jc and of jc + 1 (its last: jc again)
+    const uint64_t i0 = lng ? static_cast<uint64_t>(P.item) + P.jc : 0;
+    const uint64_t i1 = lng && P.jc < (P.info >> 8) ? i0 + 1 : i0;
+    const uint64_t e0 = a.crc_ez[i0], e1 = a.crc_ez[i1];
+    d.ez[0] = static_cast<uint32_t>(e0);
+    d.ez[1] = static_cast<uint32_t>(e0 >> 32);
+    d.ez[2] = static_cast<uint32_t>(e1);
+    d.ez[3] = static_cast<uint32_t>(e1 >> 32);
+  }
 }
 
 // WPE: waves per SIMD the register allocation targets (3, the default: 168
 // VGPRs with a few spilled dwords, C5 a14 21.5 vs 24.8 ms at 2: 181 VGPRs)
-template <int WPE>
-__global__ void __launch_bounds__(kFragThreads) FORST_WAVES_PER_EU(WPE)
+// the fused CRC's tables: [0, 64K) G and J244 replicated (crc_lds.h),
+// [64K, 124K) A16[1..15]; constant trip counts (see fill_tables3)
+template <uint32_t NT>
+__device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
+  const uint32_t tid = threadIdx.x;
+  constexpr uint32_t kN1 = (16384 + NT - 1) / NT, kN2 = (15 * 1024 + NT - 1) / NT;
+  uint32_t v1[kN1], v2[kN2];
+#pragma unroll
+  for (uint32_t k = 0; k < kN1; ++k) {
+    const uint32_t i = tid + k * NT;
+    const uint32_t e = (i >> 6) & 255, d = i & 63, t = (d >> 3) & 3;
+    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e] : kCrcJ244[t * 256 + e]) : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kN2; ++k) {
+    const uint32_t i = tid + k * NT;
+    v2[k] = i < 15 * 1024 ? kCrcA16[i] : 0u;
+  }
+#pragma unroll
+  for (uint32_t k = 0; k < kN1; ++k)
+    if (tid + k * NT < 16384) L[tid + k * NT] = v1[k];
+#pragma unroll
+  for (uint32_t k = 0; k < kN2; ++k)
+    if (tid + k * NT < 15 * 1024) L[kFcOffA16 / 4 + tid + k * NT] = v2[k];
+}
+
+// CRC = true (fused WAL recovery, wal_recover.hip): besides the XXH3 of every
+// logical record, the CRC32C of each of its physical records (fragments) is
+// checked from the same loads.  CRC32C is linear: a fragment's CRC over
+// header[6..hs) || payload is H * x^(8|p|) + raw(payload) (H = the state after
+// the header bytes from ~0), and raw(payload) is the XOR of every payload
+// chunk's contribution moved to a common end.  Lane t of a row holds the 16 B
+// chunks at window offsets 16t + 256k; its chain runs over them (J244: the
+// 240-byte hop between chunks fused with the first dword step), so at the end
+// of chunk 3 it sits 16 (15 - t) bytes before the window end; a fragment that
+// ends in the window is finished by moving every lane there (A16[15 - t]),
+// XOR-reducing the row, and comparing with Z = ~stored * x^(8m) (m = bytes
+// from the fragment end to the window end).  Bytes outside the fragment are
+// masked to zero.  H enters as E = H * x^(8 (window end - fragment start)),
+// added at the end of the fragment's first window (into lane 15's chain, which
+// ends at the window end).  E and Z per physical record come from the caller
+// (rw_cand_kernel); the verdict goes to crc_ok[physical record].  A window
+// holding a fragment boundary runs a second pass for the next fragment.
+template <int WPE, bool CRC>
+__global__ void __launch_bounds__(CRC ? kFragCrcThreads : kFragThreads) FORST_WAVES_PER_EU(WPE)
 xxh3_frag_kernel(BlockArgs a) {
   // cold per-pair constants and the accumulate keys live in LDS (registers
   // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
   __shared__ uint64_t cold[4 * kColdN];
   __shared__ uint64_t keys[24];
   __shared__ uint64_t shsec[64];
+  __shared__ uint32_t crcL[CRC ? kFcLds / 4 : 1];
+  constexpr uint32_t FW = CRC ? kFragCrcWaves : kFragWaves;
   if (kFragWg) feed_init();
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   if (threadIdx.x < 24) keys[threadIdx.x] = sec64(8 * threadIdx.x);
   short_secrets_fill(shsec, threadIdx.x);
+  if constexpr (CRC) fill_frag_crc_tables<kFragCrcThreads>(crcL);
   __syncthreads();
+  const uint8_t* Lb = reinterpret_cast<const uint8_t*>(crcL);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
@@ -1087,8 +1160,8 @@ xxh3_frag_kernel(BlockArgs a) {
   // K0[k] = keys[s4 + 2p + 4k], K1[k] = keys[s4 + 2p + 4k + 1]
   // (the scramble keys sec64(128 + 16p), sec64(136 + 16p) are keys[16 + 2p],
   // keys[17 + 2p], read where used: one spilled register pair fewer)
-  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kFragWaves;
-  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kFragWaves + wave;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * FW;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * FW + wave;
   BatchFeed feed;
   uint64_t cg = feed_first<kFragWg, 64>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
@@ -1098,7 +1171,7 @@ xxh3_frag_kernel(BlockArgs a) {
   DescBatch cb, nb;
   uint64_t kbrel = 0;
   load_batch<kModeRaw>(a, cg, a.n, lane, cb);  // extra = frag_info (init_crcs)
-  load_batch<kModeRaw>(a, ng, a.n, lane, nb);
+  load_batch<kModeRaw>(a, ng, a.n, lane, nb);  // mod = first physical record (fused CRC)
   auto fetch = [&](uint64_t rel, FRow& P) {
     const BatchSlot q = batch_slot(rel, kbrel, cg, clen, ng, nlen, a.n);
     const uint32_t lo_c = __shfl(cb.off_lo, q.src), hi_c = __shfl(cb.off_hi, q.src);
@@ -1109,6 +1182,12 @@ xxh3_frag_kernel(BlockArgs a) {
     P.off_hi = q.in_n ? hi_n : hi_c;
     P.size = q.in_n ? sz_n : sz_c;
     P.info = q.in_n ? in_nn : in_c;
+    if (CRC) {
+      const uint32_t it_c = __shfl(cb.mod, q.src), it_n = __shfl(nb.mod, q.src);
+      P.item = q.in_n ? it_n : it_c;
+    } else {
+      P.item = 0;
+    }
     P.rel = q.valid ? static_cast<uint32_t>(q.gi) : kNoMsg;
     frow_start(P);
   };
@@ -1150,15 +1229,17 @@ xxh3_frag_kernel(BlockArgs a) {
   FRow I;
   advance(C, I);
   FStep X, Y;
-  frag_issue(a, lane, C, X);
+  frag_issue<CRC>(a, lane, C, X);
   uint64_t acc0 = 0, acc1 = 0;
+  uint32_t crc_s = 0;  // (fused CRC) the lane's chain state
+  const fcrc::Lanes FK = fcrc::lanes(lane);
   auto step = [&](FStep& cu, FStep& nx) -> bool {
     // no early return: both step copies issue on every path round the loop,
     // so the compiler's waits at the loop head see the other copy's loads as
     // the younger ones (an exit path between the copies made them wait out
     // the step in flight before issuing the next)
     const bool live = __ballot(C.rel != kNoMsg) != 0;
-    frag_issue(a, lane, I, nx);
+    frag_issue<CRC>(a, lane, I, nx);
 #ifndef FORST_HOST_EMULATION
     // keep the next step's loads here, ahead of this step's compute (without
     // the fence they are sunk below the step's conditional code, and the
@@ -1213,6 +1294,15 @@ xxh3_frag_kernel(BlockArgs a) {
     asm volatile("" : "+v"(kix));
 #endif
     const uint64_t* kq = keys + kix;
+    // (fused CRC) this window's bytes of fragment jc: [0, hiA)
+    const bool crow = CRC && lng;
+    uint32_t hiA = 1024u;
+    if (CRC) {
+      const uint32_t fe = C.bn < C.size ? C.bn : C.size;
+      const uint32_t W0 = 1024u * C.g;
+      hiA = fe - W0 < 1024u ? fe - W0 : 1024u;
+    }
+    uint32_t cs = crc_s;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       uint64_t d0, d1;
@@ -1222,6 +1312,63 @@ xxh3_frag_kernel(BlockArgs a) {
       const bool use = C.g < nbC || s4 + 4 * k < nbSC;
       sum0 += use ? c0 : 0ull;
       sum1 += use ? c1 : 0ull;
+      if (CRC) {
+        const uint32_t q = 16 * t + 256 * k;
+        uint64_t m0 = ~0ull, m1 = ~0ull;
+        if (hiA < q + 16) fcrc::keep_mask(0, hiA > q ? hiA - q : 0u, m0, m1);
+        const uint64_t e0 = d0 & m0, e1 = d1 & m1;
+        cs = fcrc::chunk_step(Lb, FK, cs, static_cast<uint32_t>(e0), static_cast<uint32_t>(e0 >> 32),
+                              static_cast<uint32_t>(e1), static_cast<uint32_t>(e1 >> 32));
+      }
+    }
+    if (CRC) {
+      // the fragment's end in this window: finish it (and a fragment that
+      // starts here: second pass); else carry the chain, E added at the end
+      // of the fragment's first window
+      const uint32_t W0 = 1024u * C.g, L = C.size;
+      const uint32_t fe = C.bn < L ? C.bn : L;
+      const bool ends = crow && fe - W0 <= 1024u;
+      const uint32_t l0 = kWalBlock - static_cast<uint32_t>(C.off() & (kWalBlock - 1));
+      const uint32_t fs = C.jc == 0 ? 0u : l0 + (C.jc - 1) * (kWalBlock - C.hs());
+      const bool started = (fs >> 10) == C.g;
+      uint32_t ns = (crow && !ends) ? (cs ^ (started && t == 15 ? cu.ez[0] : 0u)) : 0u;
+      auto row_value = [&](uint32_t v) {  // lane chains -> the row's value at the window end
+        v = t == 15 ? v : fcrc::shift_at(Lb, kFcOffA16 + 4096 * (14 - t), v);
+        v = fcrc::row_ror_xor<1>(v);
+        v = fcrc::row_ror_xor<2>(v);
+        v = fcrc::row_ror_xor<4>(v);
+        return fcrc::row_ror_xor<8>(v);
+      };
+      if (__ballot(ends)) {
+        const uint32_t V = row_value(cs) ^ (started ? cu.ez[0] : 0u);
+        if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
+        const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
+        if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
+          const uint32_t B = C.bn - W0;
+          const uint32_t hiB = L - W0 < 1024u ? L - W0 : 1024u;
+          uint32_t sb = 0;
+#pragma unroll
+          for (uint32_t k = 0; k < 4; ++k) {
+            uint64_t d0, d1;
+            xx_words(cu.x[k], (fm >> (2 * k)) & 3u, d0, d1);
+            const uint32_t q = 16 * t + 256 * k;
+            const uint32_t ka = B > q ? (B - q < 16u ? B - q : 16u) : 0u;
+            const uint32_t kb = hiB > q ? (hiB - q < 16u ? hiB - q : 16u) : 0u;
+            uint64_t m0, m1;
+            fcrc::keep_mask(ka, kb > ka ? kb : ka, m0, m1);
+            const uint64_t e0 = d0 & m0, e1 = d1 & m1;
+            sb = fcrc::chunk_step(Lb, FK, sb, static_cast<uint32_t>(e0),
+                                  static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
+                                  static_cast<uint32_t>(e1 >> 32));
+          }
+          const bool endsB = pb && L - W0 <= 1024u;
+          const uint32_t VB = row_value(sb) ^ cu.ez[2];
+          if (endsB && t == 0)
+            a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = VB == cu.ez[3] ? 1 : 0;
+          if (pb && !endsB) ns = sb ^ (t == 15 ? cu.ez[2] : 0u);
+        }
+      }
+      crc_s = ns;
     }
     sum0 += row_ror64<4>(sum0);
     sum1 += row_ror64<4>(sum1);
@@ -1265,6 +1412,7 @@ xxh3_frag_kernel(BlockArgs a) {
     // without a full vmcnt(0) wait on the step in flight
     asm volatile("" ::"v"(cu.l[0]), "v"(cu.l[1]), "v"(cu.l[2]), "v"(cu.l[3]), "v"(cu.l[4]),
                  "v"(cu.alt[0]), "v"(cu.alt[1]), "v"(cu.alt[2]), "v"(cu.alt[3]), "v"(cu.alt[4]));
+    if (CRC) asm volatile("" ::"v"(cu.ez[0]), "v"(cu.ez[1]), "v"(cu.ez[2]), "v"(cu.ez[3]));
 #endif
     C = I;
     advance(C, I);
@@ -1466,12 +1614,13 @@ hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const
 
 }  // namespace
 
-template <int WPE>
+template <int WPE, bool CRC>
 uint32_t frag_occupancy() {
   static const uint32_t occ = [] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE>, kFragThreads, 0) !=
-            hipSuccess ||
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE, CRC>,
+                                                     CRC ? kFragCrcThreads : kFragThreads,
+                                                     0) != hipSuccess ||
         o < 1)
       o = 1;
     return static_cast<uint32_t>(o);
@@ -1479,17 +1628,19 @@ uint32_t frag_occupancy() {
   return occ;
 }
 
-template <int WPE>
+template <int WPE, bool CRC>
 hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name) {
   const DeviceInfo& di = device_info();
+  constexpr uint32_t FW = CRC ? kFragCrcWaves : kFragWaves;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
-      1, std::min<uint64_t>((a.n + 4 * kFragWaves - 1) / (4 * kFragWaves),
-                            uint64_t(di.num_cus) * frag_occupancy<WPE>())));
+      1, std::min<uint64_t>((a.n + 4 * FW - 1) / (4 * FW),
+                            uint64_t(di.num_cus) * frag_occupancy<WPE, CRC>())));
   BlockArgs b = a;
-  hipError_t e = feed_setup(b, uint64_t(grid) * kFragWaves, stream);
+  hipError_t e = feed_setup(b, uint64_t(grid) * FW, stream);
   if (e != hipSuccess) return e;
-  *name = WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
-  hipLaunchKernelGGL(xxh3_frag_kernel<WPE>, dim3(grid), dim3(kFragThreads), 0, stream, b);
+  *name = CRC ? "xxh3_frag_kernel<3, crc>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
+  hipLaunchKernelGGL((xxh3_frag_kernel<WPE, CRC>), dim3(grid),
+                     dim3(CRC ? kFragCrcThreads : kFragThreads), 0, stream, b);
   e = hipGetLastError();
   const hipError_t f = scratch_free(b.ticket, stream);
   return e != hipSuccess ? e : f;
@@ -1499,9 +1650,17 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
   if (a.n == 0) return hipSuccess;
   if (a.n >= 0xffffffffull || a.base_len < 4096 || !a.init_crcs) return hipErrorInvalidValue;
 #ifdef FORST_DIAG
-  if (std::string(diag_env("FORST_FRAG_WPE")) == "2") return launch_frag<2>(a, stream, name);
+  if (std::string(diag_env("FORST_FRAG_WPE")) == "2") return launch_frag<2, false>(a, stream, name);
 #endif
-  return launch_frag<3>(a, stream, name);
+  return launch_frag<3, false>(a, stream, name);
+}
+
+hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const char** name) {
+  if (a.n == 0) return hipSuccess;
+  if (a.n >= 0xffffffffull || a.base_len < 4096 || !a.init_crcs || !a.modifiers || !a.crc_ez ||
+      !a.crc_ok)
+    return hipErrorInvalidValue;
+  return launch_frag<2, true>(a, stream, name);
 }
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,

@@ -987,7 +987,7 @@ struct P2 {
     crc_ok = A.take<uint8_t>(ni);
     c.head = A.take<uint8_t>(ni);
     c.fused = A.take<uint8_t>(ni);
-    c.ez = A.take<uint64_t>(ni);
+    c.ez = A.take<uint64_t>(ni + 1);  // (+1: the fused kernel loads entries i, i + 1)
     c.p0 = A.take<uint64_t>(ni);
     c.len = A.take<uint32_t>(ni);
     c.info = A.take<uint32_t>(ni);

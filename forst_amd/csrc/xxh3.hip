@@ -42,7 +42,8 @@ constexpr uint32_t kFragThreads = kFragWaves * 64;
 constexpr uint32_t kFragCrcWaves = 8;
 constexpr uint32_t kFragCrcThreads = kFragCrcWaves * 64;
 constexpr uint32_t kFcOffA16 = 65536;                  // A16[1..15], 4 KiB each
-constexpr uint32_t kFcLds = kFcOffA16 + 15 * 4096;     // 124 KiB
+constexpr uint32_t kFcOffC256 = kFcOffA16 + 15 * 4096;  // C256[1..3], 4 KiB each
+constexpr uint32_t kFcLds = kFcOffC256 + 3 * 4096;     // 136 KiB
 
 __device__ __forceinline__ uint64_t xxh64_avalanche(uint64_t h) {
   h ^= h >> 33;
@@ -1031,6 +1032,13 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   // records that end within 32 bytes of the log end out of this kernel)
   const uint32_t crem = CRC && P.g == nb ? P.size - wpos : 0u;
   auto needk = [&](uint32_t k) { return lng && (k < lim || lof + 256 * k < crem); };
+  // The dword after a needed chunk (for unaligned starts) is loaded whatever
+  // the alignment: it starts before the record end (a full window ends before
+  // the last byte; a last-window chunk of the fused CRC ends at most 15 bytes
+  // past it, and those records end >= 32 bytes before the log end), so it
+  // lies in a mapped page.  The short-record, boundary and last-stripe
+  // addresses are worked out only in steps where some row needs them (the
+  // loads themselves stay unconditional, so every step issues the same loads).
   uint32_t fm = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
@@ -1039,13 +1047,16 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
     const uint8_t* q = R + (256 * k + (past ? dA : 0u));
     const uint32_t m = past ? m1 : m0;
     const uint8_t* pq = need ? q : a.base;
-    const uint8_t* pq4 = need && m ? q + 16 : pq;
+    const uint8_t* pq4 = pq + 16;
     uint32_t mm = need ? m : 0u;
-    if (k == 0) {  // a short record's chunk (xxh3_short_row)
+    if (k == 0 && __ballot(shrt)) {  // a short record's chunk (xxh3_short_row)
       const uint64_t sp = short_phys(P0, P.size, t);
-      pq = shrt ? a.base + (sp & ~3ull) : pq;
-      mm = shrt ? static_cast<uint32_t>(sp) & 3u : mm;
-      pq4 = shrt && mm ? pq + 16 : (shrt ? pq : pq4);
+      const uint32_t ms = static_cast<uint32_t>(sp) & 3u;
+      if (shrt) {
+        pq = a.base + (sp & ~3ull);
+        mm = ms;
+        pq4 = ms ? pq + 16 : pq;  // (the chunk may end at the log end)
+      }
     }
     const u32x4a4 v = ld16_a4(pq);
     d.x[k][0] = v.x;
@@ -1057,66 +1068,78 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   }
   // the one chunk of the lane that straddles the boundary (0 < dl - 256k < 16)
   // takes the bytes past it from the shifted frame: the same chunk hs on
-  const uint32_t ks = static_cast<uint32_t>(dl) >> 8, cut = static_cast<uint32_t>(dl) & 255u;
-  const bool straddle = dl > 0 && dl < 1024 && cut != 0 && cut < 16 && needk(ks);
-  const uint8_t* qa = straddle ? R + (256 * ks + dA) : a.base;
+  const uint8_t* qa = a.base;
+  if (__ballot(lng && dw < 1024u)) {  // a boundary in some row's window
+    const uint32_t ks = static_cast<uint32_t>(dl) >> 8, cut = static_cast<uint32_t>(dl) & 255u;
+    const bool straddle = dl > 0 && dl < 1024 && cut != 0 && cut < 16 && needk(ks);
+    if (straddle) {
+      qa = R + (256 * ks + dA);
+      fm |= (1u << 8) | (ks << 9) | (cut << 11) | (m1 << 15);
+    }
+  }
   const u32x4a4 av = ld16_a4(qa);
   d.alt[0] = av.x;
   d.alt[1] = av.y;
   d.alt[2] = av.z;
   d.alt[3] = av.w;
-  d.alt[4] = ld4_a4(straddle && m1 ? qa + 16 : qa);
-  if (straddle) fm |= (1u << 8) | (ks << 9) | (cut << 11) | (m1 << 15);
+  d.alt[4] = ld4_a4(qa + 16);
   d.fm = fm;
   // last stripe at L - 64, inside the last fragment (fragment j_last); loaded
-  // in every step (at 0 when not needed: see rows_issue)
+  // in every step (from the buffer start when not needed: see rows_issue)
   const bool lastp = lng && P.g == nb;
-  const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
-  const uint64_t lo = lastp ? (lq & ~3ull) : 0;
-  const uint32_t ml = static_cast<uint32_t>(lq & 3);
-  const u32x4a4 lv = ld16_a4(a.base + lo);
+  const uint8_t* lq0 = a.base;
+  const uint8_t* lq4 = a.base;
+  if (__ballot(lastp)) {
+    const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+    if (lastp) {
+      lq0 = a.base + (lq & ~3ull);
+      lq4 = (lq & 3) ? lq0 + 16 : lq0;  // (the stripe ends at the record end)
+    }
+  }
+  const u32x4a4 lv = ld16_a4(lq0);
   d.l[0] = lv.x;
   d.l[1] = lv.y;
   d.l[2] = lv.z;
   d.l[3] = lv.w;
-  d.l[4] = ld4_a4(a.base + (lastp && ml ? lo + 16 : lo));
-  if (CRC) {  // E, Z of the window's fragment jc and of jc + 1 (its last: jc again)
+  d.l[4] = ld4_a4(lq4);
+  if (CRC) {  // E, Z of the window's fragment jc and of jc + 1 (one 16-byte
+              // load: crc_ez holds one entry more than there are items)
     const uint64_t i0 = lng ? static_cast<uint64_t>(P.item) + P.jc : 0;
-    const uint64_t i1 = lng && P.jc < (P.info >> 8) ? i0 + 1 : i0;
-    const uint64_t e0 = a.crc_ez[i0], e1 = a.crc_ez[i1];
-    d.ez[0] = static_cast<uint32_t>(e0);
-    d.ez[1] = static_cast<uint32_t>(e0 >> 32);
-    d.ez[2] = static_cast<uint32_t>(e1);
-    d.ez[3] = static_cast<uint32_t>(e1 >> 32);
+    const u32x4a4 ez = ld16_a4(reinterpret_cast<const uint8_t*>(a.crc_ez + i0));
+    d.ez[0] = ez.x;
+    d.ez[1] = ez.y;
+    d.ez[2] = ez.z;
+    d.ez[3] = ez.w;
   }
 }
 
 // WPE: waves per SIMD the register allocation targets (3, the default: 168
 // VGPRs with a few spilled dwords, C5 a14 21.5 vs 24.8 ms at 2: 181 VGPRs)
-// the fused CRC's tables: [0, 64K) G and J244 replicated (crc_lds.h),
-// [64K, 124K) A16[1..15]; constant trip counts (see fill_tables3)
+// the fused CRC's tables: [0, 64K) G and J1012 replicated (crc_lds.h),
+// [64K, 124K) A16[1..15], [124K, 136K) C256[1..3]; constant trip counts (see
+// fill_tables3)
 template <uint32_t NT>
 __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
   const uint32_t tid = threadIdx.x;
-  constexpr uint32_t kN1 = (16384 + NT - 1) / NT, kN2 = (15 * 1024 + NT - 1) / NT;
+  constexpr uint32_t kN1 = (16384 + NT - 1) / NT, kN2 = (18 * 1024 + NT - 1) / NT;
   uint32_t v1[kN1], v2[kN2];
 #pragma unroll
   for (uint32_t k = 0; k < kN1; ++k) {
     const uint32_t i = tid + k * NT;
     const uint32_t e = (i >> 6) & 255, d = i & 63, t = (d >> 3) & 3;
-    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e] : kCrcJ244[t * 256 + e]) : 0u;
+    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e] : kCrcJ1012[t * 256 + e]) : 0u;
   }
 #pragma unroll
   for (uint32_t k = 0; k < kN2; ++k) {
     const uint32_t i = tid + k * NT;
-    v2[k] = i < 15 * 1024 ? kCrcA16[i] : 0u;
+    v2[k] = i < 15 * 1024 ? kCrcA16[i] : (i < 18 * 1024 ? kCrcC256[i - 15 * 1024] : 0u);
   }
 #pragma unroll
   for (uint32_t k = 0; k < kN1; ++k)
     if (tid + k * NT < 16384) L[tid + k * NT] = v1[k];
 #pragma unroll
   for (uint32_t k = 0; k < kN2; ++k)
-    if (tid + k * NT < 15 * 1024) L[kFcOffA16 / 4 + tid + k * NT] = v2[k];
+    if (tid + k * NT < 18 * 1024) L[kFcOffA16 / 4 + tid + k * NT] = v2[k];
 }
 
 // CRC = true (fused WAL recovery, wal_recover.hip): besides the XXH3 of every
@@ -1125,15 +1148,18 @@ __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
 // header[6..hs) || payload is H * x^(8|p|) + raw(payload) (H = the state after
 // the header bytes from ~0), and raw(payload) is the XOR of every payload
 // chunk's contribution moved to a common end.  Lane t of a row holds the 16 B
-// chunks at window offsets 16t + 256k; its chain runs over them (J244: the
-// 240-byte hop between chunks fused with the first dword step), so at the end
-// of chunk 3 it sits 16 (15 - t) bytes before the window end; a fragment that
-// ends in the window is finished by moving every lane there (A16[15 - t]),
-// XOR-reducing the row, and comparing with Z = ~stored * x^(8m) (m = bytes
+// chunks at window offsets 16t + 256k and runs one chain per column k over
+// the windows (J1012: the 1008-byte hop to the column's next chunk fused with
+// the first dword step; four independent chains, so the LDS lookups of one
+// step form four short dependency chains, not one 16 deep); after the window
+// column k sits 16 (15 - t) + 256 (3 - k) bytes before the window end.  A
+// fragment that ends in the window is finished by moving the columns onto
+// column 3 (C256), every lane to the window end (A16[15 - t]), XOR-reducing
+// the row, and comparing with Z = ~stored * x^(8m) (m = bytes
 // from the fragment end to the window end).  Bytes outside the fragment are
 // masked to zero.  H enters as E = H * x^(8 (window end - fragment start)),
-// added at the end of the fragment's first window (into lane 15's chain, which
-// ends at the window end).  E and Z per physical record come from the caller
+// added at the end of the fragment's first window (into lane 15's column-3
+// chain, which ends at the window end).  E and Z per physical record come from the caller
 // (rw_cand_kernel); the verdict goes to crc_ok[physical record].  A window
 // holding a fragment boundary runs a second pass for the next fragment.
 template <int WPE, bool CRC>
@@ -1231,7 +1257,7 @@ xxh3_frag_kernel(BlockArgs a) {
   FStep X, Y;
   frag_issue<CRC>(a, lane, C, X);
   uint64_t acc0 = 0, acc1 = 0;
-  uint32_t crc_s = 0;  // (fused CRC) the lane's chain state
+  uint32_t crc_s[4] = {0u, 0u, 0u, 0u};  // (fused CRC) the lane's column chains
   const fcrc::Lanes FK = fcrc::lanes(lane);
   auto step = [&](FStep& cu, FStep& nx) -> bool {
     // no early return: both step copies issue on every path round the loop,
@@ -1302,7 +1328,7 @@ xxh3_frag_kernel(BlockArgs a) {
       const uint32_t W0 = 1024u * C.g;
       hiA = fe - W0 < 1024u ? fe - W0 : 1024u;
     }
-    uint32_t cs = crc_s;
+    uint32_t cs[4] = {crc_s[0], crc_s[1], crc_s[2], crc_s[3]};
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       uint64_t d0, d1;
@@ -1317,8 +1343,9 @@ xxh3_frag_kernel(BlockArgs a) {
         uint64_t m0 = ~0ull, m1 = ~0ull;
         if (hiA < q + 16) fcrc::keep_mask(0, hiA > q ? hiA - q : 0u, m0, m1);
         const uint64_t e0 = d0 & m0, e1 = d1 & m1;
-        cs = fcrc::chunk_step(Lb, FK, cs, static_cast<uint32_t>(e0), static_cast<uint32_t>(e0 >> 32),
-                              static_cast<uint32_t>(e1), static_cast<uint32_t>(e1 >> 32));
+        cs[k] = fcrc::chunk_step(Lb, FK, cs[k], static_cast<uint32_t>(e0),
+                                 static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
+                                 static_cast<uint32_t>(e1 >> 32));
       }
     }
     if (CRC) {
@@ -1331,8 +1358,15 @@ xxh3_frag_kernel(BlockArgs a) {
       const uint32_t l0 = kWalBlock - static_cast<uint32_t>(C.off() & (kWalBlock - 1));
       const uint32_t fs = C.jc == 0 ? 0u : l0 + (C.jc - 1) * (kWalBlock - C.hs());
       const bool started = (fs >> 10) == C.g;
-      uint32_t ns = (crow && !ends) ? (cs ^ (started && t == 15 ? cu.ez[0] : 0u)) : 0u;
-      auto row_value = [&](uint32_t v) {  // lane chains -> the row's value at the window end
+      const bool carry = crow && !ends;
+      uint32_t ns[4];
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) ns[k] = carry ? cs[k] : 0u;
+      if (carry && started && t == 15) ns[3] ^= cu.ez[0];
+      auto row_value = [&](const uint32_t (&c)[4]) {  // columns -> the row's value at the window end
+        uint32_t v = c[3] ^ fcrc::shift_at(Lb, kFcOffC256, c[2]) ^
+                     fcrc::shift_at(Lb, kFcOffC256 + 4096, c[1]) ^
+                     fcrc::shift_at(Lb, kFcOffC256 + 8192, c[0]);
         v = t == 15 ? v : fcrc::shift_at(Lb, kFcOffA16 + 4096 * (14 - t), v);
         v = fcrc::row_ror_xor<1>(v);
         v = fcrc::row_ror_xor<2>(v);
@@ -1346,7 +1380,7 @@ xxh3_frag_kernel(BlockArgs a) {
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
           const uint32_t B = C.bn - W0;
           const uint32_t hiB = L - W0 < 1024u ? L - W0 : 1024u;
-          uint32_t sb = 0;
+          uint32_t sb[4] = {0u, 0u, 0u, 0u};
 #pragma unroll
           for (uint32_t k = 0; k < 4; ++k) {
             uint64_t d0, d1;
@@ -1357,18 +1391,23 @@ xxh3_frag_kernel(BlockArgs a) {
             uint64_t m0, m1;
             fcrc::keep_mask(ka, kb > ka ? kb : ka, m0, m1);
             const uint64_t e0 = d0 & m0, e1 = d1 & m1;
-            sb = fcrc::chunk_step(Lb, FK, sb, static_cast<uint32_t>(e0),
-                                  static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
-                                  static_cast<uint32_t>(e1 >> 32));
+            sb[k] = fcrc::chunk_step(Lb, FK, sb[k], static_cast<uint32_t>(e0),
+                                     static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
+                                     static_cast<uint32_t>(e1 >> 32));
           }
           const bool endsB = pb && L - W0 <= 1024u;
           const uint32_t VB = row_value(sb) ^ cu.ez[2];
           if (endsB && t == 0)
             a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = VB == cu.ez[3] ? 1 : 0;
-          if (pb && !endsB) ns = sb ^ (t == 15 ? cu.ez[2] : 0u);
+          if (pb && !endsB) {
+#pragma unroll
+            for (uint32_t k = 0; k < 4; ++k) ns[k] = sb[k];
+            if (t == 15) ns[3] ^= cu.ez[2];
+          }
         }
       }
-      crc_s = ns;
+#pragma unroll
+      for (uint32_t k = 0; k < 4; ++k) crc_s[k] = ns[k];
     }
     sum0 += row_ror64<4>(sum0);
     sum1 += row_ror64<4>(sum1);
@@ -1638,7 +1677,7 @@ hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name
   BlockArgs b = a;
   hipError_t e = feed_setup(b, uint64_t(grid) * FW, stream);
   if (e != hipSuccess) return e;
-  *name = CRC ? "xxh3_frag_kernel<3, crc>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
+  *name = CRC ? "xxh3_frag_kernel<2, crc>" : WPE == 4 ? "xxh3_frag_kernel<4>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
   hipLaunchKernelGGL((xxh3_frag_kernel<WPE, CRC>), dim3(grid),
                      dim3(CRC ? kFragCrcThreads : kFragThreads), 0, stream, b);
   e = hipGetLastError();
@@ -1652,7 +1691,10 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
 #ifdef FORST_DIAG
   if (std::string(diag_env("FORST_FRAG_WPE")) == "2") return launch_frag<2, false>(a, stream, name);
 #endif
-  return launch_frag<3, false>(a, stream, name);
+#ifndef FORST_FRAG_WPE_DEF
+#define FORST_FRAG_WPE_DEF 3
+#endif
+  return launch_frag<FORST_FRAG_WPE_DEF, false>(a, stream, name);
 }
 
 hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const char** name) {

@@ -17,6 +17,12 @@ enum BlockMode : int {
   kModeRaw = 3,      // crc32c::Extend(init, data, len) / XXH3_64bits
 };
 
+// The fragment XXH3 kernel (xxh3.hip xxh3_frag_kernel) loads whole windows
+// of a long record: records whose last byte lies within kFragTail bytes of
+// the log end are hashed from a gathered copy instead (wal_hash.h, and the
+// fused recovery's candidates, wal_recover.hip)
+constexpr uint64_t kFragTail = 1088;
+
 struct BlockArgs {
   const uint8_t* base;
   uint8_t* base_w;          // same buffer, writable (trailer mode)

@@ -182,8 +182,8 @@ __device__ uint64_t wave_xxph3_long(const uint8_t* p, uint32_t len, uint64_t see
   }
   // XXPH3_mergeAccs from secret + 11 (xxph3.h:1554-1582)
   uint64_t t = mul128_fold64(acc0 ^ psec64(11 + 16 * pp, seed), acc1 ^ psec64(19 + 16 * pp, seed));
-  t += shfl_xor64(t, 1);
-  t += shfl_xor64(t, 2);
+  t += quad_xor64<1>(t);
+  t += quad_xor64<2>(t);
   return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
 }
 

@@ -39,7 +39,8 @@ constexpr uint32_t kWhLanes = 256;
 // for the frag kernel, or glen = len when it must be gathered (its frag
 // descriptor then has length 0)
 template <class F>
-__global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F f, uint64_t n,
+__global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, uint64_t log_len,
+                                                           F f, uint64_t n,
                                                            uint64_t* p0, uint32_t* len,
                                                            uint32_t* info, uint64_t* glen) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
@@ -69,6 +70,9 @@ __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, F
   const bool multi = nz > 1;
   if (multi && (total <= 240 || last_len < 64)) regular = false;
   if (total > 0xffffffffull) regular = false;
+  // the frag kernel loads whole 1 KiB windows, and 32 bytes from a short
+  // record's chunk (engine.h kFragTail)
+  if (prev_end + kFragTail > log_len) regular = false;
   if (nz == 0) start = e > b && f.use(b) ? f.header(b) + f.hs(b) : 0;
   p0[j] = start;
   len[j] = regular ? static_cast<uint32_t>(total) : 0u;
@@ -168,7 +172,8 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
   uint32_t* blen = reinterpret_cast<uint32_t*>(p + 8 * s8 + 2 * s4);
   uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4);
   uint64_t* tiles2 = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4 + st8);
-  hipLaunchKernelGGL(wh_prep_kernel<F>, wh_grid(n), dim3(kWhLanes), 0, st, log, f, n, p0, len,
+  hipLaunchKernelGGL(wh_prep_kernel<F>, wh_grid(n), dim3(kWhLanes), 0, st, log, log_len, f, n,
+                     p0, len,
                      info, glen);
   scan_u64(glen, n, tiles, goff, st);
   hipLaunchKernelGGL(wh_flag_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, n, boff);

@@ -318,8 +318,9 @@ __global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t
   const bool multi = nz > 1;
   if (multi && (total <= 240 || last_len < 64)) ok = false;
   if (total > 0xffffffffull) ok = false;
-  // (the fused kernel loads whole 16-byte chunks up to the record end)
-  if (total > 240 && prev_end + 32 > a.log_len) ok = false;
+  // (the fused kernel loads whole 1 KiB windows, and 32 bytes from a short
+  // record's chunk: engine.h kFragTail)
+  if (prev_end + kFragTail > a.log_len) ok = false;
   if (!ok) return;
   if (nz == 0) start = it_off[i] + hs;
   c.head[i] = 1;
@@ -328,7 +329,9 @@ __global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t
   c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
   c.first[i] = static_cast<uint32_t>(first);
   c.last[i] = static_cast<uint32_t>(q);
+#ifndef FORST_SHORT_CRC_FUSED
   if (total <= 240) return;  // short records: the rows kernel's CRC
+#endif
   // E / Z of every non-empty fragment (xxh3.hip, the fused CRC)
   uint32_t b = 0;
   for (uint64_t r = first; r <= q; ++r) {

@@ -314,8 +314,8 @@ __device__ uint64_t wave_xxh3_64(const uint8_t* p, uint32_t len, uint32_t lane,
   }
   // XXH3_mergeAccs (xxhash.h:5164)
   uint64_t t = mul128_fold64(acc0 ^ K.km0, acc1 ^ K.km1);
-  t += shfl_xor64(t, 1);
-  t += shfl_xor64(t, 2);
+  t += quad_xor64<1>(t);
+  t += quad_xor64<2>(t);
   return xxh3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
 }
 
@@ -571,8 +571,8 @@ __device__ __forceinline__ void xxh3_stream_body(const BlockArgs& a) {
       acc0 += mul32to64(d0 ^ ck[kColdL0]) + d1;
       acc1 += d0 + mul32to64(d1 ^ ck[kColdL1]);
       uint64_t t = mul128_fold64(acc0 ^ ck[kColdM0], acc1 ^ ck[kColdM1]);  // mergeAccs
-      t += shfl_xor64(t, 1);
-      t += shfl_xor64(t, 2);
+      t += quad_xor64<1>(t);
+      t += quad_xor64<2>(t);
       h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + t);
     }
     uint32_t lastb = 0, stored = 0;
@@ -882,8 +882,8 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
         const uint64_t a0 = acc0 + mul32to64(d0 ^ ck[kColdL0]) + d1;
         const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ ck[kColdL1]);
         uint64_t tm = mul128_fold64(a0 ^ ck[kColdM0], a1 ^ ck[kColdM1]);
-        tm += shfl_xor64(tm, 1);
-        tm += shfl_xor64(tm, 2);
+        tm += quad_xor64<1>(tm);
+        tm += quad_xor64<2>(tm);
         h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
       }
       const uint64_t E = off + C.size;
@@ -975,11 +975,15 @@ struct FRow {
 };
 
 struct FStep {
+  // chunk k's 16 bytes in x[k][0..3]; x[k][4] (the dword after them, for the
+  // realignment) is loaded for k = 3 only and made in the step for k < 3:
+  // lane t's next dword is lane t+1's first (lane 15: lane 0's next chunk)
   uint32_t x[4][5];
-  uint32_t l[5];
-  uint32_t alt[5];
+  uint32_t aux[5];  // the row's last stripe (one quad), or the straddling chunk's own frame
   uint32_t ez[4];  // (fused CRC) E, Z of the window's fragment and of the next one
-  uint32_t fm;  // m0..m3 (2 bits each) | has_alt:1 @8 | kk:2 @9 | cut:4 @11 | m_alt:2 @15
+  // m0..m3 (2 bits each) | straddle:1 @8 | ks:2 @9 | cut:5 @11 (1..16) |
+  // m_own:2 @16 | last-stripe quad:1 @18 (0: lanes 0-3, 1: lanes 4-7)
+  uint32_t fm;
 };
 
 __device__ __forceinline__ void frow_start(FRow& P) {
@@ -1006,17 +1010,15 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint64_t P0 = P.off();
   const bool valid = P.rel != kNoMsg && P0 <= a.base_len;
   const bool lng = valid && P.size > 240;
-  const uint32_t nb = (P.size - 1) >> 10, nbS = ((P.size - 1) & 1023) >> 6;
+  const uint32_t nb = (P.size - 1) >> 10;
   const uint32_t hs = P.hs();
   const bool shrt = valid && !lng;  // one fragment (wal_hash.h gathers the others)
-  // Chunk k of the lane sits at window offset lof + 256k, logical offset
-  // wpos + lof + 256k; it lies past the window's boundary (hs bytes further on)
-  // iff 256k >= dl.  bn >= wpos always (frow_next), so dl fits in 32 bits.  All
-  // chunks share two physical frames: B (before the boundary) and B + hs;
-  // their dword-aligned starts differ by dA, so every load address is the
-  // lane's frame pointer R plus a small 32-bit offset (no per-chunk 64-bit
-  // multiply-add), and a chunk that is not needed loads from the buffer start.
-  const uint32_t lof = 64 * s4 + 16 * p;
+  // Chunk k of lane t sits at window offset 16 t + 256 k, logical offset
+  // wpos + 16 t + 256 k.  All chunks of a lane share two physical frames: B
+  // (before the window's fragment boundary) and B + hs (past it); their
+  // dword-aligned starts differ by dA.  bn >= wpos always (frow_next), so dl
+  // (the boundary's offset from the lane's chunk 0) fits in 32 bits.
+  const uint32_t lof = 16 * t;
   const uint32_t wpos = 1024u * P.g;
   const uint32_t dw = P.bn - wpos;
   const int32_t dl = static_cast<int32_t>(dw < 2048u ? dw : 2048u) - static_cast<int32_t>(lof);
@@ -1024,38 +1026,35 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t m0 = static_cast<uint32_t>(B) & 3u;
   const uint32_t m1 = (static_cast<uint32_t>(B) + hs) & 3u;
   const uint32_t dA = ((static_cast<uint32_t>(B) + hs) & ~3u) - (static_cast<uint32_t>(B) & ~3u);
-  const uint8_t* R = a.base + (B & ~3ull);
-  const uint32_t lim = P.g < nb ? 4u : (nbS > s4 ? (nbS - s4 + 3) >> 2 : 0u);  // chunks k < lim
-  // (fused CRC) the last window's chunks up to the record end, past the
-  // stripes XXH3 accumulates (its last stripe is loaded apart): a chunk
-  // starting before the end is loaded whole (the candidate kernel keeps
-  // records that end within 32 bytes of the log end out of this kernel)
-  const uint32_t crem = CRC && P.g == nb ? P.size - wpos : 0u;
-  auto needk = [&](uint32_t k) { return lng && (k < lim || lof + 256 * k < crem); };
-  // The dword after a needed chunk (for unaligned starts) is loaded whatever
-  // the alignment: it starts before the record end (a full window ends before
-  // the last byte; a last-window chunk of the fused CRC ends at most 15 bytes
-  // past it, and those records end >= 32 bytes before the log end), so it
-  // lies in a mapped page.  The short-record, boundary and last-stripe
-  // addresses are worked out only in steps where some row needs them (the
-  // loads themselves stay unconditional, so every step issues the same loads).
+  // Every chunk of a long record's window is loaded, needed or not: the
+  // callers (wh_prep_kernel, rw_cand_kernel) keep records that end within
+  // kFragTail bytes of the log end out of this kernel, so a window's 1 KiB
+  // (plus the header hole and the realignment dwords) past the record end is
+  // in the buffer.  Rows without a record load [0, 1 KiB) of the buffer
+  // (launches need 4 KiB).  A chunk's address is the lane's frame, plus the
+  // hole when the boundary lies at or before the chunk's END (so a chunk
+  // that straddles the boundary, or ends exactly at it, is loaded from the
+  // shifted frame and its own-frame bytes come from the aux load below), with
+  // the chunk's 256 k as the load's immediate offset.  The short-record,
+  // boundary and last-stripe addresses are worked out only in steps where
+  // some row needs them; the loads themselves are unconditional, so every
+  // step issues the same loads (the compiler's vmcnt waits stay precise).
+  const uint8_t* R = a.base + (valid ? (B & ~3ull) : 0ull);
   uint32_t fm = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    const bool past = static_cast<int32_t>(256 * k) >= dl;
-    const bool need = needk(k);
-    const uint8_t* q = R + (256 * k + (past ? dA : 0u));
-    const uint32_t m = past ? m1 : m0;
-    const uint8_t* pq = need ? q : a.base;
-    const uint8_t* pq4 = pq + 16;
-    uint32_t mm = need ? m : 0u;
-    if (k == 0 && __ballot(shrt)) {  // a short record's chunk (xxh3_short_row)
+    const bool past = lng && dl <= static_cast<int32_t>(256 * k + 16);
+    const uint8_t* pq = R + (past ? dA : 0u) + 256 * k;
+    uint32_t mm = past ? m1 : m0;
+    if (k >= 2 && __ballot(shrt)) {
+      // a short record: its window layout in x[0], x[1] (the fused CRC reads
+      // it), its XXH3 chunk (xxh3_short_row) in x[2] and the 16 bytes after
+      // that in x[3], whose first dword realigns it (the record ends >=
+      // kFragTail bytes before the log end)
       const uint64_t sp = short_phys(P0, P.size, t);
-      const uint32_t ms = static_cast<uint32_t>(sp) & 3u;
       if (shrt) {
-        pq = a.base + (sp & ~3ull);
-        mm = ms;
-        pq4 = ms ? pq + 16 : pq;  // (the chunk may end at the log end)
+        pq = a.base + (sp & ~3ull) + 16 * (k - 2);
+        mm = static_cast<uint32_t>(sp) & 3u;
       }
     }
     const u32x4a4 v = ld16_a4(pq);
@@ -1063,48 +1062,51 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
     d.x[k][1] = v.y;
     d.x[k][2] = v.z;
     d.x[k][3] = v.w;
-    d.x[k][4] = ld4_a4(pq4);
+    if (k == 3) d.x[3][4] = ld4_a4(pq + 16);
     fm |= mm << (2 * k);
   }
-  // the one chunk of the lane that straddles the boundary (0 < dl - 256k < 16)
-  // takes the bytes past it from the shifted frame: the same chunk hs on
-  const uint8_t* qa = a.base;
-  if (__ballot(lng && dw < 1024u)) {  // a boundary in some row's window
-    const uint32_t ks = static_cast<uint32_t>(dl) >> 8, cut = static_cast<uint32_t>(dl) & 255u;
-    const bool straddle = dl > 0 && dl < 1024 && cut != 0 && cut < 16 && needk(ks);
-    if (straddle) {
-      qa = R + (256 * ks + dA);
-      fm |= (1u << 8) | (ks << 9) | (cut << 11) | (m1 << 15);
-    }
+  // The chunk that straddles the boundary or ends at it (0 < dl - 256 ks <=
+  // 16): its bytes before the boundary come from its own frame, loaded into
+  // aux with their realignment dword.  (Geometric, not "needed": the lane in
+  // front of it takes its realignment dword from this aux, see the step.)
+  bool straddle = false;
+  uint32_t ks = 0;
+  if (__ballot(lng && dw <= 1024u)) {  // a boundary in, or at the end of, some row's window
+    ks = static_cast<uint32_t>(dl - 1) >> 8;
+    const int32_t cut = dl - static_cast<int32_t>(256 * ks);
+    straddle = lng && dl > 0 && dl <= 784 && cut <= 16;
+    if (straddle) fm |= (1u << 8) | (ks << 9) | (static_cast<uint32_t>(cut) << 11) | (m0 << 16);
   }
-  const u32x4a4 av = ld16_a4(qa);
-  d.alt[0] = av.x;
-  d.alt[1] = av.y;
-  d.alt[2] = av.z;
-  d.alt[3] = av.w;
-  d.alt[4] = ld4_a4(qa + 16);
-  d.fm = fm;
-  // last stripe at L - 64, inside the last fragment (fragment j_last); loaded
-  // in every step (from the buffer start when not needed: see rows_issue)
+  // The last stripe at L - 64, inside the last fragment (fragment j_last):
+  // every quad of the row would compute the same merge, so one quad loads
+  // it -- quad 0, or quad 1 when quad 0 holds the row's straddling chunk --
+  // into the same aux slot (one aux load per step instead of two)
   const bool lastp = lng && P.g == nb;
-  const uint8_t* lq0 = a.base;
-  const uint8_t* lq4 = a.base;
-  if (__ballot(lastp)) {
-    const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
-    if (lastp) {
-      lq0 = a.base + (lq & ~3ull);
-      lq4 = (lq & 3) ? lq0 + 16 : lq0;  // (the stripe ends at the record end)
+  const uint8_t* q0 = a.base;
+  const uint8_t* q4 = a.base;
+  if (__ballot(lastp || straddle)) {
+    const uint32_t rowm = static_cast<uint32_t>(__ballot(straddle) >> (lane & 48u)) & 0xffffu;
+    const uint32_t ql = (rowm & 0xfu) ? 1u : 0u;
+    if (lastp && ql) fm |= 1u << 18;
+    if (straddle) {
+      q0 = R + 256 * ks;
+      q4 = q0 + 16;
+    } else if (lastp && s4 == ql) {
+      const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+      q0 = a.base + (lq & ~3ull);
+      q4 = (lq & 3) ? q0 + 16 : q0;  // (the stripe ends at the record end)
     }
   }
-  const u32x4a4 lv = ld16_a4(lq0);
-  d.l[0] = lv.x;
-  d.l[1] = lv.y;
-  d.l[2] = lv.z;
-  d.l[3] = lv.w;
-  d.l[4] = ld4_a4(lq4);
+  const u32x4a4 av = ld16_a4(q0);
+  d.aux[0] = av.x;
+  d.aux[1] = av.y;
+  d.aux[2] = av.z;
+  d.aux[3] = av.w;
+  d.aux[4] = ld4_a4(q4);
+  d.fm = fm;
   if (CRC) {  // E, Z of the window's fragment jc and of jc + 1 (one 16-byte
               // load: crc_ez holds one entry more than there are items)
-    const uint64_t i0 = lng ? static_cast<uint64_t>(P.item) + P.jc : 0;
+    const uint64_t i0 = valid && P.size > 0 ? static_cast<uint64_t>(P.item) + P.jc : 0;
     const u32x4a4 ez = ld16_a4(reinterpret_cast<const uint8_t*>(a.crc_ez + i0));
     d.ez[0] = ez.x;
     d.ez[1] = ez.y;
@@ -1281,29 +1283,50 @@ xxh3_frag_kernel(BlockArgs a) {
       acc1 = ck[kColdI1];
     }
     uint64_t sum0 = 0, sum1 = 0;
+#ifdef FORST_AB_DBGSHORT
+    uint32_t dbgV = 0;
+#endif
     uint32_t fm = cu.fm;
-    // the slot across the boundary (one lane per row, in ~1 step in 32):
-    // merged once, out of line, into that chunk's words (realigned, m := 0),
-    // so the chunk loop below carries no per-chunk test
+    // realignment dwords of chunks 0..2: lane t's next dword is lane t+1's
+    // first, lane 15's is lane 0's in the next chunk (DPP row_ror 15 reads
+    // lane t+1 of the row); a short row's chunk 0 is followed by its x[1]
+#pragma unroll
+    for (uint32_t k = 0; k < 3; ++k) {
+      const uint32_t nx = __builtin_amdgcn_mov_dpp(cu.x[k][0], 0x12F, 0xf, 0xf, true);
+      const uint32_t nn = __builtin_amdgcn_mov_dpp(cu.x[k + 1][0], 0x12F, 0xf, 0xf, true);
+      cu.x[k][4] = t == 15 ? nn : nx;
+    }
+    if (valid && !lng) cu.x[2][4] = cu.x[3][0];
+    // the chunk across the boundary (one lane per row, in ~1 step in 32):
+    // its bytes before the boundary come from its own frame (aux), the rest
+    // from the shifted frame (x), merged once, out of line, into that chunk's
+    // words (realigned, m := 0), so the chunk loop below carries no
+    // per-chunk test.  The lane in front of it realigns with the aux frame.
     if (__ballot((fm >> 8) & 1u)) {
       uint32_t f2 = fm;
 #ifndef FORST_HOST_EMULATION
       asm volatile("" : "+v"(f2));  // nothing of the merge is hoisted out of the branch
 #endif
+      const uint32_t sk = ((f2 >> 8) & 1u) ? (f2 >> 9) & 3u : 7u;
+      const uint32_t nsk = __builtin_amdgcn_mov_dpp(sk, 0x12F, 0xf, 0xf, true);
+      const uint32_t na0 = __builtin_amdgcn_mov_dpp(cu.aux[0], 0x12F, 0xf, 0xf, true);
+#pragma unroll
+      for (uint32_t k = 0; k < 3; ++k)
+        if (nsk == (t == 15 ? k + 1 : k)) cu.x[k][4] = na0;
       if ((f2 >> 8) & 1u) {
         uint64_t a0, a1;
-        xx_words(cu.alt, (f2 >> 15) & 3u, a0, a1);
-        const uint32_t cut = (f2 >> 11) & 15u;  // bytes before the boundary
+        xx_words(cu.aux, (f2 >> 16) & 3u, a0, a1);
+        const uint32_t cut = (f2 >> 11) & 31u;  // bytes before the boundary, 1..16
         const uint64_t mlo = cut >= 8 ? ~0ull : ((1ull << (8 * cut)) - 1);
-        const uint64_t mhi = cut >= 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull;
+        const uint64_t mhi = cut >= 16 ? ~0ull : (cut > 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull);
         const uint32_t ks = (f2 >> 9) & 3u;
 #pragma unroll
         for (uint32_t k = 0; k < 4; ++k) {
           if (ks == k) {
             uint64_t d0, d1;
             xx_words(cu.x[k], (f2 >> (2 * k)) & 3u, d0, d1);
-            d0 = (d0 & mlo) | (a0 & ~mlo);
-            d1 = (d1 & mhi) | (a1 & ~mhi);
+            d0 = (a0 & mlo) | (d0 & ~mlo);
+            d1 = (a1 & mhi) | (d1 & ~mhi);
             cu.x[k][0] = static_cast<uint32_t>(d0);
             cu.x[k][1] = static_cast<uint32_t>(d0 >> 32);
             cu.x[k][2] = static_cast<uint32_t>(d1);
@@ -1321,7 +1344,13 @@ xxh3_frag_kernel(BlockArgs a) {
 #endif
     const uint64_t* kq = keys + kix;
     // (fused CRC) this window's bytes of fragment jc: [0, hiA)
+    // (short records: their one fragment from the window layout in x[0], x[1];
+    // an empty one is CRC'd by the rows kernel, rw_cand_kernel)
+#ifndef FORST_SHORT_CRC_FUSED
     const bool crow = CRC && lng;
+#else
+    const bool crow = CRC && valid && C.size > 0;
+#endif
     uint32_t hiA = 1024u;
     if (CRC) {
       const uint32_t fe = C.bn < C.size ? C.bn : C.size;
@@ -1376,6 +1405,12 @@ xxh3_frag_kernel(BlockArgs a) {
       if (__ballot(ends)) {
         const uint32_t V = row_value(cs) ^ (started ? cu.ez[0] : 0u);
         if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
+#if defined(FORST_AB_DBGSHORT) || defined(FORST_AB_FORCE)
+        if (ends && t == 0 && !lng) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = 1;
+#endif
+#ifdef FORST_AB_DBGSHORT
+        dbgV = V;
+#endif
         const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
           const uint32_t B = C.bn - W0;
@@ -1426,31 +1461,36 @@ xxh3_frag_kernel(BlockArgs a) {
       {
         uint64_t d0, d1;
         const uint64_t le = C.off() + C.size + static_cast<uint64_t>(C.hs()) * (C.info >> 8);
-        xx_words(cu.l, static_cast<uint32_t>(le & 3), d0, d1);
+        xx_words(cu.aux, static_cast<uint32_t>(le & 3), d0, d1);
         const uint64_t a0 = acc0 + mul32to64(d0 ^ ck[kColdL0]) + d1;
         const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ ck[kColdL1]);
         uint64_t tm = mul128_fold64(a0 ^ ck[kColdM0], a1 ^ ck[kColdM1]);
-        tm += shfl_xor64(tm, 1);
-        tm += shfl_xor64(tm, 2);
+        tm += quad_xor64<1>(tm);
+        tm += quad_xor64<2>(tm);
         h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
       }
       if (__ballot(fin && valid && !lng)) {  // short records: the row's chunks
         uint64_t d0, d1;
-        xx_words(cu.x[0], fm & 3u, d0, d1);
+        xx_words(cu.x[2], (fm >> 4) & 3u, d0, d1);
         const uint64_t P0 = C.off();
         const uint32_t pb = static_cast<uint32_t>(P0 - short_phys(P0, C.size, 0));
         const uint64_t hs2 = xxh3_short_row(d0, d1, C.size, t, pb, shsec);
         if (fin && valid && !lng) h = hs2;
       }
-      if (fin && t == 0 && a.out64) a.out64[C.rel] = valid ? h : 0ull;
+      // (the quad that loaded the last stripe: fm bit 18)
+      if (fin && t == 4 * ((fm >> 18) & 1u) && a.out64) a.out64[C.rel] = valid ? h : 0ull;
+#ifdef FORST_AB_DBGSHORT
+      if (CRC && fin && t == 0 && valid && !lng && C.size > 0 && a.out64)
+        a.out64[C.rel] = (static_cast<uint64_t>(dbgV) << 32) | cu.ez[1];
+#endif
     }
 #ifndef FORST_HOST_EMULATION
     // the last-stripe and boundary words are read only on some paths; a use
     // on every path retires their loads here (a precise wait: the next step's
     // loads are younger), so the registers can be reused in the next step
     // without a full vmcnt(0) wait on the step in flight
-    asm volatile("" ::"v"(cu.l[0]), "v"(cu.l[1]), "v"(cu.l[2]), "v"(cu.l[3]), "v"(cu.l[4]),
-                 "v"(cu.alt[0]), "v"(cu.alt[1]), "v"(cu.alt[2]), "v"(cu.alt[3]), "v"(cu.alt[4]));
+    asm volatile("" ::"v"(cu.aux[0]), "v"(cu.aux[1]), "v"(cu.aux[2]), "v"(cu.aux[3]),
+                 "v"(cu.aux[4]));
     if (CRC) asm volatile("" ::"v"(cu.ez[0]), "v"(cu.ez[1]), "v"(cu.ez[2]), "v"(cu.ez[3]));
 #endif
     C = I;

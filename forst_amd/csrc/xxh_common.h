@@ -56,6 +56,17 @@ __device__ __forceinline__ uint64_t mul32to64(uint64_t v) {
          static_cast<uint64_t>(static_cast<uint32_t>(v >> 32));
 }
 
+// 64-bit values as a register pair: built and split by bit casts, so a 64-bit
+// add of two DPP moves is one v_lshl_add_u64 on the pair (the shift-or form
+// made hipcc add the halves separately through zero-extended temporaries: six
+// instructions per 64-bit DPP add instead of three)
+typedef uint32_t u32x2 __attribute__((ext_vector_type(2)));
+__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
+  u32x2 w;
+  w.x = lo;
+  w.y = hi;
+  return __builtin_bit_cast(uint64_t, w);
+}
 // 16 bytes at an arbitrary address with dword-aligned loads + alignbyte.
 // `m` = address & 3 (wave-uniform), q = address & ~3.
 __device__ __forceinline__ void ld16u(const uint8_t* q, uint32_t m,
@@ -69,8 +80,8 @@ __device__ __forceinline__ void ld16u(const uint8_t* q, uint32_t m,
     x2 = __builtin_amdgcn_alignbyte(x3, x2, m);
     x3 = __builtin_amdgcn_alignbyte(x4, x3, m);
   }
-  d0 = (static_cast<uint64_t>(x1) << 32) | x0;
-  d1 = (static_cast<uint64_t>(x3) << 32) | x2;
+  d0 = mk64(x0, x1);
+  d1 = mk64(x2, x3);
 }
 
 __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
@@ -79,17 +90,24 @@ __device__ __forceinline__ uint64_t shfl_xor64(uint64_t v, int mask) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
-__device__ __forceinline__ uint64_t mk64(uint32_t lo, uint32_t hi) {
-  return (static_cast<uint64_t>(hi) << 32) | lo;
+template <int CTRL>
+__device__ __forceinline__ uint64_t dpp64(uint64_t v) {
+  // every lane reads a live lane: no "old" operand to initialise
+  const u32x2 w = __builtin_bit_cast(u32x2, v);
+  return mk64(__builtin_amdgcn_mov_dpp(w.x, CTRL, 0xf, 0xf, true),
+              __builtin_amdgcn_mov_dpp(w.y, CTRL, 0xf, 0xf, true));
 }
-// DPP row rotate (within 16-lane rows), one VALU op, no LDS traffic
+// DPP row rotate (within 16-lane rows), one VALU op per half, no LDS traffic
 template <int N>
 __device__ __forceinline__ uint64_t row_ror64(uint64_t v) {
-  // every lane reads a live lane of its row: no "old" operand to initialise
-  const uint32_t lo = __builtin_amdgcn_mov_dpp(static_cast<uint32_t>(v), 0x120 + N, 0xf, 0xf, true);
-  const uint32_t hi = __builtin_amdgcn_mov_dpp(static_cast<uint32_t>(v >> 32), 0x120 + N, 0xf, 0xf,
-                                               true);
-  return mk64(lo, hi);
+  return dpp64<0x120 + N>(v);
+}
+// the partner lane of a quad (lane ^ 1: quad_perm [1,0,3,2]; lane ^ 2:
+// [2,3,0,1]) by DPP instead of ds_bpermute
+template <int M>
+__device__ __forceinline__ uint64_t quad_xor64(uint64_t v) {
+  static_assert(M == 1 || M == 2, "quad partner");
+  return dpp64<M == 1 ? 0xB1 : 0x4E>(v);
 }
 
 // sum over the 16 lanes that share L%4 (lane bits 2..5): two DPP row

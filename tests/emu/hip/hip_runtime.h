@@ -164,6 +164,10 @@ inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
 // and row_ror:n (0x121..0x12f; lane i <- lane (i-n) mod 16 of its row)
 inline uint32_t __builtin_amdgcn_update_dpp(uint32_t old, uint32_t src, int ctrl, int, int, bool) {
   const uint32_t lane = emu::tl_tid.x & 63;
+  if (ctrl >= 0 && ctrl < 0x100) {  // quad_perm:[s0,s1,s2,s3] (lane i <- lane sel_{i%4} of its quad)
+    const uint32_t sel = (static_cast<uint32_t>(ctrl) >> (2 * (lane & 3u))) & 3u;
+    return emu::exchange(src, (lane & ~3u) | sel);
+  }
   if (ctrl > 0x110 && ctrl < 0x120) {
     const uint32_t n = static_cast<uint32_t>(ctrl - 0x110);
     const uint32_t v = emu::exchange(src, (lane & 15u) >= n ? lane - n : lane);

@@ -1,0 +1,22 @@
+#!/bin/bash
+# A/B/C... of several builds of the library on one box, alternating processes:
+#   tools/ab_multi.sh <tag> <config> <lib>...   (config C5 = tools/prof_wal.py, A14 = tools/prof_a14.py)
+set -eo pipefail
+cd "${GRAFT_REPO_ROOT:-/root/repo}"
+TAG=$1; c=$2; shift 2
+OUT=gpurun_out/$TAG
+mkdir -p "$OUT"
+for r in 1 2 3; do
+  for L in "$@"; do
+    if [ "$c" = C5 ]; then
+      timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_wal.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
+      tail -1 "$OUT/ab.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C5 $(basename $L)', d['verify_roofline_frac'], d['writer_roofline_frac'], d['record_xxh3_ms'], d['recover_ms'])"
+    elif [ "$c" = A14 ]; then
+      timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_a14.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
+      echo "A14 $(basename $L) $(tail -1 "$OUT/ab.log")"
+    else
+      timeout -k 10 300 python -u tools/with_lib.py $L bench.py --config $c --steps 20 --warmup 3 --no-cpu-baseline --no-extras > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
+      tail -1 "$OUT/ab.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('$c $(basename $L)', d['value'], {k: v['frac'] for k, v in d['kernels'].items()})"
+    fi
+  done
+done

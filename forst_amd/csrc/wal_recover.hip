@@ -329,9 +329,6 @@ __global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t
   c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
   c.first[i] = static_cast<uint32_t>(first);
   c.last[i] = static_cast<uint32_t>(q);
-#ifndef FORST_SHORT_CRC_FUSED
-  if (total <= 240) return;  // short records: the rows kernel's CRC
-#endif
   // E / Z of every non-empty fragment (xxh3.hip, the fused CRC)
   uint32_t b = 0;
   for (uint64_t r = first; r <= q; ++r) {

@@ -1283,9 +1283,6 @@ xxh3_frag_kernel(BlockArgs a) {
       acc1 = ck[kColdI1];
     }
     uint64_t sum0 = 0, sum1 = 0;
-#ifdef FORST_AB_DBGSHORT
-    uint32_t dbgV = 0;
-#endif
     uint32_t fm = cu.fm;
     // realignment dwords of chunks 0..2: lane t's next dword is lane t+1's
     // first, lane 15's is lane 0's in the next chunk (DPP row_ror 15 reads
@@ -1346,11 +1343,7 @@ xxh3_frag_kernel(BlockArgs a) {
     // (fused CRC) this window's bytes of fragment jc: [0, hiA)
     // (short records: their one fragment from the window layout in x[0], x[1];
     // an empty one is CRC'd by the rows kernel, rw_cand_kernel)
-#ifndef FORST_SHORT_CRC_FUSED
-    const bool crow = CRC && lng;
-#else
     const bool crow = CRC && valid && C.size > 0;
-#endif
     uint32_t hiA = 1024u;
     if (CRC) {
       const uint32_t fe = C.bn < C.size ? C.bn : C.size;
@@ -1405,12 +1398,7 @@ xxh3_frag_kernel(BlockArgs a) {
       if (__ballot(ends)) {
         const uint32_t V = row_value(cs) ^ (started ? cu.ez[0] : 0u);
         if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
-#if defined(FORST_AB_DBGSHORT) || defined(FORST_AB_FORCE)
-        if (ends && t == 0 && !lng) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = 1;
-#endif
-#ifdef FORST_AB_DBGSHORT
-        dbgV = V;
-#endif
+
         const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
           const uint32_t B = C.bn - W0;
@@ -1479,10 +1467,7 @@ xxh3_frag_kernel(BlockArgs a) {
       }
       // (the quad that loaded the last stripe: fm bit 18)
       if (fin && t == 4 * ((fm >> 18) & 1u) && a.out64) a.out64[C.rel] = valid ? h : 0ull;
-#ifdef FORST_AB_DBGSHORT
-      if (CRC && fin && t == 0 && valid && !lng && C.size > 0 && a.out64)
-        a.out64[C.rel] = (static_cast<uint64_t>(dbgV) << 32) | cu.ez[1];
-#endif
+
     }
 #ifndef FORST_HOST_EMULATION
     // the last-stripe and boundary words are read only on some paths; a use

@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B/C... of several builds of the library on one box, alternating processes:
-#   tools/ab_multi.sh <tag> <config> <lib>...   (config C5 = tools/prof_wal.py, A14 = tools/prof_a14.py)
+#   tools/ab_multi.sh <tag> <config> <lib>...   (config C5 = tools/prof_wal.py, A14 = tools/prof_a14.py, B:<cfg> = tools/prof_blocks.py <cfg>)
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=$1; c=$2; shift 2
@@ -11,6 +11,9 @@ for r in 1 2 3; do
     if [ "$c" = C5 ]; then
       timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_wal.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
       tail -1 "$OUT/ab.log" | python3 -c "import json,sys; d=json.loads(sys.stdin.read()); print('C5 $(basename $L)', d['verify_roofline_frac'], d['writer_roofline_frac'], d['record_xxh3_ms'], d['recover_ms'])"
+    elif [ "${c#B:}" != "$c" ]; then
+      timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_blocks.py ${c#B:} > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
+      echo "$c $(basename $L) $(tail -1 "$OUT/ab.log")"
     elif [ "$c" = A14 ]; then
       timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_a14.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
       echo "A14 $(basename $L) $(tail -1 "$OUT/ab.log")"

@@ -135,12 +135,12 @@ __device__ __forceinline__ bool pseudo_stops(uint32_t ty, bool eofb, uint32_t re
 
 // ---- walk -------------------------------------------------------------------
 // items: header offsets of the physical records the reader parses in block b
-// (REC: CRC to check; OLD: skipped old record, kSkipAnyCorruptedRecords)
-template <bool FILL>
+// (REC: CRC to check; OLD: skipped old record, kSkipAnyCorruptedRecords);
+// emit(n, header offset, old, unmasked stored CRC, packed length | type << 16
+// | recyclable << 24) for each
+template <class Emit>
 __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev, uint32_t* ev_pos,
-                                  uint64_t base, uint64_t* it_off, uint8_t* it_old,
-                                  uint64_t* crc_off, uint32_t* crc_len, uint32_t* crc_stored,
-                                  uint32_t* ipack) {
+                                  Emit emit) {
   const uint64_t start = b * kLogBlock;
   const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
   const bool eofb = end - start < kLogBlock;
@@ -165,18 +165,13 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       e = eofb ? kEvBadLenEof : kEvBadLen;
       break;
     }
+    const uint32_t pk = length | (type << 16) | (recyc ? 1u << 24 : 0u);
     if (recyc && ld_le32(h + 7) != a.log_number) {
       if (a.mode != 3) {  // not kSkipAnyCorruptedRecords: reading ends here
         e = kEvOldStop;
         break;
       }
-      if (FILL) {
-        it_off[base + n] = pos;
-        it_old[base + n] = 1;
-        crc_off[base + n] = 0;
-        crc_len[base + n] = 0;
-        ipack[base + n] = length | (type << 16) | (recyc ? 1u << 24 : 0u);
-      }
+      emit(n, pos, true, 0u, pk);
       ++n;
       pos += hs + length;
       continue;
@@ -185,14 +180,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       e = kEvZero;
       break;
     }
-    if (FILL) {
-      it_off[base + n] = pos;
-      it_old[base + n] = 0;
-      crc_off[base + n] = pos + 6;
-      crc_len[base + n] = hs + length - 6;
-      crc_stored[base + n] = unmask(ld_le32(h));  // log_reader.cc:522-523
-      ipack[base + n] = length | (type << 16) | (recyc ? 1u << 24 : 0u);
-    }
+    emit(n, pos, false, unmask(ld_le32(h)), pk);  // log_reader.cc:522-523
     ++n;
     pos += hs + length;
   }
@@ -205,19 +193,68 @@ __global__ void __launch_bounds__(kLanes) rw_count_kernel(RecoverArgs a, uint64_
   const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (b >= a.n_blocks) return;
   uint32_t ev, ep;
-  cnt[b] = rw_walk_block<false>(a, b, &ev, &ep, 0, nullptr, nullptr, nullptr, nullptr, nullptr,
-                                nullptr);
+  cnt[b] = rw_walk_block(a, b, &ev, &ep, [](uint32_t, uint64_t, bool, uint32_t, uint32_t) {});
 }
 
+// The items of a workgroup's 256 log blocks are one contiguous run of the
+// per-item arrays: staged in LDS by the lane-per-block walks and stored
+// coalesced (the walks' own stores are one partial line per item and array:
+// 4.5 GB of traffic for C5's 11.4 M items); a run over the cap is stored
+// directly.  crc_off / crc_len follow from the offset and the packed word.
+constexpr uint32_t kRwFillCap = 2560;  // 17 B per item: 42.5 KiB of LDS
 __global__ void __launch_bounds__(kLanes) rw_fill_kernel(RecoverArgs a, const uint64_t* base,
+                                                         const uint64_t* cnt,
                                                          uint64_t* it_off, uint8_t* it_old,
                                                          uint64_t* crc_off, uint32_t* crc_len,
                                                          uint32_t* crc_stored, uint32_t* ipack,
                                                          uint32_t* ev, uint32_t* ev_pos) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (b >= a.n_blocks) return;
-  rw_walk_block<true>(a, b, &ev[b], &ev_pos[b], base[b], it_off, it_old, crc_off, crc_len,
-                      crc_stored, ipack);
+  __shared__ uint64_t l_off[kRwFillCap];
+  __shared__ uint32_t l_st[kRwFillCap], l_pk[kRwFillCap];
+  __shared__ uint8_t l_old[kRwFillCap];
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * kLanes;
+  const uint64_t b = b0 + threadIdx.x;
+  const uint64_t bl = (b0 + kLanes < a.n_blocks ? b0 + kLanes : a.n_blocks) - 1;  // last block
+  const uint64_t wg_base = base[b0];
+  const uint64_t tot = base[bl] + cnt[bl] - wg_base;
+  const bool staged = tot <= kRwFillCap;  // workgroup-uniform
+  if (b < a.n_blocks) {
+    const uint64_t mine = base[b];
+    auto direct = [&](uint32_t n, uint64_t pos, bool old, uint32_t st, uint32_t pk) {
+      const uint64_t i = mine + n;
+      it_off[i] = pos;
+      it_old[i] = old ? 1 : 0;
+      crc_off[i] = old ? 0 : pos + 6;
+      crc_len[i] = old ? 0 : ((pk >> 24) ? kLogRHdr : kLogHdr) + (pk & 0xffffu) - 6;
+      if (!old) crc_stored[i] = st;
+      ipack[i] = pk;
+    };
+    auto stage = [&](uint32_t n, uint64_t pos, bool old, uint32_t st, uint32_t pk) {
+      const uint64_t i = mine - wg_base + n;
+      l_off[i] = pos;
+      l_old[i] = old ? 1 : 0;
+      l_st[i] = st;
+      l_pk[i] = pk;
+    };
+    if (staged)
+      rw_walk_block(a, b, &ev[b], &ev_pos[b], stage);
+    else
+      rw_walk_block(a, b, &ev[b], &ev_pos[b], direct);
+  }
+  if (staged) {
+    __syncthreads();
+    for (uint32_t k = threadIdx.x; k < tot; k += kLanes) {
+      const uint64_t i = wg_base + k;
+      const uint64_t pos = l_off[k];
+      const bool old = l_old[k] != 0;
+      const uint32_t pk = l_pk[k];
+      it_off[i] = pos;
+      it_old[i] = old ? 1 : 0;
+      crc_off[i] = old ? 0 : pos + 6;
+      crc_len[i] = old ? 0 : ((pk >> 24) ? kLogRHdr : kLogHdr) + (pk & 0xffffu) - 6;
+      if (!old) crc_stored[i] = l_st[k];
+      ipack[i] = pk;
+    }
+  }
 }
 
 // ---- candidates: records laid out as log::Writer lays them out ---------------
@@ -502,6 +539,30 @@ __device__ __forceinline__ uint8_t record_kind(uint32_t type, bool eofb, uint32_
   }
 }
 
+// exclusive scan of one value per lane over a kLanes-thread workgroup
+__device__ __forceinline__ uint32_t rw_wg_scan(uint32_t v, uint32_t* sh, uint32_t* total) {
+  const uint32_t t = threadIdx.x;
+  sh[t] = v;
+  __syncthreads();
+  for (uint32_t d = 1; d < kLanes; d <<= 1) {
+    const uint32_t add = t >= d ? sh[t - d] : 0u;
+    __syncthreads();
+    sh[t] += add;
+    __syncthreads();
+  }
+  const uint32_t incl = sh[t];
+  *total = sh[kLanes - 1];
+  __syncthreads();
+  return incl - v;
+}
+
+// One token per consumed physical record and per block event, in reader
+// order.  A workgroup's 256 log blocks own contiguous runs of the item and
+// token arrays; the record tokens are made item-parallel (each lane finds its
+// item's block by a binary search over the workgroup's prefix in LDS, so the
+// item reads and token stores are coalesced), the event tokens by the lane of
+// their block.  A record token's reader position is the end of the item
+// before it in its block (or the position entering the block).
 __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const uint64_t* base,
                                                           const uint64_t* it_off,
                                                           const uint8_t* it_old,
@@ -514,45 +575,66 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
                                                           const uint32_t* recycled_d, Tokens t,
                                                           uint64_t* ctl_list, uint64_t ctl_cap,
                                                           unsigned long long* ctl_n) {
-  const uint64_t b = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (b > a.n_blocks) return;
+  __shared__ uint32_t sh[kLanes];
+  __shared__ uint32_t s_loc[kLanes];
+  const uint64_t b0 = static_cast<uint64_t>(blockIdx.x) * kLanes;
+  const uint64_t b = b0 + threadIdx.x;
   const uint32_t recycled = *recycled_d;
-  uint64_t o = tok_base[b];
-  if (b == a.n_blocks) {
-    if (*first_stop == ~0ull) {  // kEof at the reader position after the last block
-      t.kind[o] = kTkStopEof;
-      t.item[o] = b;
-      t.len[o] = 0;
-      t.pos[o] = b == 0 ? 0 : rp_end[b - 1];
-      t.type[o] = 0;
-    }
-    return;
+  const uint64_t fs = *first_stop;
+  if (b == a.n_blocks && fs == ~0ull) {  // kEof at the reader position after the last block
+    const uint64_t o = tok_base[b];
+    t.kind[o] = kTkStopEof;
+    t.item[o] = b;
+    t.len[o] = 0;
+    t.pos[o] = b == 0 ? 0 : rp_end[b - 1];
+    t.type[o] = 0;
   }
-  if (b > *first_stop) return;
-  const uint64_t start = b * kLogBlock;
-  const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
-  const bool eofb = eof_block(a, b);
-  uint64_t rp = b == 0 ? 0 : rp_end[b - 1];  // reader position entering the block
-  const uint64_t n = acc[b], i0 = base[b];
-  for (uint64_t k = 0; k < n; ++k, ++o) {
-    const uint64_t off = it_off[i0 + k];
-    const uint32_t pk = ipack[i0 + k];  // the fill's header fields (no header re-read)
+  const bool live = b < a.n_blocks && b <= fs;
+  const uint32_t n = live ? static_cast<uint32_t>(acc[b]) : 0u;  // <= items of one 32 KiB block
+  uint32_t tot;
+  const uint32_t loc = rw_wg_scan(n, sh, &tot);
+  s_loc[threadIdx.x] = loc;
+  __syncthreads();
+  for (uint32_t k = threadIdx.x; k < tot; k += kLanes) {
+    uint32_t lo = 0, hi = kLanes;  // the last block j with s_loc[j] <= k
+    while (hi - lo > 1) {
+      const uint32_t mid = (lo + hi) >> 1;
+      if (s_loc[mid] <= k) lo = mid; else hi = mid;
+    }
+    const uint64_t bj = b0 + lo, kk = k - s_loc[lo];
+    const uint64_t i = base[bj] + kk, o = tok_base[bj] + kk;
+    const uint32_t pk = ipack[i];  // the fill's header fields (no header re-read)
     const uint32_t length = pk & 0xffffu;
     const uint32_t type = (pk >> 16) & 0xffu;
-    const uint8_t kind = it_old[i0 + k] ? kTkOldSkip : record_kind(type, eofb, recycled, a.mode);
+    uint64_t rp;
+    if (kk == 0) {
+      rp = bj == 0 ? 0 : rp_end[bj - 1];
+    } else {
+      const uint32_t pp = ipack[i - 1];
+      rp = it_off[i - 1] + ((pp >> 24) & 1u ? kLogRHdr : kLogHdr) + (pp & 0xffffu);
+    }
+    const uint8_t kind = it_old[i] ? kTkOldSkip : record_kind(type, eof_block(a, bj), recycled, a.mode);
     if (kind == kTkCtlComp || kind == kTkCtlTs) {  // decided on the host, in reader order
       const unsigned long long c = atomicAdd(ctl_n, 1ull);
       if (c < ctl_cap) ctl_list[c] = o;
     }
     t.kind[o] = kind;
-    t.item[o] = i0 + k;
+    t.item[o] = i;
     t.len[o] = length;
     t.pos[o] = rp;
     t.type[o] = static_cast<uint8_t>(type);
-    rp = off + ((pk >> 24) & 1u ? kLogRHdr : kLogHdr) + length;
   }
+  if (!live) return;
   const uint32_t e = ev[b];
   if (!event_token(e)) return;
+  const uint64_t start = b * kLogBlock;
+  const uint64_t end = start + kLogBlock < a.log_len ? start + kLogBlock : a.log_len;
+  uint64_t rp = b == 0 ? 0 : rp_end[b - 1];  // reader position after the consumed items
+  if (n) {
+    const uint64_t il = base[b] + n - 1;
+    const uint32_t pp = ipack[il];
+    rp = it_off[il] + ((pp >> 24) & 1u ? kLogRHdr : kLogHdr) + (pp & 0xffffu);
+  }
   const bool recyc_stop = (e == kEvChecksum || e == kEvBadLen) && recycled && a.mode == 0;
   uint8_t kind = e == kEvChecksum   ? kTkChecksum
                  : e == kEvBadLen   ? kTkBadLen
@@ -561,6 +643,7 @@ __global__ void __launch_bounds__(kLanes) rw_token_kernel(RecoverArgs a, const u
                  : e == kEvBadHeader ? kTkStopHeader
                                      : kTkStopBadLenEof;
   if (recyc_stop) kind = kTkStopRecycled;
+  const uint64_t o = tok_base[b] + n;
   t.kind[o] = kind;
   t.item[o] = b;
   t.len[o] = static_cast<uint32_t>(end - (start + ev_pos[b]));  // drop_size: rest of the buffer
@@ -1150,7 +1233,8 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   const Tokens& t = q.t;
   uint64_t n_cand = 0;
   if (nb) {
-    hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q.it_off,
+    hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q1.cnt,
+                       q.it_off,
                        q.it_old, q.crc_off, q.crc_len, q.crc_stored, q.ipack, q1.ev, q1.ev_pos);
     if (ni) {
       // candidates: the records a writer lays out, CRC'd and hashed by ONE

@@ -39,7 +39,10 @@ constexpr uint32_t kFragWaves = kWaves;
 constexpr uint32_t kFragThreads = kFragWaves * 64;
 // ... with the fused physical-record CRC (WAL recovery): 124 KiB of CRC
 // tables in LDS, so one 12-wave workgroup per CU
-constexpr uint32_t kFragCrcWaves = 8;
+#ifndef FORST_FRAG_CRC_WAVES
+#define FORST_FRAG_CRC_WAVES 12
+#endif
+constexpr uint32_t kFragCrcWaves = FORST_FRAG_CRC_WAVES;
 constexpr uint32_t kFragCrcThreads = kFragCrcWaves * 64;
 constexpr uint32_t kFcOffA16 = 65536;                  // A16[1..15], 4 KiB each
 constexpr uint32_t kFcOffC256 = kFcOffA16 + 15 * 4096;  // C256[1..3], 4 KiB each
@@ -1702,7 +1705,7 @@ hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name
   BlockArgs b = a;
   hipError_t e = feed_setup(b, uint64_t(grid) * FW, stream);
   if (e != hipSuccess) return e;
-  *name = CRC ? "xxh3_frag_kernel<2, crc>" : WPE == 4 ? "xxh3_frag_kernel<4>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
+  *name = CRC ? (WPE == 3 ? "xxh3_frag_kernel<3, crc>" : "xxh3_frag_kernel<2, crc>") : WPE == 4 ? "xxh3_frag_kernel<4>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
   hipLaunchKernelGGL((xxh3_frag_kernel<WPE, CRC>), dim3(grid),
                      dim3(CRC ? kFragCrcThreads : kFragThreads), 0, stream, b);
   e = hipGetLastError();
@@ -1727,7 +1730,13 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
   if (a.n >= 0xffffffffull || a.base_len < 4096 || !a.init_crcs || !a.modifiers || !a.crc_ez ||
       !a.crc_ok)
     return hipErrorInvalidValue;
-  return launch_frag<2, true>(a, stream, name);
+// 3 waves per SIMD (one 12-wave workgroup per CU, its 136 KiB of tables):
+// 168 VGPRs with 9 spilled dwords; A/B against 2 waves (8-wave workgroups,
+// 203 VGPRs, no spills): C5 recovery 22.95 -> 21.77 ms
+#ifndef FORST_FRAG_CRC_WPE
+#define FORST_FRAG_CRC_WPE 3
+#endif
+  return launch_frag<FORST_FRAG_CRC_WPE, true>(a, stream, name);
 }
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,

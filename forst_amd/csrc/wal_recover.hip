@@ -287,6 +287,24 @@ __device__ __forceinline__ uint32_t crc_header_state(const uint8_t* h, uint32_t 
   for (uint32_t i = 6; i < hs; ++i) v = (v >> 8) ^ kCrcG[3 * 256 + ((v ^ h[i]) & 0xffu)];
   return v;
 }
+// the same two with the tables in LDS (rw_cand_kernel): S64 / S4 / byte table
+struct ShiftLds {
+  const uint32_t* s64;
+  const uint32_t* s4;
+  const uint32_t* g3;
+  __device__ __forceinline__ uint32_t shift(uint32_t v, uint32_t n) const {  // n <= 1024
+    const uint32_t a6 = n >> 6, b4 = (n >> 2) & 15u, r = n & 3u;
+    if (a6) v = ct_shift(s64 + 1024 * (a6 - 1), v);
+    if (b4) v = ct_shift(s4 + 1024 * (b4 - 1), v);
+    for (uint32_t i = 0; i < r; ++i) v = (v >> 8) ^ g3[v & 0xffu];
+    return v;
+  }
+  __device__ __forceinline__ uint32_t header_state(const uint8_t* h, uint32_t hs) const {
+    uint32_t v = 0xffffffffu;
+    for (uint32_t i = 6; i < hs; ++i) v = (v >> 8) ^ g3[(v ^ h[i]) & 0xffu];
+    return v;
+  }
+};
 
 struct Cand {
   uint8_t* head;       // per item: 1 = a candidate starts here
@@ -299,16 +317,15 @@ struct Cand {
   uint32_t* last;      //   last item
 };
 
-__global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t ni,
-                                                         const uint64_t* it_off,
-                                                         const uint8_t* it_old,
-                                                         const uint32_t* ipack,
-                                                         const uint32_t* crc_stored, Cand c) {
-  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
-  if (i >= ni) return;
-  c.head[i] = 0;
-  c.fused[i] = 0;
-  if (!a.fuse) return;  // (logs under 4 KiB: the rows kernels' dummy loads need 4 KiB)
+// one candidate head per item; a persistent grid with the shift tables in
+// LDS (E / Z are chains of table reads: from global memory they made this
+// pass 0.6-0.7 ms on C5).  head[] and fused[] are zeroed before the launch
+// (a head marks the fragments of its run: no other thread writes them).
+constexpr uint32_t kCandThreads = 1024;
+__device__ __forceinline__ void cand_one(const RecoverArgs& a, uint64_t ni, uint64_t i,
+                                         const uint64_t* it_off, const uint8_t* it_old,
+                                         const uint32_t* ipack, const uint32_t* crc_stored,
+                                         const Cand& c, const ShiftLds& T) {
   auto ltype = [&](uint64_t q) {  // legacy type of item q (0: none of Full..Last)
     const uint32_t ty = (ipack[q] >> 16) & 0xffu;
     const uint32_t nt = (ty >= 5 && ty <= 8) ? ty - 4 : ty;
@@ -371,15 +388,33 @@ __global__ void __launch_bounds__(kLanes) rw_cand_kernel(RecoverArgs a, uint64_t
   for (uint64_t r = first; r <= q; ++r) {
     const uint32_t l = ipack[r] & 0xffffu;
     if (l == 0) continue;  // (an empty trailing fragment: the rows kernel's CRC)
-    const uint32_t H = crc_header_state(a.log + it_off[r], hs);
+    const uint32_t H = T.header_state(a.log + it_off[r], hs);
     const uint32_t e = b + l;
     const uint32_t ws = b >> 10, we = (e - 1) >> 10;
-    const uint32_t E = crc_shift_bytes(H, 1024u * (ws + 1) - b);
-    const uint32_t Z = crc_shift_bytes(~crc_stored[r], 1024u * (we + 1) - e);
+    const uint32_t E = T.shift(H, 1024u * (ws + 1) - b);
+    const uint32_t Z = T.shift(~crc_stored[r], 1024u * (we + 1) - e);
     c.ez[r] = static_cast<uint64_t>(E) | (static_cast<uint64_t>(Z) << 32);
     c.fused[r] = 1;
     b = e;
   }
+}
+
+__global__ void __launch_bounds__(kCandThreads) rw_cand_kernel(RecoverArgs a, uint64_t ni,
+                                                               const uint64_t* it_off,
+                                                               const uint8_t* it_old,
+                                                               const uint32_t* ipack,
+                                                               const uint32_t* crc_stored, Cand c) {
+  __shared__ uint32_t s64[16 * 1024], s4[15 * 1024], g3[256];
+  if (!a.fuse) return;  // (logs under 4 KiB: the rows kernels' dummy loads need 4 KiB)
+  for (uint32_t k = threadIdx.x; k < 16 * 1024; k += kCandThreads) s64[k] = kCrcS64[k];
+  for (uint32_t k = threadIdx.x; k < 15 * 1024; k += kCandThreads) s4[k] = kCrcS4[k];
+  if (threadIdx.x < 256) g3[threadIdx.x] = kCrcG[3 * 256 + threadIdx.x];
+  __syncthreads();
+  const ShiftLds T{s64, s4, g3};
+  const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kCandThreads;
+  for (uint64_t i = static_cast<uint64_t>(blockIdx.x) * kCandThreads + threadIdx.x; i < ni;
+       i += stride)
+    cand_one(a, ni, i, it_off, it_old, ipack, crc_stored, c, T);
 }
 
 // compact lists: candidates (item order) and the physical records the rows
@@ -1240,8 +1275,13 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       // candidates: the records a writer lays out, CRC'd and hashed by ONE
       // read of their bytes (the fused kernel); the other physical records
       // go to the rows kernel's CRC (sync: the two list sizes)
-      hipLaunchKernelGGL(rw_cand_kernel, grid_for(ni), dim3(kLanes), 0, st, a, ni, q.it_off,
-                         q.it_old, q.ipack, q.crc_stored, q.c);
+      (void)hipMemsetAsync(q.c.head, 0, ni, st);
+      (void)hipMemsetAsync(q.c.fused, 0, ni, st);
+      const uint64_t cg = (ni + kCandThreads - 1) / kCandThreads;
+      const uint32_t ncu = static_cast<uint32_t>(device_info().num_cus);
+      hipLaunchKernelGGL(rw_cand_kernel, dim3(static_cast<uint32_t>(cg < ncu ? cg : ncu)),
+                         dim3(kCandThreads), 0, st, a, ni, q.it_off, q.it_old, q.ipack,
+                         q.crc_stored, q.c);
       hipLaunchKernelGGL(rw_cand_flags_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni,
                          q.it_old, q.fc, q.fr);
       const uint64_t nti = (ni + kScanTile - 1) / kScanTile;

@@ -1043,11 +1043,18 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   // some row needs them; the loads themselves are unconditional, so every
   // step issues the same loads (the compiler's vmcnt waits stay precise).
   const uint8_t* R = a.base + (valid ? (B & ~3ull) : 0ull);
+  // XXH3 only: a chunk that starts past the record end (its first dword may
+  // still hold the realignment bytes of the lane in front) is read from the
+  // buffer start instead -- the last window's tail is the next record's,
+  // which its own row reads (C5 a14 -1.7 %).  The fused kernel loads them
+  // (A/B: the redirect's registers cost it 3.6 %)
+  const uint32_t rem4 = (valid ? P.size - wpos : 0u) + 4u;
   uint32_t fm = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
     const bool past = lng && dl <= static_cast<int32_t>(256 * k + 16);
-    const uint8_t* pq = R + (past ? dA : 0u) + 256 * k;
+    const bool need = CRC || (valid && 16 * t + 256 * k < rem4);
+    const uint8_t* pq = (need ? R : a.base) + (past ? dA : 0u) + 256 * k;
     uint32_t mm = past ? m1 : m0;
     if (k >= 2 && __ballot(shrt)) {
       // a short record: its window layout in x[0], x[1] (the fused CRC reads

@@ -91,3 +91,28 @@ def test_recover_c5_shape_with_corruption():
     reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
     compare(recs, reps, res, log, 0, R.kPointInTimeRecovery, "c5")
     assert res.n_physical == len(w.rec_offsets)
+
+
+@pytest.mark.gpu
+def test_recover_dense_tiny_records():
+    """20 log blocks of records of 0-2 bytes (about 4 600 per block, so the
+    first workgroup of the walk holds far more items than rw_fill's LDS stage:
+    its direct-store path), then ordinary records, with a few flips: every
+    record and report equal the serial reader's in every mode"""
+    import time
+
+    import torch
+    from forst_amd import engine
+    rng = np.random.default_rng(17)
+    tiny = rng.integers(0, 3, 20 * 32768 // 9).astype(np.uint32)
+    big = (np.exp(rng.uniform(np.log(32), np.log(20000), 400))).astype(np.uint32)
+    log, po, pl = W.frame_lens(np.concatenate([tiny, big]), 5)
+    for off in rng.choice(po[len(tiny) // 2:], 6, replace=False):
+        log[int(off) + 6] ^= 0x10  # the type byte (in the CRC'd range): a checksum mismatch
+    t0 = time.perf_counter()
+    for mode in MODES:
+        rec, rep, res = engine.wal_recover_batch(torch.from_numpy(log).cuda(), 7, mode)
+        recs = [rec[k].cpu().numpy() for k in ("offset", "length", "hash", "n_fragments")]
+        reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
+        compare(recs, reps, res, log, 7, mode, "dense")
+    assert time.perf_counter() - t0 < 120

@@ -1403,11 +1403,13 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   }
 #endif
   BatchFeed feed;
-  // block modes: the workgroup feed in 8-descriptor batches (two blocks per
-  // row; 16 measured 3 % slower at C2, 0.7 % at NS16); WAL records (raw)
-  // keep the global feed, measured 4 % faster for them (stream_common.h)
+  // block modes: the workgroup feed in 4-descriptor batches (one block per
+  // row; A/B against 8: C2 verify +2.2 %, write +1.8 %, NS16 +0.9 %, C4
+  // +1.4 %, profiles/ab_r03/crc_feed_batch.log; 16 was 3 % slower than 8);
+  // WAL records (raw) keep the global feed (byte-balanced workgroup ranges
+  // measured within noise for them, profiles/ab_r03/wal_wg_feed.log)
   constexpr bool kWgFeed = MODE != kModeRaw;
-  constexpr uint32_t kChunk = 8;
+  constexpr uint32_t kChunk = 4;
   uint64_t cg = feed_first<kWgFeed, kChunk>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)

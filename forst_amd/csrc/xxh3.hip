@@ -29,9 +29,9 @@ constexpr uint32_t kThreads = kWaves * 64;
 // workgroup feed (stream_common.h) balances every wave of a CU
 constexpr uint32_t kRowsWaves = 12;
 constexpr uint32_t kRowsThreads = kRowsWaves * 64;
-// workgroup-feed batch (stream_common.h): 8 descriptors, two per row (16
-// measured 1 % slower on C3, 0.3 % on NS16X)
-constexpr uint32_t kXxWgChunk = 8;
+// workgroup-feed batch (stream_common.h): 4 descriptors, one per row (A/B
+// against 8: C3 +0.4-0.6 %, NS16X +0.7 %; 16 was 1 % slower than 8)
+constexpr uint32_t kXxWgChunk = 4;
 // the fragment kernel (WAL records): 4-wave workgroups and the global feed
 // (the workgroup feed measured 5 % slower on C5's log-uniform records)
 constexpr bool kFragWg = false;

@@ -16,7 +16,7 @@ shift 2 || true
 if [ "$CFG" = "C5" ]; then
   PROG="tools/prof_wal.py ${*:-}"
 else
-  PROG="bench.py --config $CFG --steps 5 --warmup 2 --no-cpu-baseline --no-extras ${*:-}"
+  PROG="bench.py --config $CFG --steps 10 --warmup 3 --no-cpu-baseline --no-extras ${*:-}"
 fi
 OUT=gpurun_out/prof_${TAG}_${CFG}
 mkdir -p "$OUT"

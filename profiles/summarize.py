@@ -24,6 +24,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = {"0": "compute", "1": "trailer", "2": "verify", "3": "raw"}
+TIMED = 10  # bench.py --steps default (profiles/profile.sh runs the same count)
 
 
 def short(name):
@@ -50,6 +51,14 @@ def main():
     for r in csv.DictReader(open(stats)):
         avg_ns[short(r["Name"])] = float(r["AverageNs"])
         calls[short(r["Name"])] = int(r["Calls"])
+    # per-launch durations in dispatch order (the spread behind the average:
+    # launches of one run differ by up to ~20 % under the profiler)
+    launches = defaultdict(list)
+    trace = os.path.join(src, "trace", "trace_kernel_trace.csv")
+    if os.path.exists(trace):
+        for r in sorted(csv.DictReader(open(trace)), key=lambda r: int(r["Start_Timestamp"])):
+            launches[short(r["Kernel_Name"])].append(
+                int(r["End_Timestamp"]) - int(r["Start_Timestamp"]))
     fetch = load_counter(os.path.join(src, "fetch", "fetch_counter_collection.csv"))
     write = load_counter(os.path.join(src, "write", "write_counter_collection.csv"))
     rows = []
@@ -60,6 +69,13 @@ def main():
         w = sum(write[k]) / len(write[k]) if write[k] else None
         rows.append({"kernel": k, "config": config, "calls": calls.get(k),
                      "avg_duration_ns_kernel_trace": avg_ns.get(k),
+                     "launch_ns": launches.get(k) if len(launches.get(k, [])) <= 64 else None,
+                     # the last TIMED launches: a bench config's profiled command is the
+                     # default bench run (--steps 10 --warmup 3), whose last 10 launches
+                     # of each kernel are the steps its HIP events time
+                     "avg_duration_ns_timed_steps": (
+                         sum(launches[k][-TIMED:]) / TIMED
+                         if config != "C5" and len(launches.get(k, [])) >= TIMED else None),
                      "fetch_size_kib_avg": f, "write_size_kib_avg": w,
                      "hbm_bytes_per_launch": (int(2 * (f or 0) * 1024 + (w or 0) * 1024)
                                               if f is not None or w is not None else None)})

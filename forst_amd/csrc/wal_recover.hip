@@ -1477,6 +1477,14 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     full.length = A4.take<uint64_t>(nr);
     full.hash = A4.take<uint64_t>(nr);
     full.n_fragments = A4.take<uint32_t>(nr);
+    // the caller's arrays hold every record: the kernels write them directly
+    // (no copy-out; C5: four 80 MB device copies, 0.11 ms of a recovery)
+    if (nr <= rec_cap) {
+      if (recs.offset) full.offset = recs.offset;
+      if (recs.length) full.length = recs.length;
+      if (recs.hash) full.hash = recs.hash;
+      if (recs.n_fragments) full.n_fragments = recs.n_fragments;
+    }
     hash_begin = A4.take<uint64_t>(nr);
     last_tok = A4.take<uint64_t>(nr);
   }
@@ -1520,12 +1528,13 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   // copy the (capacity-limited) record list out
   const uint64_t nc = nr < rec_cap ? nr : rec_cap;
   if (e == hipSuccess && nc) {
-    if (recs.offset) e = hipMemcpyAsync(recs.offset, full.offset, 8 * nc, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess && recs.length)
+    if (recs.offset && recs.offset != full.offset)
+      e = hipMemcpyAsync(recs.offset, full.offset, 8 * nc, hipMemcpyDeviceToDevice, st);
+    if (e == hipSuccess && recs.length && recs.length != full.length)
       e = hipMemcpyAsync(recs.length, full.length, 8 * nc, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess && recs.hash)
+    if (e == hipSuccess && recs.hash && recs.hash != full.hash)
       e = hipMemcpyAsync(recs.hash, full.hash, 8 * nc, hipMemcpyDeviceToDevice, st);
-    if (e == hipSuccess && recs.n_fragments)
+    if (e == hipSuccess && recs.n_fragments && recs.n_fragments != full.n_fragments)
       e = hipMemcpyAsync(recs.n_fragments, full.n_fragments, 4 * nc, hipMemcpyDeviceToDevice, st);
   }
   if (e == hipSuccess) e = hipGetLastError();

@@ -1377,7 +1377,7 @@ constexpr uint32_t kRowsD2Waves = 12;
 constexpr uint32_t kDiagWaves = 8192;
 __device__ unsigned long long g_wave_t0[kDiagWaves], g_wave_t1[kDiagWaves];
 #endif
-template <int MODE, int PROBE, int DEPTH>
+template <int MODE, int PROBE, int DEPTH, bool RAW_WG = false>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint32_t L[kLds3Bytes / 4];
   feed_init();
@@ -1407,8 +1407,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   // row; A/B against 8: C2 verify +2.2 %, write +1.8 %, NS16 +0.9 %, C4
   // +1.4 %, profiles/ab_r03/crc_feed_batch.log; 16 was 3 % slower than 8);
   // WAL records (raw) keep the global feed (byte-balanced workgroup ranges
-  // measured within noise for them, profiles/ab_r03/wal_wg_feed.log)
-  constexpr bool kWgFeed = MODE != kModeRaw;
+  // measured within noise for them, profiles/ab_r03/wal_wg_feed.log), except
+  // small raw batches (RAW_WG: crc32c_rows_raw_small_kernel)
+  constexpr bool kWgFeed = MODE != kModeRaw || RAW_WG;
   constexpr uint32_t kChunk = 4;
   uint64_t cg = feed_first<kWgFeed, kChunk>(a, nw, gw, lane, feed);
   if (cg >= a.n) return;
@@ -1677,6 +1678,14 @@ template <int MODE>
 __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
   crc32c_rows_body<MODE, 0, 1>(a);
 }
+// raw batches smaller than one 64-descriptor chunk per wave of the grid (the
+// records a WAL recovery's fused kernel does not cover, a WAL write of a few
+// records): the global feed would hand them to a few waves in 64-descriptor
+// chunks, 64 records one after another on each, while the workgroup feed
+// spreads them over every wave in 4-descriptor batches
+__global__ void __launch_bounds__(kThreads) crc32c_rows_raw_small_kernel(BlockArgs a) {
+  crc32c_rows_body<kModeRaw, 0, 1, true>(a);
+}
 
 #ifdef FORST_DIAG
 template <int PROBE>
@@ -1887,6 +1896,8 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
     case CrcKernel::kRows:
       // block modes: the workgroup feed (stream_common.h), no ticket counter
       if (M != kModeRaw) return launch_kernel(crc32c_rows_kernel<M>, grid, 64 * kWaves, a, s);
+      if (a.n < uint64_t(64) * grid * kWaves)
+        return launch_kernel(crc32c_rows_raw_small_kernel, grid, 64 * kWaves, a, s);
       return launch_fed(crc32c_rows_kernel<M>, grid, kWaves, a, s);
     case CrcKernel::kV2:
       return launch_kernel(crc32c_stream2_kernel<M>, grid, kThreads, a, s);
@@ -1994,6 +2005,8 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream
   }
 #endif
   *name = crc_kernel_name(k, mode);
+  if (k == CrcKernel::kRows && mode == kModeRaw && a.n < uint64_t(64) * grid * kWaves)
+    *name = "crc32c_rows_raw_small_kernel";
   switch (mode) {
     case kModeCompute:
       return launch_crc_mode<kModeCompute>(k, a, grid, stream);

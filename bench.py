@@ -524,9 +524,8 @@ def main():
     torch.cuda.empty_cache()
     if world == 1 and not args.no_extras and args.config == "C2":
         for nm in ("NS16", "NS16X", "C3", "C3S", "C4"):
-            # the north-star points with the headline's step and warmup counts
-            r = run_config(nm, args.steps if nm.startswith("NS") else max(3, args.steps // 2),
-                           args.warmup if nm.startswith("NS") else 1, rank, world)
+            # every extra config with the headline's step and warmup counts
+            r = run_config(nm, args.steps, args.warmup, rank, world)
             r.pop("batch")
             torch.cuda.empty_cache()
             kv, kt = r["kernels"]["verify"], r["kernels"]["trailer"]

@@ -82,6 +82,8 @@ def lib():
         "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp,
                                       u64, vp]),
         "forst_wal_layout": (i, [vp, u64, i, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp]),
+        "forst_wal_layout_at": (i, [vp, u64, i, u32, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp,
+                                    vp]),
         "forst_fill_stream": (i, [vp, u64, u64, u64, vp]),
         "forst_partition_bytes": (i, [vp, u64, u32, vp]),
         "forst_block_verify_host": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp, i]),

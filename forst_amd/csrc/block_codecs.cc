@@ -12,10 +12,12 @@
 // LZ4 block (LZ4_decompress_safe); ZSTD = a zstd frame; BZip2.  zlib is
 // linked; liblz4 / libzstd / libbz2 are opened at run time when present (the
 // image ships their runtime libraries, not their headers: the few entry points
-// used are declared here with their published C signatures).  Snappy and
-// XPRESS have no library on the image: NotSupported, as a reference build
-// without them reports.  Data blocks are never decompressed -- their checksum
-// covers the compressed bytes.
+// used are declared here with their published C signatures).  Snappy (ForSt's
+// default column-family compression, options/options.cc:123) has no library on
+// the image, so its block format is decoded here from the published format
+// description (snappy_raw_decode below).  XPRESS (Windows only) is
+// NotSupported, as a reference build without it reports.  Data blocks are
+// never decompressed -- their checksum covers the compressed bytes.
 #include <dlfcn.h>
 #include <zlib.h>
 
@@ -118,10 +120,15 @@ bool zlib_inflate(const uint8_t* in, size_t n, uint32_t size, bool known,
   z_stream z;
   std::memset(&z, 0, sizeof(z));
   if (inflateInit2(&z, -14) != Z_OK) return false;
+  // a non-null output pointer even for an empty block: zlib rejects a null
+  // next_out (Z_STREAM_ERROR), where the reference's AllocateBlock(0) is a
+  // valid pointer
+  out->reserve(len ? len : 1);
   out->assign(len, 0);
   z.next_in = const_cast<Bytef*>(in);
   z.avail_in = static_cast<uInt>(n);
-  z.next_out = out->data();
+  uint8_t dummy = 0;
+  z.next_out = len ? out->data() : &dummy;
   z.avail_out = static_cast<uInt>(len);
   for (;;) {
     const int st = inflate(&z, Z_SYNC_FLUSH);
@@ -142,6 +149,90 @@ bool zlib_inflate(const uint8_t* in, size_t n, uint32_t size, bool known,
   return true;
 }
 
+
+// Snappy raw block format (the published format_description.txt of the snappy
+// project; Snappy_Uncompress, util/compression.h:729-754, calls
+// snappy::GetUncompressedLength then snappy::RawUncompress).  Snappy keeps its
+// own length prefix in every compress_format_version (compression.h:711).
+//   preamble: the uncompressed length, a little-endian base-128 varint of at
+//             most 5 bytes whose value fits 32 bits;
+//   then elements until the input is exhausted, each starting with a tag byte
+//   whose low 2 bits are the kind:
+//     00 literal: len-1 in the upper 6 bits (0..59), or 60..63 = 1..4 LE
+//        bytes of len-1 follow; then len literal bytes;
+//     01 copy, 1-byte offset: len = 4 + bits 2..4, offset = bits 5..7 << 8 |
+//        next byte;
+//     10 copy, 2-byte offset: len = 1 + upper 6 bits, LE16 offset;
+//     11 copy, 4-byte offset: len = 1 + upper 6 bits, LE32 offset.
+//   A copy reads `offset` bytes back in the output (offset 0 or beyond what
+//   was produced is an error; len > offset is an overlapping run-length copy).
+//   Success iff every element is complete and in bounds, the input ends on an
+//   element boundary, and exactly `length` bytes were produced.
+bool snappy_raw_decode(const uint8_t* in, size_t n, std::vector<uint8_t>* out) {
+  const uint8_t* p = in;
+  const uint8_t* lim = in + n;
+  uint32_t length = 0;
+  {
+    uint32_t shift = 0;
+    for (;;) {
+      if (p >= lim || shift > 28) return false;
+      const uint32_t b = *p++;
+      if (shift == 28 && b >= 16) return false;  // > 32 bits
+      length |= (b & 127u) << shift;
+      if (!(b & 128u)) break;
+      shift += 7;
+    }
+  }
+  out->assign(length, 0);
+  uint8_t* o = out->data();
+  size_t produced = 0;
+  while (p < lim) {
+    const uint32_t tag = *p++;
+    const uint32_t kind = tag & 3u;
+    if (kind == 0) {
+      uint32_t len = tag >> 2;  // len - 1 (snappy computes it in 32 bits)
+      if (len >= 60) {
+        const uint32_t nb = len - 59;
+        if (static_cast<size_t>(lim - p) < nb) return false;
+        uint32_t v = 0;
+        for (uint32_t i = 0; i < nb; ++i) v |= static_cast<uint32_t>(p[i]) << (8 * i);
+        p += nb;
+        len = v;
+      }
+      const uint64_t L = static_cast<uint64_t>(static_cast<uint32_t>(len + 1u));
+      if (static_cast<uint64_t>(lim - p) < L || L > length - produced) return false;
+      std::memcpy(o + produced, p, L);
+      p += L;
+      produced += L;
+    } else {
+      uint32_t len, off;
+      if (kind == 1) {
+        if (lim - p < 1) return false;
+        len = 4 + ((tag >> 2) & 7u);
+        off = ((tag >> 5) << 8) | p[0];
+        p += 1;
+      } else if (kind == 2) {
+        if (lim - p < 2) return false;
+        len = 1 + (tag >> 2);
+        off = static_cast<uint32_t>(p[0]) | static_cast<uint32_t>(p[1]) << 8;
+        p += 2;
+      } else {
+        if (lim - p < 4) return false;
+        len = 1 + (tag >> 2);
+        off = static_cast<uint32_t>(p[0]) | static_cast<uint32_t>(p[1]) << 8 |
+              static_cast<uint32_t>(p[2]) << 16 | static_cast<uint32_t>(p[3]) << 24;
+        p += 4;
+      }
+      if (off == 0 || off > produced || len > length - produced) return false;
+      uint8_t* d = o + produced;
+      const uint8_t* s = d - off;
+      for (uint32_t i = 0; i < len; ++i) d[i] = s[i];  // byte order: overlap repeats
+      produced += len;
+    }
+  }
+  return produced == length;
+}
+
 }  // namespace
 
 // BlockFetcher's decompression of one serialized block (contents of type
@@ -152,7 +243,7 @@ int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, s
                      std::vector<uint8_t>* out, std::string* err) {
   const bool v2 = format_version >= 2;  // GetCompressFormatForVersion
   const Libs& L = libs();
-  const bool supported = type == 2 || ((type == 4 || type == 5) && L.lz4_decompress_safe) ||
+  const bool supported = type == 1 || type == 2 || ((type == 4 || type == 5) && L.lz4_decompress_safe) ||
                          (type == 7 && L.zstd_decompress) || (type == 3 && L.bz_decompress_init);
   if (!supported) {
     *err = std::string("Unsupported compression method for this build: ") + codec_name(type);
@@ -163,7 +254,9 @@ int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, s
   uint32_t size = 0;
   const char* detail = nullptr;
   bool ok = false;
-  if (v2 && !get_varint32(p, lim, &size)) {
+  if (type == 1) {
+    ok = snappy_raw_decode(p, n, out);  // no size prefix in either format version
+  } else if (v2 && !get_varint32(p, lim, &size)) {
     ok = false;
   } else if (type == 2) {
     ok = zlib_inflate(p, static_cast<size_t>(lim - p), size, v2, out);
@@ -181,6 +274,11 @@ int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, s
       const int r = L.lz4_decompress_safe(reinterpret_cast<const char*>(p),
                                           reinterpret_cast<char*>(out->data()),
                                           static_cast<int>(lim - p), static_cast<int>(size));
+      // The reference only asserts r == size (compression.h LZ4_Uncompress,
+      // compiled out under NDEBUG).  Kept as a hard check on purpose: a
+      // short decode leaves the tail of the block zero-filled, which the
+      // index walk would then parse as garbage; reporting it as corruption
+      // is the debug build's behaviour.
       ok = r >= 0 && static_cast<uint32_t>(r) == size;
     }
   } else if (type == 7) {
@@ -192,34 +290,48 @@ int uncompress_block(uint8_t type, uint32_t format_version, const uint8_t* in, s
       if (L.zstd_is_error(r)) {
         detail = L.zstd_error_name(r);
       } else {
-        ok = r == size;
+        ok = r == size;  // same deliberate exact-size check as LZ4 above
       }
     }
   } else if (type == 3) {
+    // BZip2_Uncompress (compression.h:1036-1105): format 1 starts at 5x the
+    // input rounded to a page and grows the output by 20% whenever BZ_OK
+    // says it is full.  A stream that ends early also returns BZ_OK (no
+    // input left, output not full); the reference would grow the output
+    // forever there -- it is reported as corruption instead.
     BzStream s;
     std::memset(&s, 0, sizeof(s));
     if (L.bz_decompress_init(&s, 0, 0) == 0) {
-      out->assign(v2 ? size : (n * 5 + 4095) / 4096 * 4096 + 4096, 0);
+      const size_t n_in = static_cast<size_t>(lim - p);
+      size_t cap = v2 ? size : std::min<size_t>(((n_in * 5) & ~size_t(4095)) + 4096, 0xffffffffu);
+      out->assign(cap ? cap : 1, 0);
       s.next_in = const_cast<char*>(reinterpret_cast<const char*>(p));
-      s.avail_in = static_cast<unsigned>(lim - p);
+      s.avail_in = static_cast<unsigned>(n_in);
       s.next_out = reinterpret_cast<char*>(out->data());
-      s.avail_out = static_cast<unsigned>(out->size());
+      s.avail_out = static_cast<unsigned>(cap);
       for (;;) {
+        const unsigned in_before = s.avail_in, out_before = s.avail_out;
         const int st = L.bz_decompress(&s);
         if (st == 4) {  // BZ_STREAM_END
           ok = true;
           break;
         }
-        if (st != 0) break;  // BZ_OK
-        if (s.avail_out == 0) {
-          if (v2) break;
-          const size_t used = out->size();
-          out->resize(used * 2);
-          s.next_out = reinterpret_cast<char*>(out->data() + used);
-          s.avail_out = static_cast<unsigned>(out->size() - used);
+        if (st != 0) break;  // not BZ_OK: the reference fails too
+        if (s.avail_out != 0) {
+          // BZ_OK with room left: the input ran out mid-stream (or the call
+          // made no progress at all) -- truncated
+          if (s.avail_in == 0 || (s.avail_in == in_before && s.avail_out == out_before)) break;
+          continue;
         }
+        if (v2) break;  // the stated size was too small
+        const size_t used = cap;
+        cap = std::min<size_t>(static_cast<size_t>(cap * 1.2) + 1, 0xffffffffu);
+        if (cap <= used) break;
+        out->resize(cap);
+        s.next_out = reinterpret_cast<char*>(out->data() + used);
+        s.avail_out = static_cast<unsigned>(cap - used);
       }
-      const size_t produced = out->size() - s.avail_out;
+      const size_t produced = cap - s.avail_out;
       L.bz_decompress_end(&s);
       if (ok) out->resize(produced);
     }

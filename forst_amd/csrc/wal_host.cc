@@ -23,15 +23,16 @@ enum : uint8_t {  // db/log_format.h:20-41
 };
 }  // namespace
 
-extern "C" __attribute__((visibility("default"))) int forst_wal_layout(
-    const uint32_t* lengths, uint64_t n_records, int recyclable, uint64_t* rec_offsets,
-    uint32_t* rec_lengths, uint8_t* rec_types, uint64_t capacity, uint64_t* pad_offsets,
-    uint32_t* pad_lengths, uint64_t pad_capacity, uint64_t* n_phys, uint64_t* n_pads,
-    uint64_t* total_bytes) {
+extern "C" __attribute__((visibility("default"))) int forst_wal_layout_at(
+    const uint32_t* lengths, uint64_t n_records, int recyclable, uint32_t block_offset,
+    uint64_t* rec_offsets, uint32_t* rec_lengths, uint8_t* rec_types, uint64_t capacity,
+    uint64_t* pad_offsets, uint32_t* pad_lengths, uint64_t pad_capacity, uint64_t* n_phys,
+    uint64_t* n_pads, uint64_t* total_bytes, uint32_t* end_block_offset) {
   if (n_records && !lengths) return FORST_EINVAL;
+  if (block_offset > kBlockSize) return FORST_EINVAL;
   const uint32_t hs = recyclable ? kRecyclableHeaderSize : kHeaderSize;
   uint64_t off = 0, np = 0, npad = 0;
-  uint32_t bo = 0;  // Writer::block_offset_
+  uint32_t bo = block_offset;  // Writer::block_offset_ (offsets below: from the append position)
   for (uint64_t r = 0; r < n_records; ++r) {
     uint64_t left = lengths[r];
     bool begin = true;
@@ -75,6 +76,18 @@ extern "C" __attribute__((visibility("default"))) int forst_wal_layout(
   if (n_phys) *n_phys = np;
   if (n_pads) *n_pads = npad;
   if (total_bytes) *total_bytes = off;
+  if (end_block_offset) *end_block_offset = bo;
   return (np > capacity || npad > pad_capacity) && (rec_offsets || pad_offsets) ? FORST_EINVAL
                                                                                 : FORST_OK;
+}
+
+// a fresh log (Writer::block_offset_ = 0, log_writer.cc:25)
+extern "C" __attribute__((visibility("default"))) int forst_wal_layout(
+    const uint32_t* lengths, uint64_t n_records, int recyclable, uint64_t* rec_offsets,
+    uint32_t* rec_lengths, uint8_t* rec_types, uint64_t capacity, uint64_t* pad_offsets,
+    uint32_t* pad_lengths, uint64_t pad_capacity, uint64_t* n_phys, uint64_t* n_pads,
+    uint64_t* total_bytes) {
+  return forst_wal_layout_at(lengths, n_records, recyclable, 0, rec_offsets, rec_lengths,
+                             rec_types, capacity, pad_offsets, pad_lengths, pad_capacity, n_phys,
+                             n_pads, total_bytes, nullptr);
 }

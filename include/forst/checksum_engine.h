@@ -235,4 +235,102 @@ class GpuTrailerWriter {
   ChecksumStats stats_;
 };
 
+// ---- WAL ---------------------------------------------
+//
+// Recovery: DBImpl::RecoverLogFiles (db/db_impl/db_impl_open.cc:1195-1260)
+// loops log::Reader::ReadRecord(&record, &scratch, wal_recovery_mode,
+// &record_checksum), and the reader calls Reporter::Corruption(bytes,
+// Status::Corruption(reason)) as it goes (log_reader.cc:69-320).  WalRecovery
+// runs that reader over the whole log image on the GPU
+// (forst_wal_recover_batch) and hands the same calls back in the same order:
+// Next() yields each record (its bytes, LastRecordOffset, XXH3 record
+// checksum) together with the reports ReadRecord made before returning it;
+// trailing_reports() are the ones after the last record.
+struct WalReport {
+  uint64_t offset = 0;  // reader position of the physical record / event
+  uint64_t bytes = 0;   // as passed to Reporter::Corruption
+  uint32_t reason = 0;  // forst_wal_report_reason
+  uint32_t type = 0;    // record type (unknown record type)
+  std::string Text() const;  // the reader's reason string (log_reader.cc)
+};
+struct WalRecord {
+  const char* data = nullptr;  // the record: into the host log (one fragment) or
+  size_t size = 0;             //   the WalRecovery's scratch (several)
+  uint64_t offset = 0;         // Reader::LastRecordOffset
+  uint64_t checksum = 0;       // record_checksum (XXH3_64bits of the record)
+  uint32_t n_fragments = 0;
+  std::vector<WalReport> reports_before;
+};
+class WalRecovery {
+ public:
+  explicit WalRecovery(void* hip_stream = nullptr) : stream_(hip_stream) {}
+  ~WalRecovery();
+  WalRecovery(const WalRecovery&) = delete;
+  WalRecovery& operator=(const WalRecovery&) = delete;
+  // The log's bytes in device memory (d_log) and the same bytes in host memory
+  // (host_log: record bytes are handed out from it).  wal_recovery_mode =
+  // WALRecoveryMode (include/rocksdb/options.h).  Synchronises the stream.
+  // NotSupported for a compressed WAL (kSetCompressionType naming kZSTD):
+  // keep the serial log::Reader for that log.
+  Status Recover(const uint8_t* d_log, const uint8_t* host_log, uint64_t log_len,
+                 uint32_t log_number, int wal_recovery_mode);
+  // false after the last record; status() is then OK unless the record
+  // layout could not be followed on the host (NotSupported: fall back)
+  bool Next(WalRecord* r);
+  const std::vector<WalReport>& trailing_reports() const { return trailing_; }
+  const Status& status() const { return status_; }
+  const forst_wal_recover_result& result() const { return res_; }
+
+ private:
+  Status Grow(uint64_t rec_cap, uint64_t rep_cap);
+  void* stream_;
+  const uint8_t* host_ = nullptr;
+  uint64_t len_ = 0;
+  forst_wal_recover_result res_{};
+  std::vector<uint64_t> off_, rlen_, hash_;
+  std::vector<uint32_t> nfrag_;
+  std::vector<WalReport> reports_, trailing_;
+  size_t next_rec_ = 0, next_rep_ = 0;
+  std::string scratch_;
+  Status status_;
+  void* dev_ = nullptr;  // device arrays (records, then reports)
+  uint64_t rec_cap_ = 0, rep_cap_ = 0;
+};
+
+// Write side: log::Writer::AddRecord (db/log_writer.cc:65-160) +
+// EmitPhysicalRecord (:228-263) for a whole write group at once.  Frame()
+// lays the records out as AddRecord would from the writer's block offset
+// (forst_wal_layout_at), assembles the image on the host (zero-padded block
+// tails, [len][type][log number] headers, payloads), computes every record
+// CRC in one GPU launch (forst_wal_record_crc_batch) and puts them in the
+// headers: data()/size() is what AddRecord would have appended, record by
+// record, and end_block_offset() the writer's block_offset_ afterwards.
+struct ByteRange {
+  const char* data;
+  size_t size;
+};
+class WalWriteGroup {
+ public:
+  WalWriteGroup(bool recyclable, uint32_t log_number, void* hip_stream = nullptr)
+      : recyclable_(recyclable), log_number_(log_number), stream_(hip_stream) {}
+  ~WalWriteGroup();
+  WalWriteGroup(const WalWriteGroup&) = delete;
+  WalWriteGroup& operator=(const WalWriteGroup&) = delete;
+  Status Frame(const std::vector<ByteRange>& records, uint32_t block_offset);
+  const char* data() const { return image_.data(); }
+  size_t size() const { return image_.size(); }
+  uint32_t end_block_offset() const { return end_bo_; }
+  uint64_t physical_records() const { return offs_.size(); }
+
+ private:
+  bool recyclable_;
+  uint32_t log_number_;
+  void* stream_;
+  std::string image_;
+  std::vector<uint64_t> offs_;
+  uint32_t end_bo_ = 0;
+  void* dev_ = nullptr;
+  uint64_t dev_cap_ = 0;
+};
+
 }  // namespace forst_gpu

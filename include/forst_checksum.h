@@ -314,6 +314,16 @@ int forst_wal_layout(const uint32_t* lengths, uint64_t n_records, int recyclable
                      uint64_t capacity, uint64_t* pad_offsets, uint32_t* pad_lengths,
                      uint64_t pad_capacity, uint64_t* n_phys, uint64_t* n_pads,
                      uint64_t* total_bytes);
+/* The same from a writer that already stands at `block_offset` in its current
+ * 32 KiB block (log::Writer::block_offset_, db/log_writer.h): offsets count from
+ * the append position, *end_block_offset = block_offset_ after the last record
+ * -- a write group framed at once, appended with one WritableFileWriter::Append.
+ * forst_wal_layout == forst_wal_layout_at(..., block_offset = 0, ...). */
+int forst_wal_layout_at(const uint32_t* lengths, uint64_t n_records, int recyclable,
+                        uint32_t block_offset, uint64_t* rec_offsets, uint32_t* rec_lengths,
+                        uint8_t* rec_types, uint64_t capacity, uint64_t* pad_offsets,
+                        uint32_t* pad_lengths, uint64_t pad_capacity, uint64_t* n_phys,
+                        uint64_t* n_pads, uint64_t* total_bytes, uint32_t* end_block_offset);
 
 /* NPHash64 / Hash64 (util/hash.h:45-62, util/hash.cc:81 ->
  * XXPH3_64bits_withSeed, util/xxph3.h:1733; xxHash 0.7.2 preview):

@@ -276,6 +276,26 @@ class Reader:
             in_frag, scratch = False, b""
 
 
+def resume_at(reader, pos):
+    """TEST-INFRASTRUCTURE shortcut (no reference counterpart): put `reader`
+    in the state ReadRecord leaves behind after returning a complete record
+    whose last fragment ends at `pos` -- the 32 KiB block holding `pos` in the
+    buffer, consumed up to `pos`, no fragment in progress, a first record
+    read.  The next read_record starts at the physical record at `pos`, so a
+    window of a large log (starting at the block boundary below `pos`) can be
+    checked against the serial reader without replaying everything before
+    it.  Valid only when the log before `pos` holds no control records
+    (SetCompressionType, timestamp-size) and no recycled headers."""
+    blk = pos // kBlockSize * kBlockSize
+    reader.file_pos = blk
+    reader.end_of_buffer_offset = blk
+    reader.eof = False
+    reader.read_more()
+    reader.buf_lo = pos
+    reader.first_record_read = True
+    return reader
+
+
 def read_all(log, log_number=0, mode=kPointInTimeRecovery):
     """Every logical record ReadRecord returns, in order: (record offset =
     Reader::LastRecordOffset, length, record checksum), and the reporter's

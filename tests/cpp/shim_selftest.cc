@@ -2,12 +2,14 @@
 // (include/forst/checksum_engine.h) the way a ForSt call site would.
 //   shim_selftest pure   host-only helpers (no GPU)
 //   shim_selftest gpu    BlockChecksumEngine write/verify on a real MI355X
+//   shim_selftest wal    WalWriteGroup framing + WalRecovery round trip
 //   shim_selftest threads  4 host threads, one HIP stream each, interleaving
 //                        write-side, verify, WAL and raw-hash calls against
 //                        the engine's shared per-device scratch pool
 // Prints PASS or FAIL lines; exit code 0 iff all passed.
 #include <hip/hip_runtime.h>
 
+#include <algorithm>
 #include <atomic>
 #include <cstdio>
 #include <cstring>
@@ -287,11 +289,122 @@ static void threads() {
   std::printf("threads: %d x %d rounds, failures %d\n", kThreads, kRounds, failures.load());
 }
 
+// WalWriteGroup (log::Writer::AddRecord for a write group) and WalRecovery
+// (RecoverLogFiles' ReadRecord loop) round trip: groups framed one after the
+// other from the writer's block offset make the log the serial writer would
+// (every CRC restated here bytewise); recovery hands back every record's
+// bytes in order with no reports; a flipped payload byte gives the reader's
+// "checksum mismatch" report right before the next record it returns.
+static void wal(bool recyclable) {
+  const uint32_t log_number = 0x51u;
+  std::vector<std::string> recs;
+  for (int i = 0; i < 700; ++i) {
+    size_t n = (static_cast<size_t>(i) * 2654435761u) % (i % 50 == 0 ? 90000 : 9000);
+    if (i % 97 == 3) n = 0;
+    std::string r(n, '\0');
+    for (size_t k = 0; k < n; ++k) r[k] = static_cast<char>((k * 131 + i * 7) & 0xff);
+    recs.push_back(r);
+  }
+  std::string log;
+  uint32_t bo = 0;
+  size_t i0 = 0;
+  uint64_t n_phys = 0;
+  const uint32_t hs = recyclable ? 11 : 7;
+  WalWriteGroup g(recyclable, log_number);
+  while (i0 < recs.size()) {  // write groups of 1..37 records
+    const size_t i1 = std::min(recs.size(), i0 + 1 + (i0 * 7) % 37);
+    std::vector<ByteRange> grp;
+    for (size_t i = i0; i < i1; ++i) grp.push_back({recs[i].data(), recs[i].size()});
+    CHECK(g.Frame(grp, bo).ok());
+    log.append(g.data(), g.size());
+    bo = g.end_block_offset();
+    n_phys += g.physical_records();
+    i0 = i1;
+  }
+  CHECK(bo == (log.size() % 32768 ? log.size() % 32768 : (log.empty() ? 0 : 32768)) ||
+        (log.size() % 32768 == 0 && bo == 0));
+  // every physical record: header CRC = Mask(crc32c(header[6..hs) || payload))
+  uint64_t p = 0, seen = 0;
+  bool crc_ok = true;
+  while (p + hs <= log.size()) {
+    if (32768 - p % 32768 < hs) {
+      p += 32768 - p % 32768;
+      continue;
+    }
+    const uint8_t* h = reinterpret_cast<const uint8_t*>(log.data() + p);
+    const uint32_t n = h[4] | (h[5] << 8);
+    uint32_t stored;
+    std::memcpy(&stored, h, 4);
+    crc_ok &= crc32c::Mask(crc32c_ref(h + 6, hs - 6 + n)) == stored;
+    if (recyclable) {
+      uint32_t ln;
+      std::memcpy(&ln, h + 7, 4);
+      crc_ok &= ln == log_number;
+    }
+    p += hs + n;
+    ++seen;
+  }
+  CHECK(crc_ok);
+  CHECK(seen == n_phys && p == log.size());
+  uint8_t* d_log = nullptr;
+  CHECK(hipMalloc(&d_log, log.size() + 256) == hipSuccess);
+  CHECK(hipMemcpy(d_log, log.data(), log.size(), hipMemcpyHostToDevice) == hipSuccess);
+  const uint8_t* host = reinterpret_cast<const uint8_t*>(log.data());
+  WalRecovery rec;
+  CHECK(rec.Recover(d_log, host, log.size(), log_number, 2 /*kPointInTimeRecovery*/).ok());
+  WalRecord r;
+  size_t k = 0;
+  bool same = true;
+  while (rec.Next(&r)) {
+    same &= k < recs.size() && r.size == recs[k].size() &&
+            std::memcmp(r.data, recs[k].data(), r.size) == 0 && r.reports_before.empty();
+    ++k;
+  }
+  CHECK(rec.status().ok());
+  CHECK(same && k == recs.size());
+  CHECK(rec.trailing_reports().empty());
+  // a flipped payload byte in record 300 (the reader drops the rest of its block)
+  uint64_t off300 = 0;
+  {
+    WalRecovery r2;
+    CHECK(r2.Recover(d_log, host, log.size(), log_number, 2).ok());
+    for (int j = 0; j <= 300 && r2.Next(&r); ++j) off300 = r.offset;
+  }
+  std::string bad = log;
+  const uint64_t flip = off300 + (32768 - off300 % 32768 < hs ? 32768 - off300 % 32768 : 0) + hs;
+  bad[flip] ^= 0x04;
+  CHECK(hipMemcpy(d_log, bad.data(), bad.size(), hipMemcpyHostToDevice) == hipSuccess);
+  const uint8_t* bhost = reinterpret_cast<const uint8_t*>(bad.data());
+  CHECK(rec.Recover(d_log, bhost, bad.size(), log_number, 2).ok());
+  k = 0;
+  same = true;
+  bool reported = false;
+  while (rec.Next(&r)) {
+    if (r.offset < off300) {
+      same &= r.size == recs[k].size() && std::memcmp(r.data, recs[k].data(), r.size) == 0;
+      ++k;
+    } else if (!r.reports_before.empty() && !reported) {
+      reported = r.reports_before[0].Text() == "checksum mismatch" &&
+                 r.reports_before[0].offset <= flip;
+    }
+  }
+  CHECK(same && k == 300);
+  CHECK(reported);
+  CHECK(rec.result().n_reports >= 1);
+  std::printf("wal%s: %zu records, %llu physical, %zu log bytes\n", recyclable ? " (recyclable)" : "",
+              recs.size(), static_cast<unsigned long long>(n_phys), log.size());
+  (void)hipFree(d_log);
+}
+
 int main(int argc, char** argv) {
   const std::string mode = argc > 1 ? argv[1] : "pure";
   pure();
   if (mode == "gpu") gpu();
   if (mode == "threads") threads();
+  if (mode == "wal") {
+    wal(false);
+    wal(true);
+  }
   std::printf(g_fail ? "FAIL (%d)\n" : "PASS\n", g_fail);
   return g_fail ? 1 : 0;
 }

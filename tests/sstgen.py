@@ -141,8 +141,18 @@ class SstWriter:
     metaindex"""
 
     def __init__(self, fv=5, ctype=1, index_type=0, base_context=0, restart_interval=1,
-                 seed=1, codec=None):
+                 seed=1, codec=None, compression=None, compressible_values=False):
+        """compression: None, or "snappy" -- data blocks, index blocks and
+        index partitions go through the real snappy library (pyarrow's
+        bundled copy, snappy::RawCompress as Snappy_Compress calls it,
+        util/compression.h:713-727) and are kept compressed when the ratio is
+        good (GoodCompressionRatio, block_based_table_builder.cc:108-114,
+        with the default max_compressed_bytes_per_kb = 896), with compression type byte 1 (kSnappyCompression);
+        metaindex and properties stay uncompressed as the reference writes
+        them (block_based_table_builder.cc:1728, :2010)"""
         self.codec = codec or PyCodec()
+        self.compression = compression
+        self.compressible_values = compressible_values
         self.fv, self.ctype, self.index_type = fv, ctype, index_type
         self.bcc = base_context if fv >= 6 else 0
         self.ri = restart_interval
@@ -151,7 +161,19 @@ class SstWriter:
         self.blocks = []  # (kind, offset, size)
         self.rng = np.random.default_rng(seed)
 
+    def _maybe_compress(self, contents):
+        if self.compression is None:
+            return contents, 0
+        assert self.compression == "snappy", self.compression
+        import pyarrow as pa
+        c = pa.Codec("snappy").compress(contents, asbytes=True)
+        if len(c) <= (896 * len(contents)) >> 10:
+            return c, 1
+        return contents, 0
+
     def write_block(self, contents, kind, ctype_byte=0):
+        if kind in ("data", "index", "partition") and self.compression and ctype_byte == 0:
+            contents, ctype_byte = self._maybe_compress(contents)
         off = len(self.f)
         n = len(contents)
         self.f += contents + self.codec.trailer(self.ctype, contents, ctype_byte, self.bcc, off)
@@ -164,6 +186,8 @@ class SstWriter:
         for k in range(nkeys):
             key = b"user%010d" % (first + k) + struct.pack("<Q", (first + k) << 8 | 1)
             val = self.rng.integers(0, 256, int(self.rng.integers(10, 300)), np.uint8).tobytes()
+            if self.compressible_values:  # Flink-state-like values: repetitive
+                val = (b"flink-state:%06d;" % (first + k)) * (1 + len(val) // 18)
             ents.append((key, val, None))
             keys.append(key)
         return self.codec.block(16, True, False, ents), keys

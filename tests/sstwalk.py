@@ -11,7 +11,9 @@ rewrite.  Follows:
   metaindex   table/meta_blocks.cc (name -> BlockHandle)
   compression util/compression.h: compress_format_version 2 (fv >= 2) puts a
               varint32 uncompressed size in front; zlib is raw deflate
-              (windowBits -14), as Zlib_Compress writes it
+              (windowBits -14), as Zlib_Compress writes it; Snappy keeps its
+              own length prefix in both versions (compression.h:711) and is
+              decoded by the real snappy library bundled with pyarrow
 """
 import struct
 import zlib
@@ -68,7 +70,11 @@ def contents(data, h, fv):
     t = data[off + n]
     if t == 0:
         return raw
-    assert t == 2, f"codec {t} (only zlib in the reference-built fixtures)"
+    if t == 1:
+        import pyarrow as pa
+        n_out, _ = varint(raw, 0)
+        return pa.Codec("snappy").decompress(raw, decompressed_size=n_out, asbytes=True)
+    assert t == 2, f"codec {t} (zlib or snappy in the fixtures)"
     p = 0
     if fv >= 2:
         _, p = varint(raw, 0)

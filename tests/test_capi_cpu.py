@@ -91,6 +91,58 @@ def test_wal_layout_matches_writer_framing(recyclable):
     assert ((offs % 32768) + hs + l <= 32768).all()
 
 
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_layout_at_continues_a_writer(recyclable):
+    """forst_wal_layout_at frames a write group from the writer's current
+    block offset (log::Writer::block_offset_): the log framed in pieces --
+    every split point, offsets shifted by the bytes already written -- is the
+    log framed at once, and the end block offset is the next piece's start"""
+    import numpy as np
+    from forst_amd import workload
+    L = _lib.lib()
+    rng = np.random.default_rng(4)
+    lens = np.concatenate([workload.log_uniform_lengths(400, 1, 70000, 0xF0E57000AA),
+                           (32768 - 11 - rng.integers(0, 12, 40)).astype(np.uint32),
+                           np.zeros(3, np.uint32)]).astype(np.uint32)
+    rng.shuffle(lens)
+    whole, wl, wt, _, _, wtot = workload.wal_layout(lens, recyclable)
+
+    def piece(ls, bo):
+        ls = np.ascontiguousarray(ls, np.uint32)
+        cap = 4 * len(ls) + 8
+        o = np.zeros(cap, np.uint64)
+        ln = np.zeros(cap, np.uint32)
+        t = np.zeros(cap, np.uint8)
+        npad, nph, tot, end = (ctypes.c_uint64(), ctypes.c_uint64(), ctypes.c_uint64(),
+                               ctypes.c_uint32())
+        _lib.check(L.forst_wal_layout_at(ls.ctypes.data, len(ls), int(recyclable), bo,
+                                         o.ctypes.data, ln.ctypes.data, t.ctypes.data, cap,
+                                         None, None, 0, ctypes.byref(nph), ctypes.byref(npad),
+                                         ctypes.byref(tot), ctypes.byref(end)))
+        k = nph.value
+        return o[:k], ln[:k], t[:k], tot.value, end.value
+
+    cuts = np.unique(np.concatenate([[0, len(lens)], rng.integers(0, len(lens), 25)]))
+    pos, bo = 0, 0
+    got_o, got_l, got_t = [], [], []
+    for a, b in zip(cuts[:-1], cuts[1:]):
+        o, ln, t, tot, end = piece(lens[a:b], bo)
+        got_o.append(o + np.uint64(pos))
+        got_l.append(ln)
+        got_t.append(t)
+        pos += tot
+        assert end % 32768 == pos % 32768
+        bo = end
+    assert pos == wtot
+    assert (np.concatenate(got_o) == whole).all()
+    assert (np.concatenate(got_l) == wl).all() and (np.concatenate(got_t) == wt).all()
+    # block_offset = 0 is forst_wal_layout
+    o, ln, t, tot, end = piece(lens, 0)
+    assert (o == whole).all() and tot == wtot
+    with pytest.raises(Exception):
+        piece(lens[:3], 32769)
+
+
 def test_wal_layout_capacity_errors():
     import numpy as np
     from forst_amd import ForstError

@@ -639,3 +639,76 @@ def test_full_size_c5_record_xxh3():
         parts = [host(w.log[int(w.rec_offsets[i]) + 7:int(w.rec_offsets[i]) + 7 +
                             int(w.rec_lengths[i])]) for i in range(starts[j], ends[j])]
         assert int(hh[j]) == O.xxh3_64(np.concatenate(parts).tobytes()), j
+
+
+def test_c4_full_volume_sharded_on_one_gpu():
+    """C4 at its stated volume (BASELINE configs[3]): 64 GiB of 16 KiB kCRC32c
+    blocks (4 M descriptors, bench.py describe("C4", 8)), split into the 8
+    byte-balanced shards shard.rank_slice gives the ranks of an 8-GPU node
+    (db/compaction/compaction_job.cc:1123 -> block_based_table_reader.cc:2491:
+    independent blocks, no exchange).  On one MI355X (288 GB) each shard is
+    verified in turn exactly as its rank would -- its own view of the buffer
+    starting at the shard's first byte, offsets relative to it -- and:
+    the shards are the equal contiguous eighths;
+    the 8 results concatenated equal one unsplit 4 M-descriptor call; an
+    oracle sample per shard (first, last and 254 random blocks) matches; a
+    flip on each side of every shard boundary is reported once, by the
+    shard that owns the block, and by the unsplit call."""
+    from forst_amd import shard
+    world = 8
+    n = (1 << 19) * world
+    seed = workload.SEEDS["C4"]
+    sizes_all = workload.block_sizes(n, 16384, seed)
+    b = workload.make_sst_batch(n, 16384, seed, ctype=CT.kCRC32c)
+    assert b.total == n * (16384 + 5) and b.total >= 64 << 30
+    comp_all, st_all, ok_all, bad_all = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets,
+                                                                  b.sizes)
+    assert int(host(bad_all)[0]) == 0
+    offs = host(b.offsets)
+    slices = [shard.rank_slice(sizes_all, r, world) for r in range(world)]
+    assert [s[0] for s in slices] == [r * (n // world) for r in range(world)]  # equal sizes
+    assert slices[-1][1] == n and all(slices[r][1] == slices[r + 1][0] for r in range(world - 1))
+    rng = np.random.default_rng(44)
+
+    def run_shards():
+        comps, oks, bads = [], [], []
+        for lo, hi, start in slices:
+            end = int(offs[hi - 1]) + 16384 + 5
+            assert start == int(offs[lo])
+            # the rank's own buffer: the shard's bytes from its first block on
+            # (bench.py run_config: make_sst_batch(..., stream_start=start))
+            own = torch.empty((end - start + 255) // 256 * 256, dtype=torch.uint8, device=DEV)
+            own[:end - start].copy_(b.base[start:end])
+            c, _, ok, bad = engine.block_verify_batch(CT.kCRC32c, own[:end - start],
+                                                      b.offsets[lo:hi] - start, b.sizes[lo:hi])
+            del own
+            comps.append(host(c))
+            oks.append(host(ok))
+            bads.append(int(host(bad)[0]))
+        return np.concatenate(comps), np.concatenate(oks), bads
+
+    comp, ok, bads = run_shards()
+    assert bads == [0] * world and ok.all()
+    # a rank generating its shard on its own (bench.py run_config) has those bytes
+    lo, hi, start = slices[5]
+    rb = workload.make_sst_batch(hi - lo, None, seed, ctype=CT.kCRC32c, sizes=sizes_all[lo:hi],
+                                 stream_start=start)
+    assert torch.equal(rb.base, b.base[start:start + rb.total])
+    del rb
+    assert (comp == host(comp_all)).all()
+    for lo, hi, _ in slices:
+        for i in np.unique(np.concatenate([[lo, hi - 1], rng.integers(lo, hi, 254)])):
+            o = int(offs[i])
+            want = O.compute_builtin_checksum(int(CT.kCRC32c), host(b.base[o:o + 16385]))
+            assert int(comp[i]) == want, i
+    # a flip in the last block of every shard and the first block of the next
+    victims = sorted({s[1] - 1 for s in slices[:-1]} | {s[0] for s in slices[1:]})
+    assert len(victims) == 2 * (world - 1)
+    pos = offs[victims].astype(np.int64) + np.array([7, 16383] * (world - 1), np.int64)
+    b.base[torch.from_numpy(pos).to(DEV)] ^= 0x40
+    comp, ok, bads = run_shards()
+    assert bads == [1] + [2] * (world - 2) + [1]
+    assert np.nonzero(ok == 0)[0].tolist() == victims
+    _, _, ok_all, bad_all = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
+    assert int(host(bad_all)[0]) == len(victims)
+    assert np.nonzero(host(ok_all) == 0)[0].tolist() == victims

@@ -39,3 +39,14 @@ def test_concurrent_host_threads_share_the_engine(tmp_path):
     r = subprocess.run([exe, "threads"], capture_output=True, text=True, timeout=300)
     assert r.returncode == 0 and "PASS" in r.stdout and "failures 0" in r.stdout, \
         r.stdout + r.stderr
+
+
+def test_wal_shim_write_group_and_recovery(tmp_path):
+    """forst_gpu::WalWriteGroup frames write groups from the writer's block
+    offset with every CRC from one launch (db/log_writer.cc:65-160, :228-263),
+    and forst_gpu::WalRecovery hands the records back in reader order with
+    the reader's reports (db/db_impl/db_impl_open.cc:1195-1260), legacy and
+    recyclable logs"""
+    exe = _build(tmp_path)
+    r = subprocess.run([exe, "wal"], capture_output=True, text=True, timeout=300)
+    assert r.returncode == 0 and "PASS" in r.stdout, r.stdout + r.stderr

@@ -337,3 +337,83 @@ def test_short_file_message():
     r = sst.verify_file(bytes(10), file_name="/db/000001.sst")
     assert r.message.decode() == ("Corruption: file is too short (10 bytes) to be an sstable: "
                                   "/db/000001.sst")
+
+
+# ---- Snappy-compressed files (ForSt's default compression) -----------------
+SNAPPY_CASES = [(5, 1, 0, 1), (6, 4, 2, 4), (2, 1, 3, 1), (4, 4, 2, 1)]
+
+
+def make_snappy(fv, ct, it, ri, seed=13, **kw):
+    """index blocks, index partitions and data blocks written through the real
+    snappy library (type byte 1), as a column family with ForSt's default
+    compression (options/options.cc:123) and enable_index_compression (the
+    default, include/rocksdb/table.h:526) writes them"""
+    pytest.importorskip("pyarrow")
+    w = sstgen.SstWriter(fv=fv, ctype=ct, index_type=it, base_context=0x5EED1234 + seed,
+                         restart_interval=ri, seed=seed, compression="snappy",
+                         compressible_values=True)
+    return w, w.build(**kw)
+
+
+@pytest.mark.parametrize("fv,ct,it,ri", SNAPPY_CASES)
+def test_snappy_file_structure_decodes_on_the_host(fv, ct, it, ri):
+    """every Snappy structural block of the file decodes through the
+    product's decoder (forst_block_uncompress) to what the real snappy
+    library makes of it, and the decoded index lists the data blocks"""
+    import ctypes
+
+    import sstwalk
+    from forst_amd._lib import lib
+    w, f = make_snappy(fv, ct, it, ri)
+    blocks, foot = sstwalk.walk(f)
+    assert sstwalk.tiles(blocks, foot)
+    types = {(k, t) for k, _, _, t in blocks}
+    assert ("index", 1) in types and ("data", 1) in types
+    if it == 2:
+        assert ("index_partition", 1) in types
+    for k, o, n, t in blocks:
+        if t != 1 or k == "data":
+            continue
+        want = sstwalk.contents(f, (o, n), fv)
+        out = np.zeros(len(want) + 16, np.uint8)
+        got_n = ctypes.c_uint64()
+        err = ctypes.c_char_p()
+        src = np.frombuffer(f[o:o + n], np.uint8)
+        rc = lib().forst_block_uncompress(1, fv, src.ctypes.data, n, out.ctypes.data, len(out),
+                                          ctypes.byref(got_n), ctypes.byref(err))
+        assert rc == 0, err.value
+        assert out[:got_n.value].tobytes() == want
+    assert [(o, n) for k, o, n, _ in blocks if k == "data"] == blocks_of(w, "data")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("fv,ct,it,ri", SNAPPY_CASES)
+def test_verify_snappy_file(fv, ct, it, ri):
+    """forst_sst_verify_file walks a Snappy-compressed index (and its
+    partitions) on the host and verifies every block on the GPU; a corrupted
+    data block is named with the reference's text; a Snappy index whose
+    checksum is intact but whose stream is broken gives UncompressBlockData's
+    Status (table/format.cc:654-667)"""
+    name = "/flink/db/000123.sst"
+    w, f = make_snappy(fv, ct, it, ri)
+    r = sst.verify_file(f, file_name=name)
+    assert r.status == 0, r.message
+    assert r.data_blocks == 40 and r.n_failed == 0
+    assert r.index_partitions == (5 if it == 2 else 0)
+    data = blocks_of(w, "data")
+    b = bytearray(f)
+    o, n = data[17]
+    b[o + n // 3] ^= 0x10
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.status == 2 and r.n_failed == 1
+    assert r.message.decode() == _expected_mismatch(w, bytes(b), o, n, name)
+    # the index stream's length preamble off by one, trailer re-signed
+    io, in_ = blocks_of(w, "index")[0]
+    assert f[io + in_] == 1
+    b = bytearray(f)
+    b[io] ^= 0x01
+    b[io + in_:io + in_ + 5] = sstgen.PyCodec().trailer(w.ctype, bytes(b[io:io + in_]), 1,
+                                                        w.bcc, io)
+    r = sst.verify_file(bytes(b), file_name=name)
+    assert r.status != 0
+    assert r.message.decode() == "Corruption: Corrupted compressed block contents: Snappy"

@@ -116,3 +116,170 @@ def test_recover_dense_tiny_records():
         reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
         compare(recs, reps, res, log, 7, mode, "dense")
     assert time.perf_counter() - t0 < 120
+
+
+
+def clean_expectation(rec_offsets, rec_lengths, rec_types, hashes):
+    """the records a clean, writer-laid-out log recovers to: (offset, length,
+    hash, n_fragments) per logical record, and the first-fragment indices"""
+    nphys = len(rec_offsets)
+    starts = np.nonzero((rec_types == 1) | (rec_types == 2))[0]
+    ends = np.concatenate([starts[1:], [nphys]])
+    cum = np.concatenate([[0], np.cumsum(rec_lengths.astype(np.int64))])
+    # Reader::LastRecordOffset is where the reader stood when it went for the
+    # record's first fragment: for a header at a log-block start that is the
+    # end of the previous physical record, in front of the writer's zero pad
+    # (log_reader.cc:89-92 computes physical_record_offset before
+    # ReadPhysicalRecord skips the < 7-byte block tail)
+    offs = rec_offsets.astype(np.int64)
+    hdr = offs[starts]
+    prev = np.maximum(starts - 1, 0)
+    prev_end = np.where(starts > 0, offs[prev] + 7 + rec_lengths[prev].astype(np.int64), 0)
+    reported = np.where(hdr % 32768 == 0, prev_end, hdr)
+    return {"offset": reported,
+            "length": cum[ends] - cum[starts],
+            "hash": np.asarray(hashes).view(np.int64),
+            "n_fragments": (ends - starts).astype(np.int32)}, starts, ends
+
+
+def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode):
+    """What the serial reader returns on a writer-laid-out log after one
+    payload flip in each of the log blocks `vblocks` (physical records
+    `victims`, >= 8 blocks apart): the clean records outside the damaged
+    windows, and inside each window what oracle/wal_reader.py returns when
+    replayed from the start of the logical record holding the flip
+    (wal_reader.resume_at) to four blocks past it, cut at the first record
+    start at least two blocks past the flip (where the reader's state is
+    clean again).  Returns (offsets, lengths, hashes as uint64, reports)."""
+    n = len(exp["offset"])
+    windows = []
+    for i, v in zip(victims, vblocks):
+        li = int(np.searchsorted(starts, i, side="right")) - 1
+        o_start = int(exp["offset"][li])
+        j = int(np.searchsorted(exp["offset"], (int(v) + 2) * 32768, side="left"))
+        cutoff = int(exp["offset"][j]) if j < n else total
+        windows.append((o_start, cutoff, min(total, (int(v) + 4) * 32768)))
+    assert all(windows[k][1] <= windows[k + 1][0] for k in range(len(windows) - 1))
+    outside = np.ones(n, bool)
+    for o_start, cutoff, _ in windows:
+        outside[(exp["offset"] >= o_start) & (exp["offset"] < cutoff)] = False
+    win_recs, want_reps = [], []
+    for o_start, cutoff, end in windows:
+        b0 = o_start // 32768 * 32768
+        r = R.resume_at(R.Reader(read_window(b0, end)), o_start - b0)
+        while True:
+            got = r.read_record(mode)
+            if got is None:
+                break
+            off, payload, h = got
+            if off + b0 < cutoff:
+                win_recs.append((off + b0, len(payload), h))
+        want_reps += [(nb_, why, p + b0) for nb_, why, p in r.reports if p + b0 < cutoff]
+    wo = np.concatenate([exp["offset"][outside], np.array([t[0] for t in win_recs], np.int64)])
+    wl = np.concatenate([exp["length"][outside], np.array([t[1] for t in win_recs], np.int64)])
+    wh = np.concatenate([exp["hash"][outside].view(np.uint64),
+                         np.array([t[2] for t in win_recs], np.uint64)])
+    order = np.argsort(wo, kind="stable")
+    return wo[order], wl[order], wh[order], want_reps, outside
+
+
+def pick_flips(rng, rec_offsets, rec_lengths, n_log_blocks, k):
+    """k log blocks >= 8 apart, a physical record with payload in each, and
+    one payload byte of it: (victims, blocks, byte positions)"""
+    vblocks = np.sort(rng.choice(np.arange(4, n_log_blocks - 8, 8), k, replace=False))
+    blk_of = (rec_offsets // 32768).astype(np.int64)
+    victims = np.array([int(rng.choice(np.nonzero((blk_of == v) & (rec_lengths > 0))[0]))
+                        for v in vblocks])
+    pos = rec_offsets[victims].astype(np.int64) + 7 + \
+        rng.integers(0, rec_lengths[victims].astype(np.int64))
+    return victims, vblocks, pos
+
+
+@pytest.mark.parametrize("mode", [R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords])
+def test_windowed_expectation_equals_full_replay(mode):
+    """the composition the full-size GPU test relies on, checked on a log the
+    serial reader replays whole: clean records + per-flip windows replayed
+    from resume_at == read_all over the entire corrupted log"""
+    from oracle import oracle as O
+    rng = np.random.default_rng(8)
+    lens = (np.exp(rng.uniform(np.log(32), np.log(32768), 2500))).astype(np.uint32)
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), np.uint8)
+    log, po, pl = O.wal_frame(payload, lens)
+    types = np.array([log[int(o) + 6] for o in po], np.uint8)
+    cuml = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
+    hashes = np.array([O.xxh3_64(payload[cuml[j]:cuml[j + 1]].tobytes())
+                       for j in range(len(lens))], np.uint64)
+    exp, starts, _ = clean_expectation(po.astype(np.uint64), pl, types, hashes)
+    nblk = (len(log) + 32767) // 32768
+    victims, vblocks, pos = pick_flips(rng, po.astype(np.uint64), pl, nblk, 6)
+    bad = log.copy()
+    bad[pos] ^= 1
+    wo, wl, wh, reps, _ = windowed_expectation(lambda a, b: bad[a:b], exp, starts, victims,
+                                               vblocks, len(bad), mode)
+    recs, want_reps = R.read_all(bad, 0, mode)
+    assert [(int(a), int(b), int(c)) for a, b, c in zip(wo, wl, wh)] == recs
+    assert reps == want_reps
+
+
+@pytest.mark.gpu
+def test_full_size_c5_recovery():
+    """f2 at the bench's size (C5: 10 M logical records, ~44 GiB log, the log
+    bench.py times).  Clean log, PIT and skip modes: every record's (offset,
+    length, XXH3, fragment count) equals the writer's layout plus the a14
+    kernel's hashes (forst_wal_record_xxh3_batch), and 2000 sampled hashes the
+    oracle's XXH3 over the gathered payload.  Then one payload byte flipped in
+    each of 48 log blocks (>= 8 blocks apart): every record and every report
+    equals the serial reader's (oracle/wal_reader.py, db/log_reader.cc:69-531)
+    -- around each flip the reader is replayed from the start of the logical
+    record holding it to past the recovery point, elsewhere the clean
+    expectation holds."""
+    import torch
+    from forst_amd import engine, workload
+    n = 10_000_000
+    w = workload.make_wal_batch(n, workload.SEEDS["C5"])
+    DEV = w.log.device
+    nphys = len(w.rec_offsets)
+    h_a14, _ = engine.wal_record_xxh3_batch(w.log, torch.from_numpy(
+        w.rec_offsets.view(np.int64)).to(DEV))
+    exp, starts, ends = clean_expectation(w.rec_offsets, w.rec_lengths, w.rec_types,
+                                          h_a14.cpu().numpy())
+    assert len(starts) == n
+    keys = ("offset", "length", "hash", "n_fragments")
+
+    def recover(mode):
+        rec, rep, res = engine.wal_recover_batch(w.log, 0, mode, record_capacity=n + 1024)
+        assert res.n_physical == nphys
+        return ({k: rec[k].cpu().numpy() for k in keys},
+                [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")], res)
+
+    for mode in (R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords):
+        got, _, res = recover(mode)
+        assert res.n_records == n and res.n_reports == 0
+        for k in keys:
+            assert (got[k] == exp[k]).all(), (mode, k)
+    from oracle import oracle as O
+    rng = np.random.default_rng(3)
+    for j in rng.choice(n, 2000, replace=False):
+        parts = [w.log[int(w.rec_offsets[i]) + 7:int(w.rec_offsets[i]) + 7 +
+                       int(w.rec_lengths[i])].cpu().numpy() for i in range(starts[j], ends[j])]
+        assert int(exp["hash"][j]) & (2**64 - 1) == O.xxh3_64(np.concatenate(parts).tobytes())
+
+    # ---- 48 flipped payload bytes, one per chosen log block ----------------
+    victims, vblocks, pos = pick_flips(rng, w.rec_offsets, w.rec_lengths, w.n_log_blocks, 48)
+    w.log[torch.from_numpy(pos).to(DEV)] ^= 0x01
+    for mode in (R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords):
+        wo, wl, wh, want_reps, outside = windowed_expectation(
+            lambda a, b: w.log[a:b].cpu().numpy(), exp, starts, victims, vblocks, w.total, mode)
+        got, reps, res = recover(mode)
+        assert len(got["offset"]) == len(wo), (mode, len(got["offset"]), len(wo))
+        assert np.array_equal(got["offset"], wo), mode
+        assert np.array_equal(got["length"], wl), mode
+        assert np.array_equal(got["hash"].view(np.uint64), wh), mode
+        # outside the windows the fragment counts are the clean layout's
+        sel = np.isin(got["offset"], exp["offset"][outside])
+        assert (got["n_fragments"][sel] == exp["n_fragments"][outside]).all()
+        po, pb, pr, pt = reps
+        gr = [(int(b), reason_text(int(r_), int(t) & 0xFFFFFFFF), int(o))
+              for o, b, r_, t in zip(po, pb, pr, pt)]
+        assert gr == want_reps, (mode, gr[:4], want_reps[:4])
+        assert sum(1 for g in gr if g[1] == "checksum mismatch") == len(victims)

@@ -65,7 +65,47 @@ Status WriterSnippet(const BlockBasedTableOptions& table_options, BuilderRep* r,
   return s;
 }
 
+// the surroundings of DBImpl::RecoverLogFiles' read loop
+// (db/db_impl/db_impl_open.cc:1195-1260): its reporter, options and log
+Status WalRecoverSnippet(log::Reader::Reporter& reporter, WALRecoveryMode wal_recovery_mode,
+                         uint64_t wal_number, void* stream, const uint8_t* d_log,
+                         const uint8_t* host_log, uint64_t log_len) {
+  Status status;
+@WAL_RECOVER@
+  return status;
+}
+
+// the fields of log::Writer (db/log_writer.h) the write-group member uses
+struct WalWriterFields {
+  std::unique_ptr<WritableFileWriter> dest_;
+  size_t block_offset_ = 0;
+  uint64_t log_number_ = 0;
+  bool recycle_log_files_ = false;
+  IOStatus AddRecordGroup(const std::vector<Slice>& group, void* stream) {
+@WAL_WRITER@
+    return s;
+  }
+};
+
 }  // namespace ROCKSDB_NAMESPACE
+'''
+
+# keeps every snippet function (and what it reaches) in the linked program
+MAIN = r'''
+#include <cstdio>
+namespace ROCKSDB_NAMESPACE {
+Status VerifySnippet(const Footer&, void*, const uint8_t*, uint64_t, const uint64_t*,
+                     const uint32_t*, uint64_t, const std::string&,
+                     const std::vector<uint64_t>&, Statistics*);
+}
+int main(int argc, char**) {
+  using namespace ROCKSDB_NAMESPACE;
+  void* fns[] = {reinterpret_cast<void*>(&VerifySnippet), reinterpret_cast<void*>(&WriterSnippet),
+                 reinterpret_cast<void*>(&WalRecoverSnippet),
+                 reinterpret_cast<void*>(&WalWriterFields::AddRecordGroup)};
+  if (argc > 99) std::printf("%p", fns[argc % 4]);  // never run: link check only
+  return 0;
+}
 '''
 
 
@@ -83,22 +123,91 @@ def split_includes(code):
     return inc, body
 
 
+SNIPPETS = {"verify": "@VERIFY@", "writer": "@WRITER@", "wal_recover": "@WAL_RECOVER@",
+            "wal_writer": "@WAL_WRITER@"}
+
+
+def integration_source():
+    sn = snippets()
+    assert set(SNIPPETS) <= set(sn), sn.keys()
+    incs, src = [], TEMPLATE
+    for name, mark in SNIPPETS.items():
+        inc, body = split_includes(sn[name])
+        incs += inc
+        src = src.replace(mark, body)
+    return src.replace("@INCLUDES@", "\n".join(sorted(set(incs))))
+
+
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "rocksdb")),
                     reason="needs the reference headers (/root/reference)")
 def test_integration_snippets_compile_inside_forst(tmp_path):
-    sn = snippets()
-    assert {"verify", "writer"} <= set(sn), sn.keys()
-    inc_v, body_v = split_includes(sn["verify"])
-    inc_w, body_w = split_includes(sn["writer"])
-    src = (TEMPLATE.replace("@INCLUDES@", "\n".join(sorted(set(inc_v + inc_w))))
-           .replace("@VERIFY@", body_v).replace("@WRITER@", body_w))
+    """INTEGRATION.md's four call-site snippets (block verify, table writer,
+    WAL recovery loop, WAL write group) type-check against the reference's
+    own headers (db/log_reader.h, db/log_writer.h, db/write_batch_internal.h
+    for the WAL ones)"""
     f = tmp_path / "integration_snippets.cc"
-    f.write_text(src)
+    f.write_text(integration_source())
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror=shadow",
                         "-DROCKSDB_PLATFORM_POSIX", "-DOS_LINUX", f"-I{REF}",
                         f"-I{REF}/include", f"-I{os.path.join(ROOT, 'include')}", str(f)],
                        capture_output=True, text=True)
     assert r.returncode == 0, r.stderr[-4000:]
+
+
+def _archive_ready():
+    import sys
+    sys.path.insert(0, os.path.join(ROOT, "tests", "golden"))
+    import refbuild
+    if not os.path.isdir(os.path.join(REF, "include", "rocksdb")):
+        return None, "needs the reference sources (/root/reference)"
+    if os.environ.get("FORST_LINK_CHECK") == "0":
+        return None, "FORST_LINK_CHECK=0"
+    # builds the archive when it is not cached (~3 min on 8 cores, once)
+    return refbuild, None
+
+
+def test_integration_snippets_link_against_reference_objects(tmp_path):
+    """Link check of the boundary (not run): the four snippets, compiled with
+    the reference archive's own flags, plus the C++ shim's sources
+    (engine_shim.cc, wal_shim.cc, table_writer.cc, sst_host.cc: what a ForSt
+    build embedding the shim compiles) are linked into one program with the
+    reference's library objects (tests/golden/refbuild.py: src.mk's
+    LIB_SOURCES compiled from /root/reference, only the members the program
+    reaches) and the product library for the C ABI, with no undefined
+    symbol allowed (-z defs) -- so no symbol of namespace forstdb is
+    defined twice and every reference symbol the snippets use
+    (WriteBatchInternal::SetContents / UpdateProtectionInfo,
+    WritableFileWriter::Append, Status, RecordTick ...) resolves."""
+    refbuild, why = _archive_ready()
+    if refbuild is None:
+        pytest.skip(why)
+    lib = refbuild.build_archive()
+    inc = [f"-I{REF}", f"-I{REF}/include", f"-I{os.path.join(ROOT, 'include')}",
+           "-I/opt/rocm/include", "-D__HIP_PLATFORM_AMD__"]
+    src = tmp_path / "integration_snippets.cc"
+    src.write_text(integration_source() + MAIN)
+    csrc = os.path.join(ROOT, "forst_amd", "csrc")
+    objs = []
+    for f in [str(src)] + [os.path.join(csrc, n) for n in
+                           ("engine_shim.cc", "wal_shim.cc", "table_writer.cc", "sst_host.cc")]:
+        o = str(tmp_path / (os.path.basename(f) + ".o"))
+        r = subprocess.run(["g++"] + refbuild.CXXFLAGS + inc + ["-c", f, "-o", o],
+                           capture_output=True, text=True)
+        assert r.returncode == 0, (f, r.stderr[-4000:])
+        objs.append(o)
+    libdir = os.path.join(ROOT, "forst_amd", "lib")
+    exe = str(tmp_path / "integration_link")
+    r = subprocess.run(["g++"] + refbuild.CXXFLAGS + ["-o", exe] + objs +
+                       ["-Wl,--gc-sections", "-Wl,-z,defs", "-Wl,--no-undefined", lib,
+                        f"-L{libdir}", "-lforst_checksum", "-L/opt/rocm/lib", "-lamdhip64",
+                        "-lz", "-lpthread", "-ldl"], capture_output=True, text=True)
+    assert r.returncode == 0, r.stderr[-6000:]
+    syms = subprocess.run(["nm", "-C", "--defined-only", exe], capture_output=True,
+                          text=True).stdout
+    # the program really holds reference code and the shim side by side
+    assert "rocksdb::WriteBatchInternal::SetContents" in syms or \
+        "forstdb::WriteBatchInternal::SetContents" in syms
+    assert "forst_gpu::WalRecovery::Next" in syms and "forst_gpu::WalWriteGroup::Frame" in syms
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "rocksdb")),

@@ -31,7 +31,10 @@ constexpr uint32_t kRowsWaves = 12;
 constexpr uint32_t kRowsThreads = kRowsWaves * 64;
 // workgroup-feed batch (stream_common.h): 4 descriptors, one per row (A/B
 // against 8: C3 +0.4-0.6 %, NS16X +0.7 %; 16 was 1 % slower than 8)
-constexpr uint32_t kXxWgChunk = 4;
+#ifndef FORST_XX_WG_CHUNK
+#define FORST_XX_WG_CHUNK 4
+#endif
+constexpr uint32_t kXxWgChunk = FORST_XX_WG_CHUNK;
 // the fragment kernel (WAL records): 4-wave workgroups and the global feed
 // (the workgroup feed measured 5 % slower on C5's log-uniform records)
 constexpr bool kFragWg = false;

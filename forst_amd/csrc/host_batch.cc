@@ -81,11 +81,36 @@ bool is_device_readable_host(const void* p) {
   return at.type == hipMemoryTypeHost;  // pinned or registered
 }
 
-// DMA straight from the caller's pages only if the whole range is pinned or
-// registered: the first and the last byte (a registration that covers part of
-// the range, or was dropped, falls back to staging)
+// ranges registered through forst_host_register: start -> length
+std::mutex g_reg_mu;
+std::map<uintptr_t, uint64_t> g_regs;
+
+// DMA straight from the caller's pages only if ONE pinned allocation or
+// registration covers the whole range: a forst_host_register'ed range, or a
+// hipHostMalloc'ed / otherwise registered allocation whose extent
+// (hipMemGetAddressRange) holds it.  Anything else -- two registrations with
+// unregistered pages between them, a registration over part of the range, a
+// dropped one -- is staged.
 bool range_device_readable(const uint8_t* base, uint64_t len) {
-  return len && is_device_readable_host(base) && is_device_readable_host(base + len - 1);
+  if (!len) return false;
+  const uintptr_t lo = reinterpret_cast<uintptr_t>(base);
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    auto it = g_regs.upper_bound(lo);
+    if (it != g_regs.begin()) {
+      --it;
+      if (it->first <= lo && lo + len <= it->first + it->second) return true;
+    }
+  }
+  if (!is_device_readable_host(base)) return false;
+  void* pb = nullptr;
+  size_t ps = 0;
+  if (hipMemGetAddressRange(&pb, &ps, const_cast<uint8_t*>(base)) != hipSuccess) {
+    (void)hipGetLastError();
+    return false;
+  }
+  const uintptr_t ab = reinterpret_cast<uintptr_t>(pb);
+  return ab <= lo && lo + len <= ab + ps;
 }
 
 enum class Op { kVerify, kChecksum };
@@ -189,6 +214,7 @@ struct DeviceCtx {
   std::condition_variable cv;
   std::function<void()> job;
   bool busy = false;
+  std::mutex res_mu;  // held while the slots' buffers change (reserve / trim) or are read (stats)
 
   explicit DeviceCtx(int dev) : device(dev) {
     worker = std::thread([this] { loop(); });
@@ -222,19 +248,24 @@ struct DeviceCtx {
     cv.wait(lk, [this] { return !busy; });
   }
   // stream and events, once (on the worker's device)
+  // (all or nothing: a partial failure destroys what it created, so a later
+  // call retries from scratch instead of finding a stream without events)
   hipError_t init() {
     if (st) return hipSuccess;
-    hipError_t e = hipStreamCreateWithFlags(&st, hipStreamNonBlocking);
-    if (e != hipSuccess) {
-      st = nullptr;
-      return e;
-    }
+    hipStream_t s0 = nullptr;
+    hipError_t e = hipStreamCreateWithFlags(&s0, hipStreamNonBlocking);
+    if (e != hipSuccess) return e;
     for (Slot& s : slot) {
       if ((e = hipEventCreateWithFlags(&s.done, hipEventDisableTiming)) != hipSuccess) {
-        s.done = nullptr;
+        for (Slot& u : slot) {
+          if (u.done) (void)hipEventDestroy(u.done);
+          u.done = nullptr;
+        }
+        (void)hipStreamDestroy(s0);
         return e;
       }
     }
+    st = s0;
     return hipSuccess;
   }
 };
@@ -303,7 +334,10 @@ void run_device(const HostBatch& b, bool direct, DeviceCtx& cx, DeviceRun& r) {
     c0 = c1;
   }
   for (Slot& s : cx.slot) {
-    if ((e = s.reserve(max_bytes, max_blocks, !direct)) != hipSuccess)
+    std::unique_lock<std::mutex> rl(cx.res_mu);
+    e = s.reserve(max_bytes, max_blocks, !direct);
+    rl.unlock();
+    if (e != hipSuccess)
       return bail(e, "window allocation");
     s.win = -1;
   }
@@ -482,14 +516,37 @@ FORST_API int forst_host_context_stats(uint32_t* contexts, uint64_t* device_byte
                                        uint64_t* pinned_bytes) {
   std::lock_guard<std::mutex> lk(g_pool_mu);
   uint64_t db = 0, pb = 0;
-  for (const DeviceCtx* c : *g_all)
+  for (DeviceCtx* c : *g_all) {
+    std::lock_guard<std::mutex> rl(c->res_mu);
     for (const Slot& s : c->slot) {
       if (s.d) db += s.dbytes + s.blocks * kPerBlock + 64;
       if (s.hbase) pb += s.blocks * kPerBlock + 128 + s.hbytes;
     }
+  }
   if (contexts) *contexts = static_cast<uint32_t>(g_all->size());
   if (device_bytes) *device_bytes = db;
   if (pinned_bytes) *pinned_bytes = pb;
+  return FORST_OK;
+}
+
+// the windows and staging of every context not in use right now go back to
+// the driver (contexts, threads and streams stay; the next call that takes
+// one grows it again)
+FORST_API int forst_host_context_trim(uint64_t* released_bytes) {
+  std::lock_guard<std::mutex> lk(g_pool_mu);
+  uint64_t freed = 0;
+  for (auto& kv : *g_free)
+    for (DeviceCtx* c : kv.second) {
+      std::lock_guard<std::mutex> rl(c->res_mu);
+      (void)hipSetDevice(c->device);
+      for (Slot& s : c->slot) {
+        if (s.d) freed += s.dbytes + s.blocks * kPerBlock + 64;
+        if (s.hbase) freed += s.blocks * kPerBlock + 128 + s.hbytes;
+        s.release();
+        s.win = -1;
+      }
+    }
+  if (released_bytes) *released_bytes = freed;
   return FORST_OK;
 }
 
@@ -503,10 +560,16 @@ FORST_API int forst_host_register(void* p, uint64_t len) {
     e = hipHostRegister(p, len, hipHostRegisterDefault);
   }
   if (e != hipSuccess) return fail(FORST_EHIP, std::string("hipHostRegister: ") + hipGetErrorString(e));
+  std::lock_guard<std::mutex> g(g_reg_mu);
+  g_regs[reinterpret_cast<uintptr_t>(p)] = len;
   return FORST_OK;
 }
 
 FORST_API int forst_host_unregister(void* p) {
+  {
+    std::lock_guard<std::mutex> g(g_reg_mu);
+    g_regs.erase(reinterpret_cast<uintptr_t>(p));
+  }
   const hipError_t e = hipHostUnregister(p);
   if (e != hipSuccess)
     return fail(FORST_EHIP, std::string("hipHostUnregister: ") + hipGetErrorString(e));

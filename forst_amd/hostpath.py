@@ -119,3 +119,11 @@ def context_stats():
     c, d, p = ctypes.c_uint32(), ctypes.c_uint64(), ctypes.c_uint64()
     _check(lib().forst_host_context_stats(ctypes.byref(c), ctypes.byref(d), ctypes.byref(p)))
     return c.value, d.value, p.value
+
+
+def context_trim():
+    """give the buffers of every idle context back to the driver
+    (forst_host_context_trim); returns the bytes released"""
+    r = ctypes.c_uint64()
+    _check(lib().forst_host_context_trim(ctypes.byref(r)))
+    return r.value

@@ -403,29 +403,37 @@ int forst_block_checksum_host(int checksum_type, const uint8_t* host_base, uint6
                               const uint8_t* last_bytes, const uint32_t* modifiers, uint32_t* out,
                               uint64_t n_blocks, const int* devices, int n_devices);
 /* hipHostRegister / hipHostUnregister of a host range (e.g. an mmap'd SST
- * file) so the host-memory calls read it by DMA without staging. */
+ * file) so the host-memory calls read it by DMA without staging.  A batch is
+ * DMA'd in place only when ONE registration (or one pinned allocation) covers
+ * all of it; otherwise it is staged. */
 int forst_host_register(void* p, uint64_t len);
 int forst_host_unregister(void* p);
 const char* forst_host_last_error(void);
 /* The host-memory calls keep one context per device and caller -- worker
  * thread, HIP stream, two device windows, pinned mirrors and staging --
  * created on first use and reused by every later call (buffers only grow).
- * Reports how many contexts exist and the device / pinned bytes they hold. */
+ * forst_host_context_stats reports how many contexts exist and the device /
+ * pinned bytes they hold; forst_host_context_trim gives the buffers of every
+ * context not in use back to the driver (*released_bytes, nullable), e.g.
+ * after a burst of concurrent callers. */
+int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
+                             uint64_t* pinned_bytes);
+int forst_host_context_trim(uint64_t* released_bytes);
 /* BlockFetcher's decompression of one block (table/block_fetcher.cc:333-345,
  * UncompressSerializedBlock, table/format.cc:637-700), host only: the
  * structural blocks the whole-file verify decodes.  compression_type =
- * CompressionType (0 none, 2 Zlib, 3 BZip2, 4 LZ4, 5 LZ4HC, 7 ZSTD; zlib is
- * linked, the others are opened from the system's runtime libraries;
- * 1 Snappy / 6 XPRESS: FORST_EUNSUPPORTED).  format_version >= 2 blocks carry
- * a varint32 size in front (compress_format_version 2).  FORST_ECORRUPT /
- * FORST_EUNSUPPORTED set *err to the reference's message ("Corrupted
- * compressed block contents: Zlib", "Unsupported compression method for this
- * build: Snappy"); FORST_EINVAL if capacity is short (*out_len = size). */
+ * CompressionType (0 none, 1 Snappy, 2 Zlib, 3 BZip2, 4 LZ4, 5 LZ4HC, 7 ZSTD;
+ * zlib is linked, Snappy is decoded here from its published block format, the
+ * others are opened from the system's runtime libraries; 6 XPRESS:
+ * FORST_EUNSUPPORTED).  format_version >= 2 blocks carry a varint32 size in
+ * front (compress_format_version 2; Snappy keeps its own length prefix in
+ * both).  FORST_ECORRUPT / FORST_EUNSUPPORTED set *err to the reference's
+ * message ("Corrupted compressed block contents: Zlib", "Unsupported
+ * compression method for this build: Xpress"); FORST_EINVAL if capacity is
+ * short (*out_len = size). */
 int forst_block_uncompress(uint8_t compression_type, uint32_t format_version,
                            const uint8_t* in, uint64_t n, uint8_t* out, uint64_t capacity,
                            uint64_t* out_len, const char** err);
-int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
-                             uint64_t* pinned_bytes);
 
 /* ---- Write side of flush / compaction with deferred trailers (§8f-3) --------
  * BlockBasedTableBuilder::WriteMaybeCompressedBlock

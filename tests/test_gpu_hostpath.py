@@ -104,6 +104,12 @@ def test_back_to_back_calls_reuse_the_context():
     assert hostpath.context_stats() == s0, (s0, hostpath.context_stats())
     assert torch.cuda.mem_get_info()[0] == free0
     assert s0[0] >= 1 and s0[1] > 0 and s0[2] > 0
+    # trim: idle contexts give their buffers back; the next call grows them again
+    assert hostpath.context_trim() == s0[1] + s0[2]
+    assert hostpath.context_stats() == (s0[0], 0, 0)
+    got = hostpath.block_verify_host(CT.kCRC32c, hb, offs, sizes, devices=(0,))
+    assert (got[0] == want[0]).all() and got[3] == 0
+    assert hostpath.context_stats()[1] > 0
 
 
 def test_out_of_order_descriptors_and_partial_registration():
@@ -130,6 +136,18 @@ def test_out_of_order_descriptors_and_partial_registration():
         comp2, _, ok2, bad2 = hostpath.block_verify_host(CT.kXXH3, buf[:len(hb)], offs, sizes,
                                                          devices=(0,))
         assert bad2 == 0 and (comp2 == want).all()
+        # a second registration over the tail, unregistered pages between the
+        # two: the first and last bytes are both pinned, the batch is still
+        # staged (one registration must cover the whole range)
+        tail = (len(buf) - half) // 2 // 4096 * 4096
+        t0 = len(buf) - tail
+        assert lib().forst_host_register(ptr + t0, tail) == 0
+        try:
+            comp3, _, ok3, bad3 = hostpath.block_verify_host(CT.kXXH3, buf[:len(hb)], offs,
+                                                             sizes, devices=(0,))
+            assert bad3 == 0 and (comp3 == want).all()
+        finally:
+            lib().forst_host_unregister(ptr + t0)
     finally:
         lib().forst_host_unregister(ptr)
         del buf

@@ -20,9 +20,13 @@ offs = w.rec_offsets.astype(np.int64) + 6   # the CRC covers header[6..7) + payl
 lens = w.rec_lengths.astype(np.int64) + 1
 
 
-def timed(sel):
-    o = torch.from_numpy(np.ascontiguousarray(offs[sel])).cuda()
-    n = torch.from_numpy(np.ascontiguousarray(lens[sel]).astype(np.int32)).cuda()
+def timed(sel, order=None):
+    oo, nn = offs[sel], lens[sel]
+    if order is not None:  # descriptors reordered (binning experiments)
+        k = order(nn)
+        oo, nn = oo[k], nn[k]
+    o = torch.from_numpy(np.ascontiguousarray(oo)).cuda()
+    n = torch.from_numpy(np.ascontiguousarray(nn).astype(np.int32)).cuda()
     out = torch.empty(len(o), dtype=torch.uint32, device="cuda")
     for _ in range(2):
         engine.crc32c_batch(w.log, o, n, out=out)
@@ -41,6 +45,15 @@ def timed(sel):
 res = {"all": timed(np.ones(len(offs), bool))}
 for lo, hi in ((0, 64), (64, 128), (128, 256), (256, 512), (512, 1024), (1024, 1 << 20)):
     res[f"{lo}-{hi}"] = timed((lens > lo) & (lens <= hi))
+everything = np.ones(len(offs), bool)
+# descriptors grouped by 1 KiB round count (stable: log order within a group)
+res["by_rounds"] = timed(everything, lambda nn: np.argsort((nn + 1023) // 1024, kind="stable"))
+# ... and in groups of 64 descriptors sorted by round count (a local sort)
+res["by_rounds_local64"] = timed(everything, lambda nn: np.argsort(
+    (np.arange(len(nn)) // 64) * 64 + (nn + 1023) // 1024, kind="stable"))
+res["by_rounds_desc"] = timed(everything, lambda nn: np.argsort(-((nn + 1023) // 1024),
+                                                                kind="stable"))
+res["by_len"] = timed(everything, lambda nn: np.argsort(nn, kind="stable"))
 res["le512"] = timed(lens <= 512)
 res["gt512"] = timed(lens > 512)
 print(json.dumps(res), flush=True)

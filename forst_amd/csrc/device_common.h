@@ -122,6 +122,44 @@ __device__ __forceinline__ uint32_t ldu8(const uint8_t* p) {
 // dword-aligned single dword, vector path
 __device__ __forceinline__ uint32_t ld4v(const uint8_t* p) { return ld4_a4(p + vzero()); }
 
+// A WAL physical-record header [crc:4 len:2 type:1 (lognum:4)] at byte pos
+// (db/log_format.h, any alignment): one dword-aligned 16-byte load covers all
+// 11 bytes.  The walks chase one header after another per lane at scattered
+// addresses, so the header read is their cost: one load request instead of
+// 7-11 byte loads.  Within 16 bytes of the buffer end, byte loads (bytes at
+// or past log_len read as 0; callers check the room they need first).
+struct WalHdr {
+  uint32_t crc;     // masked, as stored
+  uint32_t length;  // payload bytes
+  uint32_t type;    // the type byte
+  uint32_t lognum;  // recyclable headers' log number
+};
+__device__ __forceinline__ WalHdr load_wal_header(const uint8_t* log, uint64_t log_len,
+                                                  uint64_t pos) {
+  WalHdr r;
+  const uint64_t q = pos & ~3ull;
+  if (q + 16 <= log_len) {
+    const u32x4a4 v = ld16_a4(log + q + vzero());
+    const uint32_t o = static_cast<uint32_t>(pos & 3);
+    const uint32_t d0 = __builtin_amdgcn_alignbyte(v.y, v.x, o);
+    const uint32_t d1 = __builtin_amdgcn_alignbyte(v.z, v.y, o);
+    const uint32_t d2 = __builtin_amdgcn_alignbyte(v.w, v.z, o);
+    r.crc = d0;
+    r.length = d1 & 0xffffu;
+    r.type = (d1 >> 16) & 0xffu;
+    r.lognum = (d1 >> 24) | (d2 << 8);
+  } else {
+    uint32_t b[11];
+#pragma unroll
+    for (int k = 0; k < 11; ++k) b[k] = pos + k < log_len ? log[pos + k] : 0u;
+    r.crc = b[0] | (b[1] << 8) | (b[2] << 16) | (b[3] << 24);
+    r.length = b[4] | (b[5] << 8);
+    r.type = b[6];
+    r.lognum = b[7] | (b[8] << 8) | (b[9] << 16) | (b[10] << 24);
+  }
+  return r;
+}
+
 // util/crc32c.h:44-53
 __device__ __forceinline__ uint32_t crc_mask(uint32_t crc) {
   return ((crc >> 15) | (crc << 17)) + 0xa282ead8u;

@@ -61,11 +61,22 @@ __device__ __forceinline__ uint32_t ld_le32(const uint8_t* p) {  // any alignmen
   return static_cast<uint32_t>(p[0]) | (static_cast<uint32_t>(p[1]) << 8) |
          (static_cast<uint32_t>(p[2]) << 16) | (static_cast<uint32_t>(p[3]) << 24);
 }
+// little-endian 32-bit store at any alignment with the fewest naturally
+// aligned stores: 1 (p % 4 == 0), 2 (p % 2 == 0) or 3 (odd: byte, short, byte)
+// -- the writer's in-place CRCs land at arbitrary header offsets, and each
+// store is a scattered partial-line write
 __device__ __forceinline__ void st_le32(uint8_t* p, uint32_t v) {
-  p[0] = static_cast<uint8_t>(v);
-  p[1] = static_cast<uint8_t>(v >> 8);
-  p[2] = static_cast<uint8_t>(v >> 16);
-  p[3] = static_cast<uint8_t>(v >> 24);
+  const uintptr_t m = reinterpret_cast<uintptr_t>(p) & 3;
+  if (m == 0) {
+    *reinterpret_cast<uint32_t*>(p) = v;
+  } else if (m == 2) {
+    reinterpret_cast<uint16_t*>(p)[0] = static_cast<uint16_t>(v);
+    reinterpret_cast<uint16_t*>(p)[1] = static_cast<uint16_t>(v >> 16);
+  } else {
+    p[0] = static_cast<uint8_t>(v);
+    *reinterpret_cast<uint16_t*>(p + 1) = static_cast<uint16_t>(v >> 8);
+    p[3] = static_cast<uint8_t>(v >> 24);
+  }
 }
 __device__ __forceinline__ uint32_t crc_unmask(uint32_t m) {  // util/crc32c.h:39
   const uint32_t r = m - kMaskDelta;
@@ -101,9 +112,9 @@ __device__ __forceinline__ uint32_t walk_block(const WalArgs& a, uint64_t b, uin
   uint32_t status = 0, cnt = 0;
   uint64_t pos = start;
   while (start < end && end - pos >= kLogHdr) {
-    const uint8_t* h = a.log + pos;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t type = h[6];
+    const WalHdr h = load_wal_header(a.log, a.log_len, pos);
+    const uint32_t length = h.length;
+    const uint32_t type = h.type;
     const bool recyc = recyclable_type(type);
     const uint32_t hs = recyc ? kLogRHdr : kLogHdr;
     if (end - pos < hs) break;
@@ -111,7 +122,7 @@ __device__ __forceinline__ uint32_t walk_block(const WalArgs& a, uint64_t b, uin
       status = 2;
       break;
     }
-    if (recyc && ld_le32(h + 7) != a.log_number) {
+    if (recyc && h.lognum != a.log_number) {
       status = 4;
       break;
     }
@@ -122,7 +133,7 @@ __device__ __forceinline__ uint32_t walk_block(const WalArgs& a, uint64_t b, uin
     if (FILL) {
       d_off[out_base + cnt] = pos + 6;
       d_len[out_base + cnt] = hs + length - 6;
-      d_stored[out_base + cnt] = crc_unmask(ld_le32(h));  // log_reader.cc:522-523
+      d_stored[out_base + cnt] = crc_unmask(h.crc);  // log_reader.cc:522-523
     }
     ++cnt;
     pos += hs + length;
@@ -255,12 +266,11 @@ __global__ void __launch_bounds__(kTile) wal_rec_desc_kernel(WalArgs a, uint64_t
   uint64_t o = 0;
   uint32_t n = 0;
   if (off <= a.log_len && a.log_len - off >= kLogHdr) {
-    const uint8_t* h = a.log + off;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t hs = recyclable_type(h[6]) ? kLogRHdr : kLogHdr;
-    if (a.log_len - off >= uint64_t(hs) + length) {
+    const WalHdr h = load_wal_header(a.log, a.log_len, off);
+    const uint32_t hs = recyclable_type(h.type) ? kLogRHdr : kLogHdr;
+    if (a.log_len - off >= uint64_t(hs) + h.length) {
       o = off + 6;
-      n = hs + length - 6;
+      n = hs + h.length - 6;
     }
   }
   d_off[i] = o;
@@ -298,13 +308,12 @@ __device__ __forceinline__ FragInfo frag_info(const WalArgs& a, uint64_t i) {
   FragInfo f{0, 0, 0, false};
   const uint64_t off = a.header_offsets[i];
   if (off <= a.log_len && a.log_len - off >= kLogHdr) {
-    const uint8_t* h = a.log + off;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t hs = recyclable_type(h[6]) ? kLogRHdr : kLogHdr;
-    if (a.log_len - off >= uint64_t(hs) + length) {
+    const WalHdr h = load_wal_header(a.log, a.log_len, off);
+    const uint32_t hs = recyclable_type(h.type) ? kLogRHdr : kLogHdr;
+    if (a.log_len - off >= uint64_t(hs) + h.length) {
       f.off = off + hs;
-      f.len = length;
-      f.type = norm_type(h[6]);
+      f.len = h.length;
+      f.type = norm_type(h.type);
       f.ok = f.type >= 1 && f.type <= 4;
     }
   }

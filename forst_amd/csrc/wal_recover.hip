@@ -152,9 +152,9 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       if (rem > 0 && eofb) e = kEvBadHeader;
       break;
     }
-    const uint8_t* h = a.log + pos;
-    const uint32_t length = static_cast<uint32_t>(h[4]) | (static_cast<uint32_t>(h[5]) << 8);
-    const uint32_t type = h[6];  // the byte; sign extension matters only in reports
+    const WalHdr h = load_wal_header(a.log, a.log_len, pos);
+    const uint32_t length = h.length;
+    const uint32_t type = h.type;  // the byte; sign extension matters only in reports
     const bool recyc = recyclable_type(type);
     const uint32_t hs = recyc ? kLogRHdr : kLogHdr;
     if (rem < hs) {
@@ -166,7 +166,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       break;
     }
     const uint32_t pk = length | (type << 16) | (recyc ? 1u << 24 : 0u);
-    if (recyc && ld_le32(h + 7) != a.log_number) {
+    if (recyc && h.lognum != a.log_number) {
       if (a.mode != 3) {  // not kSkipAnyCorruptedRecords: reading ends here
         e = kEvOldStop;
         break;
@@ -180,7 +180,7 @@ __device__ uint32_t rw_walk_block(const RecoverArgs& a, uint64_t b, uint32_t* ev
       e = kEvZero;
       break;
     }
-    emit(n, pos, false, unmask(ld_le32(h)), pk);  // log_reader.cc:522-523
+    emit(n, pos, false, unmask(h.crc), pk);  // log_reader.cc:522-523
     ++n;
     pos += hs + length;
   }
@@ -299,9 +299,15 @@ struct ShiftLds {
     for (uint32_t i = 0; i < r; ++i) v = (v >> 8) ^ g3[v & 0xffu];
     return v;
   }
-  __device__ __forceinline__ uint32_t header_state(const uint8_t* h, uint32_t hs) const {
+  // the CRC state after header[6..hs): the type byte, then (recyclable) the
+  // log number -- both known from the walk (the packed word; a non-old
+  // recyclable record carries the reader's log number), so no header read
+  __device__ __forceinline__ uint32_t header_state(uint32_t type, uint32_t lognum,
+                                                   uint32_t hs) const {
     uint32_t v = 0xffffffffu;
-    for (uint32_t i = 6; i < hs; ++i) v = (v >> 8) ^ g3[(v ^ h[i]) & 0xffu];
+    v = (v >> 8) ^ g3[(v ^ type) & 0xffu];
+    if (hs == kLogRHdr)
+      for (uint32_t k = 0; k < 4; ++k) v = (v >> 8) ^ g3[(v ^ (lognum >> (8 * k))) & 0xffu];
     return v;
   }
 };
@@ -388,7 +394,7 @@ __device__ __forceinline__ void cand_one(const RecoverArgs& a, uint64_t ni, uint
   for (uint64_t r = first; r <= q; ++r) {
     const uint32_t l = ipack[r] & 0xffffu;
     if (l == 0) continue;  // (an empty trailing fragment: the rows kernel's CRC)
-    const uint32_t H = T.header_state(a.log + it_off[r], hs);
+    const uint32_t H = T.header_state((ipack[r] >> 16) & 0xffu, a.log_number, hs);
     const uint32_t e = b + l;
     const uint32_t ws = b >> 10, we = (e - 1) >> 10;
     const uint32_t E = T.shift(H, 1024u * (ws + 1) - b);

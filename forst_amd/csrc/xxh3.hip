@@ -1177,9 +1177,13 @@ __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
 // chain, which ends at the window end).  E and Z per physical record come from the caller
 // (rw_cand_kernel); the verdict goes to crc_ok[physical record].  A window
 // holding a fragment boundary runs a second pass for the next fragment.
-template <int WPE, bool CRC>
+// DEPTH: steps of loads in flight per wave (DEPTH + 1 step buffers rotate):
+// the kernel's memory rate is its bytes in flight (waves x DEPTH x 4 KiB per
+// CU) over the load latency, so fewer waves can carry more steps each
+template <int WPE, bool CRC, int DEPTH = 1>
 __global__ void __launch_bounds__(CRC ? kFragCrcThreads : kFragThreads) FORST_WAVES_PER_EU(WPE)
 xxh3_frag_kernel(BlockArgs a) {
+  static_assert(DEPTH >= 1 && DEPTH <= 3, "1..3 steps in flight");
   // cold per-pair constants and the accumulate keys live in LDS (registers
   // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
   __shared__ uint64_t cold[4 * kColdN];
@@ -1267,10 +1271,16 @@ xxh3_frag_kernel(BlockArgs a) {
       }
     }
   };
-  FRow I;
-  advance(C, I);
-  FStep X, Y;
-  frag_issue<CRC>(a, lane, C, X);
+  // Q[d]: the row position d + 1 steps ahead of C; the step issues the loads
+  // of Q[DEPTH - 1]
+  FRow Q[DEPTH];
+  advance(C, Q[0]);
+#pragma unroll
+  for (int d = 1; d < DEPTH; ++d) advance(Q[d - 1], Q[d]);
+  FStep B[DEPTH + 1];
+  frag_issue<CRC>(a, lane, C, B[0]);
+#pragma unroll
+  for (int d = 1; d < DEPTH; ++d) frag_issue<CRC>(a, lane, Q[d - 1], B[d]);
   uint64_t acc0 = 0, acc1 = 0;
   uint32_t crc_s[4] = {0u, 0u, 0u, 0u};  // (fused CRC) the lane's column chains
   const fcrc::Lanes FK = fcrc::lanes(lane);
@@ -1280,7 +1290,7 @@ xxh3_frag_kernel(BlockArgs a) {
     // the younger ones (an exit path between the copies made them wait out
     // the step in flight before issuing the next)
     const bool live = __ballot(C.rel != kNoMsg) != 0;
-    frag_issue<CRC>(a, lane, I, nx);
+    frag_issue<CRC>(a, lane, Q[DEPTH - 1], nx);
 #ifndef FORST_HOST_EMULATION
     // keep the next step's loads here, ahead of this step's compute (without
     // the fence they are sunk below the step's conditional code, and the
@@ -1491,13 +1501,32 @@ xxh3_frag_kernel(BlockArgs a) {
                  "v"(cu.aux[4]));
     if (CRC) asm volatile("" ::"v"(cu.ez[0]), "v"(cu.ez[1]), "v"(cu.ez[2]), "v"(cu.ez[3]));
 #endif
-    C = I;
-    advance(C, I);
+    C = Q[0];
+#pragma unroll
+    for (int d = 1; d < DEPTH; ++d) Q[d - 1] = Q[d];
+    advance(DEPTH > 1 ? Q[DEPTH > 1 ? DEPTH - 2 : 0] : C, Q[DEPTH - 1]);
     return live;
   };
-  for (bool more = true; more;) {
-    step(X, Y);
-    more = step(Y, X);
+  // step k computes on B[k mod (DEPTH + 1)] and loads into B[(k + DEPTH) mod
+  // (DEPTH + 1)]; one bottom exit (see the loop-shape note)
+  if constexpr (DEPTH == 1) {
+    for (bool more = true; more;) {
+      step(B[0], B[1]);
+      more = step(B[1], B[0]);
+    }
+  } else if constexpr (DEPTH == 2) {
+    for (bool more = true; more;) {
+      step(B[0], B[2]);
+      step(B[1], B[0]);
+      more = step(B[2], B[1]);
+    }
+  } else {
+    for (bool more = true; more;) {
+      step(B[0], B[3]);
+      step(B[1], B[0]);
+      step(B[2], B[1]);
+      more = step(B[3], B[2]);
+    }
   }
 }
 
@@ -1691,11 +1720,11 @@ hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const
 
 }  // namespace
 
-template <int WPE, bool CRC>
+template <int WPE, bool CRC, int DEPTH = 1>
 uint32_t frag_occupancy() {
   static const uint32_t occ = [] {
     int o = 0;
-    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE, CRC>,
+    if (hipOccupancyMaxActiveBlocksPerMultiprocessor(&o, xxh3_frag_kernel<WPE, CRC, DEPTH>,
                                                      CRC ? kFragCrcThreads : kFragThreads,
                                                      0) != hipSuccess ||
         o < 1)
@@ -1705,18 +1734,18 @@ uint32_t frag_occupancy() {
   return occ;
 }
 
-template <int WPE, bool CRC>
+template <int WPE, bool CRC, int DEPTH = 1>
 hipError_t launch_frag(const BlockArgs& a, hipStream_t stream, const char** name) {
   const DeviceInfo& di = device_info();
   constexpr uint32_t FW = CRC ? kFragCrcWaves : kFragWaves;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
       1, std::min<uint64_t>((a.n + 4 * FW - 1) / (4 * FW),
-                            uint64_t(di.num_cus) * frag_occupancy<WPE, CRC>())));
+                            uint64_t(di.num_cus) * frag_occupancy<WPE, CRC, DEPTH>())));
   BlockArgs b = a;
   hipError_t e = feed_setup(b, uint64_t(grid) * FW, stream);
   if (e != hipSuccess) return e;
   *name = CRC ? (WPE == 3 ? "xxh3_frag_kernel<3, crc>" : "xxh3_frag_kernel<2, crc>") : WPE == 4 ? "xxh3_frag_kernel<4>" : WPE == 3 ? "xxh3_frag_kernel<3>" : "xxh3_frag_kernel<2>";
-  hipLaunchKernelGGL((xxh3_frag_kernel<WPE, CRC>), dim3(grid),
+  hipLaunchKernelGGL((xxh3_frag_kernel<WPE, CRC, DEPTH>), dim3(grid),
                      dim3(CRC ? kFragCrcThreads : kFragThreads), 0, stream, b);
   e = hipGetLastError();
   const hipError_t f = scratch_free(b.ticket, stream);
@@ -1746,7 +1775,10 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 #ifndef FORST_FRAG_CRC_WPE
 #define FORST_FRAG_CRC_WPE 3
 #endif
-  return launch_frag<FORST_FRAG_CRC_WPE, true>(a, stream, name);
+#ifndef FORST_FRAG_CRC_DEPTH
+#define FORST_FRAG_CRC_DEPTH 1
+#endif
+  return launch_frag<FORST_FRAG_CRC_WPE, true, FORST_FRAG_CRC_DEPTH>(a, stream, name);
 }
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,

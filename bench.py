@@ -168,6 +168,7 @@ def run_wal(steps, warmup, n_records=10_000_000):
 
     w = workload.make_wal_batch(n_records, workload.SEEDS["C5"])
     offs = torch.from_numpy(w.rec_offsets.view(np.int64)).cuda()
+    lens = torch.from_numpy(w.rec_lengths.astype(np.int32)).cuda()
     crc = torch.empty(len(w.rec_offsets), dtype=torch.uint32, device="cuda")
     nb = w.n_log_blocks
     st = torch.empty(nb, dtype=torch.uint8, device="cuda")
@@ -182,8 +183,9 @@ def run_wal(steps, warmup, n_records=10_000_000):
                                               st.data_ptr(), nrec.data_ptr(), fail.data_ptr(),
                                               bad.data_ptr(), s0))
 
-    def write():
-        engine.wal_record_crc_batch(w.log, offs, write_in_place=True, out=crc)
+    def write():  # the writer's own lengths (forst_wal_record_crc_lengths)
+        engine.wal_record_crc_batch(w.log, offs, write_in_place=True, out=crc,
+                                    payload_lengths=lens)
 
     for _ in range(max(1, warmup)):
         write()

@@ -77,6 +77,7 @@ def lib():
         "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
         "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
         "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
+        "forst_wal_record_crc_lengths": (i, [vp, u64, vp, vp, u64, i, i, vp, vp]),
         "forst_hash64_batch": (i, [vp, u64, vp, vp, vp, u64, vp, u64, vp]),
         "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp,

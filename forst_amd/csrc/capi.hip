@@ -458,6 +458,31 @@ FORST_API int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                     "wal_record_crc launch");
 }
 
+FORST_API int forst_wal_record_crc_lengths(uint8_t* log, uint64_t log_len,
+                                           const uint64_t* header_offsets,
+                                           const uint32_t* payload_lengths, uint64_t n_records,
+                                           int recyclable, int write_in_place, uint32_t* crc_out,
+                                           void* stream) {
+  if (n_records == 0) return FORST_OK;
+  if (!log || !aligned4(log) || !header_offsets || !payload_lengths)
+    return set_error(FORST_EINVAL,
+                     "log/header_offsets/payload_lengths must be non-null, log 4-byte aligned");
+  int rc = check_device();
+  if (rc) return rc;
+  WalArgs a{};
+  a.log = log;
+  a.log_w = log;
+  a.log_len = log_len;
+  a.header_offsets = header_offsets;
+  a.payload_lengths = payload_lengths;
+  a.recyclable = recyclable ? 1 : 0;
+  a.n_records = n_records;
+  a.write_in_place = write_in_place;
+  a.crc_out = crc_out;
+  return hip_status(launch_wal_record_crc(a, static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "wal_record_crc_lengths launch");
+}
+
 namespace forst {
 namespace {
 int dispatch_kv(int mode, const KvArgs& a, void* stream) {

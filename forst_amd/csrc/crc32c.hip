@@ -1612,7 +1612,12 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
       const uint64_t i = kbeg + (C.rel == kNoBlk ? 0 : C.rel);
       bool ok = valid;
       if (MODE == kModeRaw) {
-        if (mine && a.out32) a.out32[i] = valid ? crc : 0u;
+        // WAL writer mode: masked (log_writer.cc:263).  The in-place header
+        // stores are a separate pass (wal.hip): stores share vmcnt with the
+        // loads on gfx950, so scattered partial-line stores here made every
+        // later step wait for them (C5 writer 9.19 -> 9.90 ms)
+        const uint32_t v = a.wal_hs ? crc_mask(crc) : crc;
+        if (mine && a.out32) a.out32[i] = valid ? v : 0u;
       } else if (MODE == kModeVerify) {
         const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
         const uint32_t st = stored - cu.mod;

@@ -122,6 +122,24 @@ __device__ __forceinline__ uint32_t ldu8(const uint8_t* p) {
 // dword-aligned single dword, vector path
 __device__ __forceinline__ uint32_t ld4v(const uint8_t* p) { return ld4_a4(p + vzero()); }
 
+// little-endian 32-bit store at any alignment with the fewest naturally
+// aligned stores: 1 (p % 4 == 0), 2 (p % 2 == 0) or 3 (odd: byte, short, byte)
+// -- the writer's in-place CRCs land at arbitrary header offsets, and each
+// store is a scattered partial-line write
+__device__ __forceinline__ void st_le32(uint8_t* p, uint32_t v) {
+  const uintptr_t m = reinterpret_cast<uintptr_t>(p) & 3;
+  if (m == 0) {
+    *reinterpret_cast<uint32_t*>(p) = v;
+  } else if (m == 2) {
+    reinterpret_cast<uint16_t*>(p)[0] = static_cast<uint16_t>(v);
+    reinterpret_cast<uint16_t*>(p)[1] = static_cast<uint16_t>(v >> 16);
+  } else {
+    p[0] = static_cast<uint8_t>(v);
+    *reinterpret_cast<uint16_t*>(p + 1) = static_cast<uint16_t>(v >> 8);
+    p[3] = static_cast<uint8_t>(v >> 24);
+  }
+}
+
 // A WAL physical-record header [crc:4 len:2 type:1 (lognum:4)] at byte pos
 // (db/log_format.h, any alignment): one dword-aligned 16-byte load covers all
 // 11 bytes.  The walks chase one header after another per lane at scattered

@@ -49,6 +49,12 @@ struct BlockArgs {
   // first physical record index
   const uint64_t* crc_ez;
   uint8_t* crc_ok;
+  // WAL writer mode of the raw CRC rows kernel (forst_wal_record_crc_lengths):
+  // wal_hs = the header size (7, or 11 recyclable) when offsets[] are header
+  // offsets and sizes[] payload lengths -- each record's CRC covers
+  // header[6..hs) + payload (log_writer.cc:240-263) and out32 gets it masked
+  // (util/crc32c.h:33)
+  uint32_t wal_hs;
 };
 
 struct WalArgs {
@@ -67,6 +73,8 @@ struct WalArgs {
   uint64_t n_records;
   int write_in_place;
   uint32_t* crc_out;
+  const uint32_t* payload_lengths;  // nullable: forst_wal_record_crc_lengths
+  int recyclable;
 };
 
 // Per-KV protection / Hash64 batches (kv_protect.hip).

@@ -238,10 +238,16 @@ __device__ __forceinline__ void load_batch(const BlockArgs& a, uint64_t kb, uint
                                            uint32_t lane, DescBatch& d) {
   uint64_t i = kb + lane;
   i = i < kend ? i : kend - 1;  // clamped: the loads are unconditional
-  const uint64_t off = a.offsets[i];
+  uint64_t off = a.offsets[i];
+  uint32_t size = a.sizes[i];
+  if (MODE == kModeRaw && a.wal_hs) {  // WAL writer mode: header offset + payload length
+    const bool ok = off <= a.base_len && a.base_len - off >= uint64_t(a.wal_hs) + size;
+    off = ok ? off + 6 : ~0ull;  // (out of range: reported, never read)
+    size = ok ? a.wal_hs + size - 6 : 0u;
+  }
   d.off_lo = static_cast<uint32_t>(off);
   d.off_hi = static_cast<uint32_t>(off >> 32);
-  d.size = a.sizes[i];
+  d.size = size;
   const uint32_t* mp = a.modifiers ? a.modifiers : a.sizes;
   const uint32_t mv = mp[i];
   d.mod = a.modifiers ? mv : 0u;

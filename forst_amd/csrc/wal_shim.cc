@@ -245,7 +245,7 @@ Status WalWriteGroup::Frame(const std::vector<ByteRange>& records, uint32_t bloc
   if (np == 0) return Status::OK();
   // every CRC from one launch: the image in device memory, CRCs (4 B each) back
   hipStream_t st = static_cast<hipStream_t>(stream_);
-  const uint64_t need = align8(total) + np * 8 + np * 4;
+  const uint64_t need = align8(total) + np * 8 + np * 4 + np * 4;
   if (need > dev_cap_) {
     (void)hipFree(dev_);
     dev_ = nullptr;
@@ -257,12 +257,17 @@ Status WalWriteGroup::Frame(const std::vector<ByteRange>& records, uint32_t bloc
   uint8_t* d_img = static_cast<uint8_t*>(dev_);
   uint64_t* d_off = reinterpret_cast<uint64_t*>(d_img + align8(total));
   uint32_t* d_crc = reinterpret_cast<uint32_t*>(d_off + np);
+  uint32_t* d_len = d_crc + np;
   s = FromHip(hipMemcpyAsync(d_img, image_.data(), total, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
   if (s.ok())
     s = FromHip(hipMemcpyAsync(d_off, offs_.data(), np * 8, hipMemcpyHostToDevice, st),
                 "hipMemcpyAsync");
+  if (s.ok())
+    s = FromHip(hipMemcpyAsync(d_len, flen.data(), np * 4, hipMemcpyHostToDevice, st),
+                "hipMemcpyAsync");
   if (!s.ok()) return s;
-  s = FromRc(forst_wal_record_crc_batch(d_img, total, d_off, np, 0, d_crc, stream_));
+  s = FromRc(forst_wal_record_crc_lengths(d_img, total, d_off, d_len, np, recyclable_, 0, d_crc,
+                                          stream_));
   if (!s.ok()) return s;
   std::vector<uint32_t> crc(np);
   s = FromHip(hipMemcpyAsync(crc.data(), d_crc, np * 4, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");

@@ -187,13 +187,24 @@ def wal_verify_batch(log, log_number=0, first_block=0, n_blocks=None, bad_blocks
     return status, nrec, fail, bad_blocks
 
 
-def wal_record_crc_batch(log, header_offsets, write_in_place=True, out=None, stream=None):
+def wal_record_crc_batch(log, header_offsets, write_in_place=True, out=None, stream=None,
+                         payload_lengths=None, recyclable=False):
     """log::Writer::EmitPhysicalRecord CRC (db/log_writer.cc:228-263) for
-    headers already laid out in `log`."""
+    headers already laid out in `log`.  With payload_lengths (device int32,
+    the lengths the writer laid out: forst_wal_record_crc_lengths) the
+    descriptors come from the arrays instead of a pass over the headers."""
     _dev_u8(log)
     n = header_offsets.numel()
     if out is None:
         out = torch.empty(n, dtype=torch.uint32, device=log.device)
+    if payload_lengths is not None:
+        assert payload_lengths.numel() == n and payload_lengths.element_size() == 4
+        check(lib().forst_wal_record_crc_lengths(log.data_ptr(), log.numel(),
+                                                 header_offsets.data_ptr(),
+                                                 payload_lengths.data_ptr(), n, int(recyclable),
+                                                 int(write_in_place), out.data_ptr(),
+                                                 _stream(stream)))
+        return out
     check(lib().forst_wal_record_crc_batch(log.data_ptr(), log.numel(),
                                            header_offsets.data_ptr(), n, int(write_in_place),
                                            out.data_ptr(), _stream(stream)))

@@ -199,6 +199,18 @@ int forst_wal_record_crc_batch(uint8_t* log, uint64_t log_len,
                                const uint64_t* header_offsets,
                                uint64_t n_records, int write_in_place,
                                uint32_t* crc_out, void* stream);
+/* The same with the payload lengths the writer laid out (forst_wal_layout[_at]
+ * rec_lengths; they must equal the headers' length fields) and the header size
+ * (recyclable: 11 bytes, else 7): the CRC kernel takes its descriptors from
+ * these arrays and stores the masked CRCs in place itself, so no pass reads
+ * the headers first -- log::Writer::EmitPhysicalRecord knows every length it
+ * emits (log_writer.cc:228-263).  Headers that do not fit in the log get
+ * crc_out 0 and are not written. */
+int forst_wal_record_crc_lengths(uint8_t* log, uint64_t log_len,
+                                 const uint64_t* header_offsets,
+                                 const uint32_t* payload_lengths, uint64_t n_records,
+                                 int recyclable, int write_in_place, uint32_t* crc_out,
+                                 void* stream);
 
 /* XXH3_64bits of every logical record (log::Reader::ReadRecord record
  * checksum, db/log_reader.cc:95-165, compared by WriteBatchInternal::

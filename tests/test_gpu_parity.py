@@ -301,6 +301,63 @@ def test_wal_verify_and_writer_crc(recyclable):
     assert (host(d3) == buf).all()
     want = [struct.unpack("<I", buf[int(o):int(o) + 4].tobytes())[0] for o in poffs]
     assert (host(crcs).astype(np.uint64) == np.array(want, dtype=np.uint64)).all()
+    # ... and from the writer's own lengths (forst_wal_record_crc_lengths: the
+    # rows kernel's WAL writer mode, descriptors from the arrays, CRCs masked
+    # and stored in place by the kernel)
+    d4 = d(buf3)
+    crcs4 = engine.wal_record_crc_batch(d4, d(poffs.astype(np.int64)),
+                                        payload_lengths=d(plens.astype(np.int32)),
+                                        recyclable=recyclable)
+    assert (host(d4) == buf).all()
+    assert (host(crcs4) == host(crcs)).all()
+    # without writing in place: only crc_out
+    d5 = d(buf3)
+    crcs5 = engine.wal_record_crc_batch(d5, d(poffs.astype(np.int64)), write_in_place=False,
+                                        payload_lengths=d(plens.astype(np.int32)),
+                                        recyclable=recyclable)
+    assert (host(d5) == buf3).all() and (host(crcs5) == host(crcs)).all()
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_wal_writer_crc_with_lengths_edges(recyclable):
+    """forst_wal_record_crc_lengths against the header-reading path on the
+    write-group shapes a writer produces: records of 0..70000 bytes at every
+    header alignment (in-place stores of 1, 2 or 3 pieces), a log shorter
+    than one 4 KiB round (the fallback path), headers that do not fit the
+    log (crc_out 0, nothing written), and a C5-sized batch"""
+    hs = 11 if recyclable else 7
+    rng = np.random.default_rng(31)
+    lens = np.concatenate([np.arange(0, 40), rng.integers(0, 70000, 300),
+                           [32761, 32762, 32757, 32758]]).astype(np.uint32)
+    for sub in (lens, lens[:3]):  # (3 short records: a log under 4 KiB)
+        payload = rng.integers(0, 256, int(sub.astype(np.int64).sum()), dtype=np.uint8)
+        buf, poffs, plens = O.wal_frame(payload, sub, recyclable=recyclable, log_number=77)
+        wiped = buf.copy()
+        for o in poffs:
+            wiped[int(o):int(o) + 4] = 0
+        offs = poffs.astype(np.int64)
+        lengths = plens.astype(np.int32)
+        # two headers that do not fit: past the end, and a length overrunning it
+        offs = np.concatenate([offs, [len(buf) + 5, int(offs[-1])]])
+        lengths = np.concatenate([lengths, [3, len(buf)]]).astype(np.int32)
+        dl = d(wiped)
+        got = host(engine.wal_record_crc_batch(dl, d(offs), payload_lengths=d(lengths),
+                                               recyclable=recyclable))
+        assert (host(dl) == buf).all(), len(sub)
+        want = [struct.unpack("<I", buf[int(o):int(o) + 4].tobytes())[0] for o in poffs]
+        assert got[:len(poffs)].astype(np.uint64).tolist() == want
+        assert got[-2:].tolist() == [0, 0]
+    # C5 volume of records (the bench's writer call)
+    w = workload.make_wal_batch(200_000, workload.SEEDS["C5"], recyclable=recyclable,
+                                log_number=77)
+    ref = host(w.log)
+    o = torch.from_numpy(w.rec_offsets.view(np.int64)).to(DEV)
+    wiped = w.log.clone()
+    wiped[(o[:, None] + torch.arange(4, device=DEV)[None, :]).reshape(-1)] = 0
+    got = engine.wal_record_crc_batch(wiped, o, payload_lengths=d(w.rec_lengths.astype(np.int32)),
+                                      recyclable=recyclable)
+    assert (host(wiped) == ref).all()
+    assert (host(got) == host(engine.wal_record_crc_batch(w.log.clone(), o))).all()
 
 
 def test_wal_old_record_and_zero_type():

@@ -723,18 +723,30 @@ __global__ void __launch_bounds__(kLanes) rw_seg_kernel(Tokens t, uint64_t n, co
 // fragmented record; a control record (types 9-11) keeps the state it finds
 // (log_reader.cc:167-213), i.e. that of the segment before it -- a run of
 // control-headed segments is resolved by walking back to the segment that
-// decides; every other head clears it
+// decides; every other head clears it.  A segment is TRANSPARENT when its
+// head is a control record and no record completes in it: the walk passes
+// those and stops at the first other one.  The walk is capped at kLiveWalk
+// segments (log::Writer writes at most a few control records in a row, so the
+// cap is never reached by a writer's log); a head whose walk hits the cap is
+// counted in *over and decided by the linear pass below instead (a crafted
+// log of long control runs would otherwise cost O(run^2)).
+constexpr uint32_t kLiveWalk = 64;
 __global__ void __launch_bounds__(kLanes) rw_live_kernel(Tokens t, uint64_t n, const uint64_t* head,
                                                          const uint64_t* seg,
                                                          const uint64_t* seg_head,
                                                          const unsigned long long* seg_fl,
-                                                         uint8_t* live) {
+                                                         uint8_t* live, unsigned long long* over) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= n || !head[i]) return;
   const uint8_t k = t.kind[i];
   uint8_t l = k == kTkFirst ? 1 : 0;
   if (is_ctl(k)) {
+    uint32_t steps = 0;
     for (uint64_t x = seg[i] - 1; x > 0; --x) {
+      if (++steps > kLiveWalk) {
+        atomicAdd(over, 1ull);
+        break;
+      }
       if (seg_fl[x] != ~0ull) break;  // a record completed there: not in a fragmented record
       const uint8_t kx = t.kind[seg_head[x]];
       if (kx == kTkFirst) {
@@ -745,6 +757,40 @@ __global__ void __launch_bounds__(kLanes) rw_live_kernel(Tokens t, uint64_t n, c
     }
   }
   live[seg[i]] = l;
+}
+
+// The linear form (runs only when a walk above hit its cap): nt[s] = 1 for the
+// segments that are not transparent (segment 0, before the first head, is
+// not); cnt = exclusive scan of nt; pos[cnt[x] + 1] = x for each such x; the
+// segment that decides a control-headed segment s is pos[cnt[s]], the last
+// non-transparent one before s -- what the walk finds.
+__global__ void __launch_bounds__(kLanes) rw_live_nt_kernel(Tokens t, uint64_t n,
+                                                            const uint64_t* head,
+                                                            const uint64_t* seg,
+                                                            const unsigned long long* seg_fl,
+                                                            uint64_t* nt) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= n || !head[i]) return;
+  const uint64_t s = seg[i];
+  nt[s] = is_ctl(t.kind[i]) && seg_fl[s] == ~0ull ? 0 : 1;
+}
+__global__ void __launch_bounds__(kLanes) rw_live_pos_kernel(uint64_t ns, const uint64_t* nt,
+                                                             const uint64_t* cnt, uint64_t* pos) {
+  const uint64_t s = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (s < ns && nt[s]) pos[cnt[s] + 1] = s;
+}
+__global__ void __launch_bounds__(kLanes) rw_live_fix_kernel(Tokens t, uint64_t n,
+                                                             const uint64_t* head,
+                                                             const uint64_t* seg,
+                                                             const uint64_t* seg_head,
+                                                             const unsigned long long* seg_fl,
+                                                             const uint64_t* cnt,
+                                                             const uint64_t* pos, uint8_t* live) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i >= n || !head[i] || !is_ctl(t.kind[i])) return;
+  const uint64_t s = seg[i];
+  const uint64_t x = pos[cnt[s]];
+  live[s] = x >= 1 && seg_fl[x] == ~0ull && t.kind[seg_head[x]] == kTkFirst ? 1 : 0;
 }
 
 // reasons (forst_wal_report.reason)
@@ -1098,7 +1144,7 @@ struct P2 {
   Tokens t;
   uint64_t *ntok, *tok_base, *head, *plen, *pl, *seg, *seg_head, *n_emit, *n_rep, *emit_at, *rep_at,
       *tiles2, *ctl_list;
-  unsigned long long* seg_fl;
+  unsigned long long *seg_fl, *live_over;
   uint8_t* live;
   void take(Arena& A, uint64_t ni, uint64_t nb, uint64_t nt) {
     it_off = A.take<uint64_t>(ni);
@@ -1149,6 +1195,7 @@ struct P2 {
     rep_at = A.take<uint64_t>(nt);
     tiles2 = A.take<uint64_t>(nt / kScanTile + 2);
     ctl_list = A.take<uint64_t>(kCtlCap);
+    live_over = A.take<unsigned long long>(1);
   }
 };
 
@@ -1353,33 +1400,58 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   scan_u64(q.plen, n_tok, q.tiles2, q.pl, st);
   (void)hipMemsetAsync(q.seg_fl, 0xff, 8 * (n_tok + 1), st);
   (void)hipMemsetAsync(q.live, 0, n_tok + 1, st);
+  (void)hipMemsetAsync(q.live_over, 0, 8, st);
   hipLaunchKernelGGL(rw_seg_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg, q.seg_head,
                      q.seg_fl);
   hipLaunchKernelGGL(rw_live_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg, q.seg_head,
-                     q.seg_fl, q.live);
+                     q.seg_fl, q.live, q.live_over);
   const Fsm f{q.seg, q.seg_head, q.seg_fl, q.live, q.pl, q.plen};
   forst_wal_records no_recs{};
   forst_wal_reports no_reps{};
   CtlReps cr{};
-  hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
-                     q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr);
   uint64_t tot[2] = {0, 0};
-  unsigned long long n_ctl = 0;
+  unsigned long long n_ctl = 0, live_over = 0;
   const uint64_t ntl = (n_tok + kScanTile - 1) / kScanTile;
-  scan_u64(q.n_emit, n_tok, q.tiles2, q.emit_at, st);
-  e = hipMemcpyAsync(&tot[0], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
-  scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (after the copy above, stream order)
-  if (e == hipSuccess) e = hipMemcpyAsync(&tot[1], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
-  // stop reason / offset: the last token
   uint8_t last_kind = 0;
   uint64_t last_pos = 0;
-  if (e == hipSuccess) e = hipMemcpyAsync(&n_ctl, q1.ctl_n, 8, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && n_tok)
-    e = hipMemcpyAsync(&last_kind, t.kind + n_tok - 1, 1, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess && n_tok)
-    e = hipMemcpyAsync(&last_pos, t.pos + n_tok - 1, 8, hipMemcpyDeviceToHost, st);
-  if (e == hipSuccess) e = hipStreamSynchronize(st);
-  if (e != hipSuccess) return fail(e);
+  // the state machine's counts (emitted records, reports), the control-record
+  // count and the stop token (one sync)
+  auto count_pass = [&]() -> hipError_t {
+    hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
+                       q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr);
+    scan_u64(q.n_emit, n_tok, q.tiles2, q.emit_at, st);
+    hipError_t r = hipMemcpyAsync(&tot[0], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
+    scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (after the copy above, stream order)
+    if (r == hipSuccess) r = hipMemcpyAsync(&tot[1], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess) r = hipMemcpyAsync(&n_ctl, q1.ctl_n, 8, hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess) r = hipMemcpyAsync(&live_over, q.live_over, 8, hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess && n_tok)
+      r = hipMemcpyAsync(&last_kind, t.kind + n_tok - 1, 1, hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess && n_tok)
+      r = hipMemcpyAsync(&last_pos, t.pos + n_tok - 1, 8, hipMemcpyDeviceToHost, st);
+    if (r == hipSuccess) r = hipStreamSynchronize(st);
+    return r;
+  };
+  if ((e = count_pass()) != hipSuccess) return fail(e);
+  if (live_over) {  // a control run longer than the walk's cap: the linear form, then recount
+    const uint64_t ns = n_tok + 1;  // segments 0..n_tok at most
+    const uint64_t tl = up256(8 * (ns / kScanTile + 2));
+    void* lin = nullptr;
+    if ((e = alloc(3 * up256(8 * (ns + 1)) + tl, &lin)) != hipSuccess) return fail(e);
+    uint64_t* nt_f = static_cast<uint64_t*>(lin);
+    uint64_t* cnt = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(lin) + up256(8 * (ns + 1)));
+    uint64_t* pos = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(lin) + 2 * up256(8 * (ns + 1)));
+    uint64_t* tiles = reinterpret_cast<uint64_t*>(static_cast<uint8_t*>(lin) + 3 * up256(8 * (ns + 1)));
+    (void)hipMemsetAsync(nt_f, 0, 8 * ns, st);
+    (void)hipMemsetAsync(nt_f, 1, 1, st);  // segment 0: nt = 1 (little endian)
+    hipLaunchKernelGGL(rw_live_nt_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg,
+                       q.seg_fl, nt_f);
+    scan_u64(nt_f, ns, tiles, cnt, st);
+    hipLaunchKernelGGL(rw_live_pos_kernel, grid_for(ns), dim3(kLanes), 0, st, ns, nt_f, cnt, pos);
+    hipLaunchKernelGGL(rw_live_fix_kernel, tg, dim3(kLanes), 0, st, t, n_tok, q.head, q.seg,
+                       q.seg_head, q.seg_fl, cnt, pos, q.live);
+    if ((e = count_pass()) != hipSuccess) return fail(e);
+  }
   // control records (types 9-11): read back, decided in reader order on the
   // host, their reports added before the report scan is taken again
   CtlHost ch;

@@ -283,3 +283,28 @@ def test_full_size_c5_recovery():
               for o, b, r_, t in zip(po, pb, pr, pt)]
         assert gr == want_reps, (mode, gr[:4], want_reps[:4])
         assert sum(1 for g in gr if g[1] == "checksum mismatch") == len(victims)
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_long_control_runs_on_emulator(recyclable):
+    """runs of 200 control records (beyond rw_live_kernel's walk-back cap:
+    the linear liveness fallback) inside a fragmented record, after an
+    unfinished First and between Full records, every mode"""
+    E = _emu()
+    for name, log, ln in W.long_control_runs(recyclable):
+        for mode in MODES:
+            recs, reps, res = E.wal_recover(log, ln, mode)
+            compare(recs, reps, res, log, ln, mode, name)
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_long_control_runs_on_gpu(recyclable):
+    import torch
+    from forst_amd import engine
+    for name, log, ln in W.long_control_runs(recyclable):
+        for mode in MODES:
+            rec, rep, res = engine.wal_recover_batch(torch.from_numpy(log).cuda(), ln, mode)
+            recs = [rec[k].cpu().numpy() for k in ("offset", "length", "hash", "n_fragments")]
+            reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
+            compare(recs, reps, res, log, ln, mode, name)

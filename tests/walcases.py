@@ -331,3 +331,47 @@ def old_tail_log(total_blocks=600, seed=33):
     cut = (len(new) // 32768) * 32768 + 32768
     out[:len(new)] = new
     return out[:max(n, cut)]
+
+
+def long_control_runs(recyclable, run=200, seed=41):
+    """runs of `run` consecutive control records (far more than the walk-back
+    cap of rw_live_kernel, so the linear fallback decides liveness): inside a
+    fragmented record (First ... Last), after a First that never completes,
+    and between Full records; timestamp-size records alternate with
+    kSetCompressionType ones, one cf is recorded twice with another size"""
+    ln = 7
+    base = 4 if recyclable else 0
+    ts_type = 11 if recyclable else 10
+    lens = np.full(3 * run + 60, 12, np.uint32)
+    buf, po, pl = frame_lens(lens, seed, recyclable, ln)
+    assert len(po) == len(lens)
+
+    def control(k, i):
+        o = int(po[k])
+        hs = hdr_size(buf, o)
+        if i % 2 == 0:  # two (cf, size) pairs: exactly the 12-byte payload
+            cf = 5 if i == 40 else 1000 + i  # cf 5 recorded again (8 -> 16) at i == 40
+            sz = 16 if i == 40 else 8
+            pay = struct.pack("<IHIH", cf, sz, 2000 + i, 8)
+            buf[o + 6] = ts_type
+            buf[o + hs:o + hs + len(pay)] = np.frombuffer(pay, np.uint8)
+            set_type(buf, o, ts_type)
+        else:  # compression record with the 7-byte header over the same span
+            pay = struct.pack("<I", 0) + bytes(12 + hs - 7 - 4)
+            buf[o + 4:o + 6] = np.frombuffer(struct.pack("<H", len(pay)), np.uint8)
+            buf[o + 7:o + 7 + len(pay)] = np.frombuffer(pay, np.uint8)
+            set_type(buf, o, 9)
+
+    k = 5
+    set_type(buf, int(po[k]), 2 + base)          # First ... run ... Last
+    for i in range(run):
+        control(k + 1 + i, i)
+    set_type(buf, int(po[k + 1 + run]), 4 + base)
+    k += run + 10
+    set_type(buf, int(po[k]), 2 + base)          # First ... run ... Full (partial record)
+    for i in range(run):
+        control(k + 1 + i, i)
+    k += run + 10
+    for i in range(run):                          # Full ... run ... Full
+        control(k + i, i)
+    return [("long_ctl", buf, ln)]

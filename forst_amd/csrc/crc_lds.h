@@ -16,18 +16,19 @@ namespace forst {
 namespace fcrc {
 
 struct Lanes {
-  uint32_t lreg[4];  // 4 (8 (i ^ g) + c)
-  uint32_t sel[4];   // v_perm selector: {0, 0, x.byte(i ^ g), lreg.b0}
+  uint32_t lpack;   // byte i: 4 (8 (i ^ g) + c)
+  uint32_t sel[4];  // v_perm selector: {0, 0, x.byte(i ^ g), lpack.byte(i)}
 };
 
 __device__ __forceinline__ Lanes lanes(uint32_t lane) {
   Lanes k;
   const uint32_t c = lane & 7, g = (lane >> 3) & 3;
+  k.lpack = 0;
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
     const uint32_t tt = i ^ g;
-    k.lreg[i] = 4 * (8 * tt + c);
-    k.sel[i] = 0x0c0c0000u | ((4 + tt) << 8);
+    k.lpack |= (4 * (8 * tt + c)) << (8 * i);
+    k.sel[i] = 0x0c0c0000u | ((4 + tt) << 8) | i;
   }
   return k;
 }
@@ -46,7 +47,7 @@ __device__ __forceinline__ void look(const uint8_t* __restrict__ Lb, const Lanes
                                      uint32_t (&l)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    l[i] = lds32(Lb, __builtin_amdgcn_perm(x, k.lreg[i], k.sel[i]) + (J ? 128u : 0u));
+    l[i] = lds32(Lb, __builtin_amdgcn_perm(x, k.lpack, k.sel[i]) + (J ? 128u : 0u));
 }
 
 // G(x) ^ e: the next chain input when e is the next data word
@@ -69,6 +70,33 @@ __device__ __forceinline__ uint32_t chunk_step(const uint8_t* __restrict__ Lb, c
   x = g_then(Lb, k, x, w2);
   x = g_then(Lb, k, x, w3);
   return g_then(Lb, k, x, 0u);
+}
+
+// chunk_step on four independent chains at once: each dependent level issues
+// the table reads of all four chains before any of them is waited for
+__device__ __forceinline__ void chunk_step4(const uint8_t* __restrict__ Lb, const Lanes& k,
+                                            uint32_t (&s)[4], const uint32_t (&w)[4][4]) {
+  uint32_t x[4];
+#pragma unroll
+  for (int c = 0; c < 4; ++c) {
+    uint32_t lj[4], lg[4];
+    look<true>(Lb, k, s[c], lj);
+    look<false>(Lb, k, w[c][0], lg);
+    x[c] = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]), xor3(lg[2], lg[3], w[c][1]));
+  }
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = g_then(Lb, k, x[c], w[c][2]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) x[c] = g_then(Lb, k, x[c], w[c][3]);
+#pragma unroll
+  for (int c = 0; c < 4; ++c) s[c] = g_then(Lb, k, x[c], 0u);
+}
+
+// the mask of dword i of a 16-byte chunk whose first n bytes are kept (n >=
+// 16: all): the high word of 0xffffffff << 8 clamp(n - 4 i, 0, 4)
+__device__ __forceinline__ uint32_t keep_word(uint32_t n, uint32_t i) {
+  const uint32_t b = n > 4 * i ? (n - 4 * i < 4u ? n - 4 * i : 4u) : 0u;
+  return static_cast<uint32_t>((0xffffffffull << (8 * b)) >> 32);
 }
 
 // linear shift through an unreplicated 4 x 256 table at byte offset b

@@ -26,6 +26,7 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
 // on gfx950 (dword-aligned multi-dword loads are legal), so lane segments that
 // start at any dword boundary are read with one instruction.
 typedef uint32_t u32x4a4 __attribute__((ext_vector_type(4), aligned(4)));
+typedef uint32_t u32x4 __attribute__((ext_vector_type(4)));  // 16-byte aligned (LDS)
 
 // Opaque per-lane zero.  Adding it to a wave-uniform data address forces a
 // VECTOR (global_load) access: hipcc otherwise turns uniform loads it proves
@@ -55,6 +56,17 @@ __device__ __forceinline__ uint32_t retire(uint32_t v) {
   r = v;
 #endif
   return r;
+}
+
+// A value the compiler may not hoist: a lane constant recomputed where it is
+// used, inside a loop, rather than kept live across it (at high register
+// pressure such constants are spilled, and a spill reload in a streaming
+// loop is a vmcnt(0) wait on the loads in flight).
+__device__ __forceinline__ uint32_t fresh(uint32_t v) {
+#ifndef FORST_HOST_EMULATION
+  asm volatile("" : "+v"(v));
+#endif
+  return v;
 }
 
 #ifdef FORST_DEBUG_BOUNDS

@@ -35,6 +35,26 @@ constexpr uint32_t kRowsThreads = kRowsWaves * 64;
 #define FORST_XX_WG_CHUNK 4
 #endif
 constexpr uint32_t kXxWgChunk = FORST_XX_WG_CHUNK;
+// fused WAL recovery: the four CRC column chains of a step interleaved (1) or
+// one after the other (0, the round-3 form)
+#ifndef FORST_FRAG_CRC_IL
+#define FORST_FRAG_CRC_IL 0
+#endif
+// the fragment kernel's lane constants recomputed where used (1) or left to
+// the compiler, which hoists and, at 168 VGPRs, spills them (0)
+#ifndef FORST_FRAG_FRESH
+#define FORST_FRAG_FRESH 1
+#endif
+// the fused CRC's byte masks (bytes of a 16-byte chunk inside the fragment)
+// read from a 17-entry LDS table (1), or computed in a branch per chunk (0)
+#ifndef FORST_FRAG_MASK_LDS
+#define FORST_FRAG_MASK_LDS 1
+#endif
+#if FORST_FRAG_FRESH
+#define FR(x) fresh(x)
+#else
+#define FR(x) (x)
+#endif
 // the fragment kernel (WAL records): 4-wave workgroups and the global feed
 // (the workgroup feed measured 5 % slower on C5's log-uniform records)
 constexpr bool kFragWg = false;
@@ -223,7 +243,9 @@ __device__ __forceinline__ uint64_t xxh3_short_row(uint64_t d0, uint64_t d1, uin
     const uint32_t bf = static_cast<uint32_t>(sec64(0)) ^ static_cast<uint32_t>(sec64(4));
     return xxh64_avalanche(static_cast<uint64_t>(combined ^ bf));
   }
-  return xxh64_avalanche(sec64(56) ^ sec64(64));
+  // (an opaque zero: the folded constant, kept live across the callers'
+  // loops, was a spilled register pair)
+  return xxh64_avalanche(sec64(56) ^ sec64(64) ^ fresh(0u));
 }
 
 struct LaneKeys {
@@ -1064,7 +1086,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
       // it), its XXH3 chunk (xxh3_short_row) in x[2] and the 16 bytes after
       // that in x[3], whose first dword realigns it (the record ends >=
       // kFragTail bytes before the log end)
-      const uint64_t sp = short_phys(P0, P.size, t);
+      const uint64_t sp = short_phys(P0, P.size, FR(lane) & 15u);
       if (shrt) {
         pq = a.base + (sp & ~3ull) + 16 * (k - 2);
         mm = static_cast<uint32_t>(sp) & 3u;
@@ -1105,7 +1127,8 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
       q0 = R + 256 * ks;
       q4 = q0 + 16;
     } else if (lastp && s4 == ql) {
-      const uint64_t lq = P0 + P.size - 64 + 16 * p + static_cast<uint64_t>(hs) * (P.info >> 8);
+      const uint64_t lq = P0 + (P.size - 64u + 16u * (FR(lane) & 3u)) +
+                            static_cast<uint64_t>(hs) * (P.info >> 8);
       q0 = a.base + (lq & ~3ull);
       q4 = (lq & 3) ? q0 + 16 : q0;  // (the stripe ends at the record end)
     }
@@ -1190,18 +1213,23 @@ xxh3_frag_kernel(BlockArgs a) {
   __shared__ uint64_t keys[24];
   __shared__ uint64_t shsec[64];
   __shared__ uint32_t crcL[CRC ? kFcLds / 4 : 1];
+  // kmask[4 n + i]: the mask of dword i of a chunk whose first n bytes are
+  // kept (n = 0..16)
+  __shared__ __attribute__((aligned(16))) uint32_t kmask[CRC ? 17 * 4 : 4];
   constexpr uint32_t FW = CRC ? kFragCrcWaves : kFragWaves;
   if (kFragWg) feed_init();
   if (threadIdx.x < 4 * kColdN) cold[threadIdx.x] = (&kXxCold[0][0])[threadIdx.x];
   if (threadIdx.x < 24) keys[threadIdx.x] = sec64(8 * threadIdx.x);
   short_secrets_fill(shsec, threadIdx.x);
-  if constexpr (CRC) fill_frag_crc_tables<kFragCrcThreads>(crcL);
+  if constexpr (CRC) {
+    fill_frag_crc_tables<kFragCrcThreads>(crcL);
+    if (threadIdx.x < 17 * 4) kmask[threadIdx.x] = fcrc::keep_word(threadIdx.x >> 2, threadIdx.x & 3);
+  }
   __syncthreads();
   const uint8_t* Lb = reinterpret_cast<const uint8_t*>(crcL);
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
-  const uint64_t* ck = cold + kColdN * p;
   // K0[k] = keys[s4 + 2p + 4k], K1[k] = keys[s4 + 2p + 4k + 1]
   // (the scramble keys sec64(128 + 16p), sec64(136 + 16p) are keys[16 + 2p],
   // keys[17 + 2p], read where used: one spilled register pair fewer)
@@ -1302,8 +1330,9 @@ xxh3_frag_kernel(BlockArgs a) {
     const bool lng = valid && C.size > 240;
     const uint32_t nbC = (C.size - 1) >> 10, nbSC = ((C.size - 1) & 1023) >> 6;
     if (C.g == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
-      acc0 = ck[kColdI0];
-      acc1 = ck[kColdI1];
+      const uint64_t* ci = cold + kColdN * (FR(lane) & 3u);
+      acc0 = ci[kColdI0];
+      acc1 = ci[kColdI1];
     }
     uint64_t sum0 = 0, sum1 = 0;
     uint32_t fm = cu.fm;
@@ -1374,6 +1403,14 @@ xxh3_frag_kernel(BlockArgs a) {
       hiA = fe - W0 < 1024u ? fe - W0 : 1024u;
     }
     uint32_t cs[4] = {crc_s[0], crc_s[1], crc_s[2], crc_s[3]};
+#if FORST_FRAG_CRC_IL
+    // (fused CRC) the four column chains advance together, one dependent
+    // LDS level at a time (fcrc::chunk_step4), and the bytes past the
+    // fragment end are masked in one wave-uniform branch ahead of them: with
+    // a mask branch per chunk every chain sat in its own basic block and the
+    // 4 chains' 16 table-read levels ran back to back
+    uint32_t cw[4][4];
+#endif
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       uint64_t d0, d1;
@@ -1383,16 +1420,46 @@ xxh3_frag_kernel(BlockArgs a) {
       const bool use = C.g < nbC || s4 + 4 * k < nbSC;
       sum0 += use ? c0 : 0ull;
       sum1 += use ? c1 : 0ull;
+#if FORST_FRAG_CRC_IL
+      cw[k][0] = static_cast<uint32_t>(d0);
+      cw[k][1] = static_cast<uint32_t>(d0 >> 32);
+      cw[k][2] = static_cast<uint32_t>(d1);
+      cw[k][3] = static_cast<uint32_t>(d1 >> 32);
+#else
       if (CRC) {
         const uint32_t q = 16 * t + 256 * k;
+#if FORST_FRAG_MASK_LDS
+        const uint32_t n = hiA > q ? (hiA - q < 16u ? hiA - q : 16u) : 0u;
+        const u32x4 m = *reinterpret_cast<const u32x4*>(kmask + 4 * n);
+        cs[k] = fcrc::chunk_step(Lb, FK, cs[k], static_cast<uint32_t>(d0) & m.x,
+                                 static_cast<uint32_t>(d0 >> 32) & m.y,
+                                 static_cast<uint32_t>(d1) & m.z,
+                                 static_cast<uint32_t>(d1 >> 32) & m.w);
+#else
         uint64_t m0 = ~0ull, m1 = ~0ull;
         if (hiA < q + 16) fcrc::keep_mask(0, hiA > q ? hiA - q : 0u, m0, m1);
         const uint64_t e0 = d0 & m0, e1 = d1 & m1;
         cs[k] = fcrc::chunk_step(Lb, FK, cs[k], static_cast<uint32_t>(e0),
                                  static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
                                  static_cast<uint32_t>(e1 >> 32));
+#endif
       }
+#endif
     }
+#if FORST_FRAG_CRC_IL
+    if (CRC) {
+      if (__ballot(hiA < 1024u)) {  // some row's fragment ends inside its window
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t q = 16 * t + 256 * k;
+          const uint32_t n = hiA > q ? hiA - q : 0u;  // bytes of the chunk kept (>= 16: all)
+#pragma unroll
+          for (uint32_t i = 0; i < 4; ++i) cw[k][i] &= fcrc::keep_word(n, i);
+        }
+      }
+      fcrc::chunk_step4(Lb, FK, cs, cw);
+    }
+#endif
     if (CRC) {
       // the fragment's end in this window: finish it (and a fragment that
       // starts here: second pass); else carry the chain, E added at the end
@@ -1434,12 +1501,23 @@ xxh3_frag_kernel(BlockArgs a) {
             const uint32_t q = 16 * t + 256 * k;
             const uint32_t ka = B > q ? (B - q < 16u ? B - q : 16u) : 0u;
             const uint32_t kb = hiB > q ? (hiB - q < 16u ? hiB - q : 16u) : 0u;
+#if FORST_FRAG_MASK_LDS
+            // bytes [ka, kb): mask(kb) & ~mask(ka)
+            const u32x4 mb = *reinterpret_cast<const u32x4*>(kmask + 4 * (kb > ka ? kb : ka));
+            const u32x4 ma = *reinterpret_cast<const u32x4*>(kmask + 4 * ka);
+            sb[k] = fcrc::chunk_step(
+                Lb, FK, sb[k], __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d0), mb.x, ma.x, 0x40),
+                __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d0 >> 32), mb.y, ma.y, 0x40),
+                __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d1), mb.z, ma.z, 0x40),
+                __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d1 >> 32), mb.w, ma.w, 0x40));
+#else
             uint64_t m0, m1;
             fcrc::keep_mask(ka, kb > ka ? kb : ka, m0, m1);
             const uint64_t e0 = d0 & m0, e1 = d1 & m1;
             sb[k] = fcrc::chunk_step(Lb, FK, sb[k], static_cast<uint32_t>(e0),
                                      static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
                                      static_cast<uint32_t>(e1 >> 32));
+#endif
           }
           const bool endsB = pb && L - W0 <= 1024u;
           const uint32_t VB = row_value(sb) ^ cu.ez[2];
@@ -1473,9 +1551,10 @@ xxh3_frag_kernel(BlockArgs a) {
         uint64_t d0, d1;
         const uint64_t le = C.off() + C.size + static_cast<uint64_t>(C.hs()) * (C.info >> 8);
         xx_words(cu.aux, static_cast<uint32_t>(le & 3), d0, d1);
-        const uint64_t a0 = acc0 + mul32to64(d0 ^ ck[kColdL0]) + d1;
-        const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ ck[kColdL1]);
-        uint64_t tm = mul128_fold64(a0 ^ ck[kColdM0], a1 ^ ck[kColdM1]);
+        const uint64_t* cf = cold + kColdN * (FR(lane) & 3u);
+        const uint64_t a0 = acc0 + mul32to64(d0 ^ cf[kColdL0]) + d1;
+        const uint64_t a1 = acc1 + d0 + mul32to64(d1 ^ cf[kColdL1]);
+        uint64_t tm = mul128_fold64(a0 ^ cf[kColdM0], a1 ^ cf[kColdM1]);
         tm += quad_xor64<1>(tm);
         tm += quad_xor64<2>(tm);
         h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
@@ -1485,11 +1564,12 @@ xxh3_frag_kernel(BlockArgs a) {
         xx_words(cu.x[2], (fm >> 4) & 3u, d0, d1);
         const uint64_t P0 = C.off();
         const uint32_t pb = static_cast<uint32_t>(P0 - short_phys(P0, C.size, 0));
-        const uint64_t hs2 = xxh3_short_row(d0, d1, C.size, t, pb, shsec);
+        const uint64_t hs2 = xxh3_short_row(d0, d1, C.size, FR(lane) & 15u, pb, shsec);
         if (fin && valid && !lng) h = hs2;
       }
       // (the quad that loaded the last stripe: fm bit 18)
-      if (fin && t == 4 * ((fm >> 18) & 1u) && a.out64) a.out64[C.rel] = valid ? h : 0ull;
+      if (fin && (FR(lane) & 15u) == 4 * ((fm >> 18) & 1u) && a.out64)
+        a.out64[C.rel] = valid ? h : 0ull;
 
     }
 #ifndef FORST_HOST_EMULATION

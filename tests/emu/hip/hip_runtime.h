@@ -217,6 +217,14 @@ inline unsigned long long atomicMin(unsigned long long* p, unsigned long long v)
   return cur;
 }
 
+inline uint32_t atomicMin(uint32_t* p, uint32_t v) {
+  uint32_t cur = __atomic_load_n(p, __ATOMIC_RELAXED);
+  while (v < cur && !__atomic_compare_exchange_n(p, &cur, v, false, __ATOMIC_RELAXED,
+                                                 __ATOMIC_RELAXED)) {
+  }
+  return cur;
+}
+
 // stream-ordered allocation / copies: host memory, everything synchronous
 typedef void* hipMemPool_t;
 constexpr hipError_t hipErrorInvalidDevice = 101;

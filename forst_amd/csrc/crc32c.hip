@@ -562,18 +562,19 @@ __device__ __forceinline__ uint32_t lds32(const uint8_t* __restrict__ Lb, uint32
 }
 
 struct Lanes2 {
-  uint32_t lreg[4];   // 4 (8 (i^g) + c)  (G; J2 is +128, folded into the ds_read offset)
-  uint32_t sel[4];    // v_perm selector: addr = {0, 0, x.b(i^g), S1.b0}
+  uint32_t lpack;     // byte i: 4 (8 (i^g) + c)  (G; J2 is +128, folded into the ds_read offset)
+  uint32_t sel[4];    // v_perm selector: addr = {0, 0, x.b(i^g), lpack.b(i)}
 };
 
 __device__ __forceinline__ Lanes2 lanes2(uint32_t lane) {
   Lanes2 k;
   const uint32_t c = lane & 7, g = (lane >> 3) & 3;
+  k.lpack = 0;
 #pragma unroll
   for (uint32_t i = 0; i < 4; ++i) {
     const uint32_t tt = i ^ g;
-    k.lreg[i] = 4 * (8 * tt + c);
-    k.sel[i] = 0x0c0c0000u | ((4 + tt) << 8);
+    k.lpack |= (4 * (8 * tt + c)) << (8 * i);
+    k.sel[i] = 0x0c0c0000u | ((4 + tt) << 8) | i;
   }
   return k;
 }
@@ -586,7 +587,7 @@ __device__ __forceinline__ uint32_t rep_map(const uint8_t* __restrict__ Lb, cons
   uint32_t r = 0;
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    r ^= lds32(Lb, __builtin_amdgcn_perm(x, k.lreg[i], k.sel[i]) + (J ? 128u : 0u));
+    r ^= lds32(Lb, __builtin_amdgcn_perm(x, k.lpack, k.sel[i]) + (J ? 128u : 0u));
   return r;
 }
 
@@ -821,7 +822,7 @@ __device__ __forceinline__ void rep_look(const uint8_t* __restrict__ Lb, const L
                                          uint32_t x, uint32_t (&l)[4]) {
 #pragma unroll
   for (int i = 0; i < 4; ++i)
-    l[i] = lds32(Lb, __builtin_amdgcn_perm(x, k.lreg[i], k.sel[i]) + (J ? 128u : 0u));
+    l[i] = lds32(Lb, __builtin_amdgcn_perm(x, k.lpack, k.sel[i]) + (J ? 128u : 0u));
 }
 
 // G(x) ^ e: the next chain input when e is the next data word
@@ -1160,6 +1161,13 @@ __global__ void __launch_bounds__(kThreads) crc32c_stream2_probe_kernel(BlockArg
 // LDS: [0, 64K) G and J3 interleaved as in the v2 kernel, [64K, 124K) A[1..15],
 // [124K, 128K) B[1].
 // ---------------------------------------------------------------------------
+// verify results staged in LDS and stored after the loop (1), or stored as
+// rows finish (0): result stores in the streaming loop cost C2 verify 4.7 %
+// (stores share vmcnt with the loads; profiles/ab_r04/c2_verify_stores.log)
+#ifndef FORST_ROWS_STAGE
+#define FORST_ROWS_STAGE 1
+#endif
+constexpr uint32_t kStageW = 6144;  // results per workgroup (30 KiB of LDS)
 constexpr uint32_t kRowRound = 1024;
 constexpr uint32_t kRowChain = 512;
 constexpr uint32_t kLds3Bytes = kOffB2 + 4096;
@@ -1412,7 +1420,13 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   constexpr bool kWgFeed = MODE != kModeRaw || RAW_WG;
   constexpr uint32_t kChunk = 4;
   uint64_t cg = feed_first<kWgFeed, kChunk>(a, nw, gw, lane, feed);
-  if (cg >= a.n) return;
+  // verify: results staged in LDS, stored after the loop by the whole
+  // workgroup (so every wave reaches the end: no early return)
+  constexpr bool kStage = FORST_ROWS_STAGE && MODE != kModeRaw && kWgFeed && DEPTH == 1 &&
+                          PROBE == 0;
+  __shared__ uint32_t st_out[kStage ? kStageW : 1];
+  __shared__ uint8_t st_ok[kStage ? kStageW : 4];
+  if (!kStage && cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
   uint64_t ng = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
   uint32_t nlen = feed.len;
@@ -1622,17 +1636,32 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
         const uint32_t st = stored - cu.mod;
         ok = valid && st == computed;
-        if (mine && a.out32) a.out32[i] = valid ? computed : 0u;
+        // the workgroup's first kStageW results go to LDS (written after the
+        // loop), the rest (ranges longer than that) directly
+        const uint64_t sj = i - feed.wlo;
+        const bool staged = kStage && sj < kStageW;
+        if (mine && staged) {
+          st_out[sj] = valid ? computed : 0u;
+          st_ok[sj] = ok ? 1 : 0;
+        }
+        if (mine && !staged && a.out32) a.out32[i] = valid ? computed : 0u;
         if (mine && a.stored_out) a.stored_out[i] = valid ? st : 0u;
-        if (mine && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (mine && !staged && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (staged) ok = true;  // (counted in the flush)
       } else {
         const uint32_t out = crc_mask(crc) + cu.mod;  // format.cc:594-600 + builder.cc:1340-1345
-        if (mine && a.out32) a.out32[i] = valid ? out : 0u;
+        const uint64_t sj = i - feed.wlo;
+        const bool staged = kStage && sj < kStageW;  // (see verify)
+        if (mine && staged) {
+          st_out[sj] = valid ? out : 0u;
+          st_ok[sj] = valid ? 1 : 0;
+        }
+        if (mine && !staged && a.out32) a.out32[i] = valid ? out : 0u;
         if (MODE == kModeTrailer) {
           // the 5 trailer bytes [type][LE32] by lanes 11..15 of the row: one
           // byte store per wave instead of five per finishing row
           const uint32_t k = t - 11;
-          if (calc && valid && (k != 0 || a.last_bytes)) {
+          if (!staged && calc && valid && (k != 0 || a.last_bytes)) {
             uint8_t* pw = a.base_w + C.template end<MODE>(mem_last_byte<MODE>(a));
             pw[k] = static_cast<uint8_t>(k == 0 ? cu.extra : out >> (8 * (k - 1)));
           }
@@ -1677,6 +1706,35 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
 #ifdef FORST_DIAG
   if (lane == 0 && gw < kDiagWaves) g_wave_t1[gw] = wall_clock64();
 #endif
+  if constexpr (kStage) {  // the staged results, coalesced
+    __syncthreads();
+    const uint64_t lo = feed.wlo, hi = feed.whi;
+    const uint64_t m = hi > lo ? (hi - lo < kStageW ? hi - lo : kStageW) : 0;
+    uint32_t bad = 0;
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+      const uint64_t g = lo + j;
+      if (a.out32) a.out32[g] = st_out[j];
+      if (MODE == kModeVerify) {
+        if (a.ok_out) a.ok_out[g] = st_ok[j];
+        bad += st_ok[j] ? 0u : 1u;
+      }
+      if (MODE == kModeTrailer && st_ok[j]) {  // [type][LE32] at offset + size
+        uint8_t* pw = a.base_w + a.offsets[g] + a.sizes[g];
+        const uint32_t v = st_out[j];
+        if (a.last_bytes) pw[0] = a.last_bytes[g];
+        pw[1] = static_cast<uint8_t>(v);
+        pw[2] = static_cast<uint8_t>(v >> 8);
+        pw[3] = static_cast<uint8_t>(v >> 16);
+        pw[4] = static_cast<uint8_t>(v >> 24);
+      }
+    }
+    if (MODE == kModeVerify && a.mismatches) {
+      uint32_t wb = bad;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wb += __shfl_xor(wb, o);
+      if (lane == 0 && wb) atomicAdd(a.mismatches, static_cast<unsigned long long>(wb));
+    }
+  }
 }
 
 template <int MODE>

@@ -35,6 +35,13 @@ constexpr uint32_t kRowsThreads = kRowsWaves * 64;
 #define FORST_XX_WG_CHUNK 4
 #endif
 constexpr uint32_t kXxWgChunk = FORST_XX_WG_CHUNK;
+// block modes: results staged in LDS and stored after the loop (1) or as
+// rows finish (0); the workgroup's first kXxStageW results (96 KiB: the
+// kernel runs one 12-wave workgroup per CU for its registers anyway)
+#ifndef FORST_XX_STAGE
+#define FORST_XX_STAGE 1
+#endif
+constexpr uint32_t kXxStageW = 16384;
 // fused WAL recovery: the four CRC column chains of a step interleaved (1) or
 // one after the other (0, the round-3 form)
 #ifndef FORST_FRAG_CRC_IL
@@ -801,7 +808,14 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
   // index (n < 2^32 - 1), kbrel the stream position of cb's first entry
   BatchFeed feed;
   uint64_t cg = feed_first<MODE != kModeRaw, kXxWgChunk>(a, nw, gw, lane, feed);
-  if (cg >= a.n) return;
+  // block modes: results staged in LDS and stored after the loop by the
+  // whole workgroup (as crc32c_rows_kernel: stores share vmcnt with the
+  // stream's loads), so every wave reaches the end: no early return
+  constexpr bool kStage = FORST_XX_STAGE && MODE != kModeRaw;
+  __shared__ uint32_t st_out[kStage ? kXxStageW : 1];
+  __shared__ uint8_t st_ok[kStage ? kXxStageW : 4];  // verify: ok; else: valid
+  __shared__ uint8_t st_lb[MODE == kModeTrailer && kStage ? kXxStageW : 4];
+  if (!kStage && cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
   uint64_t ng = feed_next<MODE != kModeRaw, kXxWgChunk>(a, nw, lane, feed);
   uint32_t nlen = feed.len;
@@ -939,13 +953,27 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
         const uint32_t computed = modify_for_last_byte(static_cast<uint32_t>(h), lastb);
         const uint32_t st = stored - cu.mod;
         ok = valid && st == computed;
-        if (mine && a.out32) a.out32[i] = valid ? computed : 0u;
+        const uint64_t sj = i - feed.wlo;
+        const bool staged = kStage && sj < kXxStageW;
+        if (mine && staged) {
+          st_out[sj] = valid ? computed : 0u;
+          st_ok[sj] = ok ? 1 : 0;
+        }
+        if (mine && !staged && a.out32) a.out32[i] = valid ? computed : 0u;
         if (mine && a.stored_out) a.stored_out[i] = valid ? st : 0u;
-        if (mine && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (mine && !staged && a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (staged) ok = true;  // (counted after the loop)
       } else {
         const uint32_t out = modify_for_last_byte(static_cast<uint32_t>(h), lastb) + cu.mod;
-        if (mine && a.out32) a.out32[i] = valid ? out : 0u;
-        if (MODE == kModeTrailer && mine && valid) {
+        const uint64_t sj = i - feed.wlo;
+        const bool staged = kStage && sj < kXxStageW;
+        if (mine && staged) {
+          st_out[sj] = valid ? out : 0u;
+          st_ok[sj] = valid ? 1 : 0;
+          if (MODE == kModeTrailer) st_lb[sj] = static_cast<uint8_t>(lastb);
+        }
+        if (mine && !staged && a.out32) a.out32[i] = valid ? out : 0u;
+        if (MODE == kModeTrailer && mine && valid && !staged) {
           uint8_t* w = a.base_w + off + C.size;
           w[0] = static_cast<uint8_t>(lastb);
           stu32_bytes(w + 1, out);
@@ -962,6 +990,31 @@ __global__ void __launch_bounds__(kRowsThreads) FORST_WAVES_PER_EU(3)
     return true;
   };
   while (step(X, Y) && step(Y, X)) {
+  }
+  if constexpr (kStage) {  // the staged results, coalesced
+    __syncthreads();
+    const uint64_t lo = feed.wlo, hi = feed.whi;
+    const uint64_t m = hi > lo ? (hi - lo < kXxStageW ? hi - lo : kXxStageW) : 0;
+    uint32_t bad = 0;
+    for (uint32_t j = threadIdx.x; j < m; j += blockDim.x) {
+      const uint64_t g = lo + j;
+      if (a.out32) a.out32[g] = st_out[j];
+      if (MODE == kModeVerify) {
+        if (a.ok_out) a.ok_out[g] = st_ok[j];
+        bad += st_ok[j] ? 0u : 1u;
+      }
+      if (MODE == kModeTrailer && st_ok[j]) {  // [last byte][LE32] at offset + size
+        uint8_t* w = a.base_w + a.offsets[g] + a.sizes[g];
+        w[0] = st_lb[j];
+        stu32_bytes(w + 1, st_out[j]);
+      }
+    }
+    if (MODE == kModeVerify && a.mismatches) {
+      uint32_t wb = bad;
+#pragma unroll
+      for (int o = 32; o > 0; o >>= 1) wb += __shfl_xor(wb, o);
+      if (lane == 0 && wb) atomicAdd(a.mismatches, static_cast<unsigned long long>(wb));
+    }
   }
 }
 

@@ -177,18 +177,21 @@ int dispatch_blocks(int type, int mode, const BlockArgs& a, void* stream) {
   if (type < FORST_kNoChecksum || type > FORST_kXXH3)  // options_helper.h:34
     return set_error(FORST_EINVAL, "unknown ChecksumType " + std::to_string(type));
   hipStream_t s = static_cast<hipStream_t>(stream);
-  // Write side: the streaming kernel runs in compute mode and the 5 trailer
-  // bytes per block are stored by a second, tiny kernel.  Trailer bytes are
-  // partial writes into 64 B memory sectors shared with block data (a
-  // read-modify-write below the L2); done inside the streaming kernel they
-  // cost 16 % of the pass (C2), split off 8 % (tools/gpu_trailer_ab.sh; a
-  // read-merge-write of the covering dwords in the scatter kernel measured
-  // the same).
-  // (diagnostics build: FORST_TRAILER=fused keeps them in the streaming
-  // kernel, the A/B reference)
-  bool split = true;
+  // Write side: the 5 trailer bytes per block are partial writes into 64 B
+  // memory sectors shared with block data (a read-modify-write below the
+  // L2).  Stored by the streaming kernel as rows finish they cost 16 % of
+  // the pass (C2, round 1), split off into a second, tiny kernel 8 %.  Since
+  // round 4 the rows kernels stage a workgroup's results in LDS and write
+  // them after their loop, which beats the split form (C2 write side -1.4 %,
+  // NS16X -0.2 %, profiles/ab_r04/trailer_fused_staged.log);
+  // FORST_TRAILER_SPLIT=1 builds the split form.
+  // (diagnostics build: FORST_TRAILER=fused|split at run time)
+#ifndef FORST_TRAILER_SPLIT
+#define FORST_TRAILER_SPLIT 0
+#endif
+  bool split = FORST_TRAILER_SPLIT;
 #ifdef FORST_DIAG
-  split = std::string(diag_env("FORST_TRAILER")) != "fused";
+  if (*diag_env("FORST_TRAILER")) split = std::string(diag_env("FORST_TRAILER")) != "fused";
 #endif
   if (mode == kModeTrailer && split && a.n) {
     BlockArgs c = a;

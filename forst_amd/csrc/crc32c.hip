@@ -1365,7 +1365,7 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
   if (MODE != kModeRaw)
     d.mod = a.modifiers ? a.modifiers[idx] : 0u;
   else
-    d.mod = 0u;
+    d.mod = a.expect ? a.expect[idx] : 0u;  // (raw: the expected CRC)
   if (MODE == kModeRaw)
     d.extra = a.init_crcs ? a.init_crcs[idx] : 0u;
   else if (MODE != kModeVerify)
@@ -1631,7 +1631,8 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         // loads on gfx950, so scattered partial-line stores here made every
         // later step wait for them (C5 writer 9.19 -> 9.90 ms)
         const uint32_t v = a.wal_hs ? crc_mask(crc) : crc;
-        if (mine && a.out32) a.out32[i] = valid ? v : 0u;
+        const bool differs = !a.expect || !valid || v != cu.mod;
+        if (mine && differs && a.out32) a.out32[i] = valid ? v : 0u;
       } else if (MODE == kModeVerify) {
         const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
         const uint32_t st = stored - cu.mod;

@@ -55,6 +55,10 @@ struct BlockArgs {
   // header[6..hs) + payload (log_writer.cc:240-263) and out32 gets it masked
   // (util/crc32c.h:33)
   uint32_t wal_hs;
+  // raw CRC mode: expected values; out32[i] is written only where the CRC
+  // differs (the caller pre-fills out32 with them), so a clean verify stores
+  // nothing from the streaming loop (stores share vmcnt with its loads)
+  const uint32_t* expect;
 };
 
 struct WalArgs {

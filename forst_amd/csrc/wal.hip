@@ -202,16 +202,21 @@ __global__ void __launch_bounds__(kTile) wal_fill_kernel(WalArgs a, WalScratch s
     if (cnt) {
       if (staged)
         walk_block<true>(a, a.first_block + bi, &stop, excl, l_off, l_len, l_st);
-      else
+      else {
         walk_block<true>(a, a.first_block + bi, &stop, base, s.desc_off, s.desc_len, s.stored);
+        for (uint32_t j = 0; j < cnt; ++j) s.computed[base + j] = s.stored[base + j];
+      }
     }
   }
+  // computed[] pre-filled with the stored CRCs (crc_records' expect: the CRC
+  // kernel overwrites only the records whose CRC differs)
   if (staged) {
     __syncthreads();
     for (uint32_t i = threadIdx.x; i < tot; i += kTile) {
       s.desc_off[wg_base + i] = l_off[i];
       s.desc_len[wg_base + i] = l_len[i];
       s.stored[wg_base + i] = l_st[i];
+      s.computed[wg_base + i] = l_st[i];
     }
   }
 }
@@ -421,9 +426,12 @@ namespace {
 
 // out[i] = crc32c::Extend(0, base + off[i], len[i]) for a record list
 // (FORST_WAL_SPLIT=1: split by size between the rows and v2 kernels)
+#ifndef FORST_WAL_EXPECT
+#define FORST_WAL_EXPECT 1
+#endif
 hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* off,
                        const uint32_t* len, uint64_t n, uint32_t* out, hipStream_t stream,
-                       const char** name) {
+                       const char** name, const uint32_t* expect = nullptr) {
   BlockArgs b{};
   b.base = base;
   b.base_len = base_len;
@@ -431,6 +439,7 @@ hipError_t crc_records(const uint8_t* base, uint64_t base_len, const uint64_t* o
   b.sizes = len;
   b.out32 = out;
   b.n = n;
+  b.expect = expect;  // (out pre-filled with it)
   // default: one launch (the rows kernel for this size mix); the split is an
   // A/B variant (C5: 0.499 one launch vs 0.478 split, tools/wal_ab.py)
 #ifndef FORST_DIAG
@@ -537,7 +546,11 @@ hipError_t launch_wal_verify(const WalArgs& a, hipStream_t stream, const char** 
   s.stored = reinterpret_cast<uint32_t*>(static_cast<uint8_t*>(desc) + sz_off + 2 * sz_len);
   hipLaunchKernelGGL(wal_fill_kernel, grid, dim3(kTile), 0, stream, a, s);
   *name = "wal_walk_kernel";
-  if (total) e = crc_records(a.log, a.log_len, s.desc_off, s.desc_len, total, s.computed, stream, name);
+  // computed[] arrives pre-filled with the stored CRCs (wal_fill_kernel):
+  // the CRC kernel writes only the records whose CRC differs
+  if (total)
+    e = crc_records(a.log, a.log_len, s.desc_off, s.desc_len, total, s.computed, stream, name,
+                    FORST_WAL_EXPECT ? s.stored : nullptr);
   hipLaunchKernelGGL(wal_status_kernel, grid, dim3(kTile), 0, stream, a, s);
   if (e == hipSuccess) e = hipGetLastError();
   const hipError_t f1 = scratch_free(desc, stream), f2 = scratch_free(scratch, stream);

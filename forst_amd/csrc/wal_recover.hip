@@ -1380,9 +1380,10 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         fa.init_crcs = q.l_info;
         fa.modifiers = q.l_first;
         fa.crc_ez = q.c.ez;
-        fa.crc_ok = q.crc_ok;
+        fa.crc_ok = q.crc_ok;  // pre-filled with 1: the fused kernel stores mismatches only
         fa.out64 = q.cand_hash;
         fa.n = n_cand;
+        if ((e = hipMemsetAsync(q.crc_ok, 1, ni, st)) != hipSuccess) return fail(e);
         const char* fname = nullptr;
         if ((e = launch_xxh3_frag_crc(fa, st, &fname)) != hipSuccess) return fail(e);
       }

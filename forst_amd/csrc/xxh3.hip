@@ -1540,7 +1540,8 @@ xxh3_frag_kernel(BlockArgs a) {
       };
       if (__ballot(ends)) {
         const uint32_t V = row_value(cs) ^ (started ? cu.ez[0] : 0u);
-        if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
+        // (the caller pre-fills crc_ok with 1: only mismatches are stored)
+        if (ends && t == 0 && V != cu.ez[1]) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = 0;
 
         const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
@@ -1575,7 +1576,7 @@ xxh3_frag_kernel(BlockArgs a) {
           const bool endsB = pb && L - W0 <= 1024u;
           const uint32_t VB = row_value(sb) ^ cu.ez[2];
           if (endsB && t == 0)
-            a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = VB == cu.ez[3] ? 1 : 0;
+            if (VB != cu.ez[3]) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = 0;
           if (pb && !endsB) {
 #pragma unroll
             for (uint32_t k = 0; k < 4; ++k) ns[k] = sb[k];

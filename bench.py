@@ -515,7 +515,11 @@ def main():
         cpu = cpu_baseline(b, main_res["ctype"])
     if world == 1 and not args.no_extras:
         try:
-            extras["end_to_end_pcie_GiBps"] = round(end_to_end_pcie(b, main_res["ctype"]), 2)
+            # the first pass pays one-time costs (host pinning, first touch of
+            # the staging buffers): best of 3 passes, the first reported too
+            e2e = [end_to_end_pcie(b, main_res["ctype"]) for _ in range(3)]
+            extras["end_to_end_pcie_GiBps"] = round(max(e2e), 2)
+            extras["end_to_end_pcie_first_pass_GiBps"] = round(e2e[0], 2)
         except Exception as e:  # pragma: no cover
             extras["end_to_end_pcie_error"] = str(e)
         try:

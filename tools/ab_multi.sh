@@ -1,6 +1,6 @@
 #!/bin/bash
 # A/B/C... of several builds of the library on one box, alternating processes:
-#   tools/ab_multi.sh <tag> <config> <lib>...   (config C5 = tools/prof_wal.py, A14 = tools/prof_a14.py, SW = tools/prof_small_wal.py, B:<cfg> = tools/prof_blocks.py <cfg>)
+#   tools/ab_multi.sh <tag> <config> <lib>...   (config C5 = tools/prof_wal.py, A14 = tools/prof_a14.py, E2E = tools/prof_e2e.py, SW = tools/prof_small_wal.py, B:<cfg> = tools/prof_blocks.py <cfg>)
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 TAG=$1; c=$2; shift 2
@@ -17,6 +17,9 @@ for r in 1 2 3; do
     elif [ "$c" = SW ]; then
       timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_small_wal.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
       echo "SW $(basename $L) $(tail -1 "$OUT/ab.log")"
+    elif [ "$c" = E2E ]; then
+      timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_e2e.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
+      echo "E2E $(basename $L) $(tail -1 "$OUT/ab.log")"
     elif [ "$c" = A14 ]; then
       timeout -k 10 300 python -u tools/with_lib.py $L tools/prof_a14.py > "$OUT/ab.log" 2>&1 || { tail -20 "$OUT/ab.log"; exit 1; }
       echo "A14 $(basename $L) $(tail -1 "$OUT/ab.log")"

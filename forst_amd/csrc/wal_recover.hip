@@ -861,6 +861,30 @@ struct CtlReps {
   }
 };
 
+// where the XXH3 state feeding a record was last reset: the log start, the
+// token after an emitted record, or a First that starts over a partial
+// record ("partial record without end(2)")
+__device__ __forceinline__ bool hb_start(const Tokens& t, const Fsm& f, const uint64_t* n_emit,
+                                         uint64_t p) {
+  if (p == 0 || n_emit[p - 1]) return true;
+  if (t.kind[p] != kTkFirst) return false;
+  bool in_frag;
+  uint64_t scratch;
+  prev_state(f, p, &in_frag, &scratch);
+  return in_frag && scratch;
+}
+constexpr uint32_t kHashWalk = 64;
+__global__ void __launch_bounds__(kLanes) rw_hb_flag_kernel(Tokens t, Fsm f, uint64_t n,
+                                                            const uint64_t* n_emit, uint64_t* fl) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i < n) fl[i] = hb_start(t, f, n_emit, i) ? 1u : 0u;
+}
+__global__ void __launch_bounds__(kLanes) rw_hb_pos_kernel(const uint64_t* fl, const uint64_t* cnt,
+                                                           uint64_t n, uint64_t* pos) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
+  if (i < n && fl[i]) pos[cnt[i]] = i;
+}
+
 // per token: emitted logical records (0/1) and reports -- or, with WRITE,
 // the records and reports themselves at their scanned positions
 template <bool WRITE>
@@ -871,7 +895,10 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
                                                          forst_wal_records recs, uint64_t rec_cap,
                                                          forst_wal_reports reps, uint64_t rep_cap,
                                                          uint64_t* rec_hash_begin,
-                                                         uint64_t* rec_last_tok) {
+                                                         uint64_t* rec_last_tok,
+                                                         const uint64_t* hb_cnt,
+                                                         const uint64_t* hb_pos,
+                                                         unsigned long long* hb_over) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= n) return;
   const uint8_t k = t.kind[i];
@@ -967,14 +994,18 @@ __global__ void __launch_bounds__(kLanes) rw_emit_kernel(Tokens t, uint64_t n, F
     // started (the token after the previous emitted record) or at a
     // "partial record without end(2)" First; a Full record is hashed alone
     uint64_t hb = i;
-    if (k == kTkLast) {
+    if (k == kTkLast && hb_pos) {  // the linear form (rw_hb_flag_kernel): the last start <= first
+      hb = hb_pos[hb_cnt[first] + hb_start(t, f, n_emit, first) - 1];
+    } else if (k == kTkLast) {
+      // walk back over the tokens no record was emitted for, at most
+      // kHashWalk of them (a crafted log of long non-emitting runs made this
+      // O(run) on one thread); beyond that the host runs the linear form
       hb = first;
-      while (hb > 0 && !n_emit[hb - 1]) {
-        if (t.kind[hb] == kTkFirst) {
-          bool in_frag;
-          uint64_t scratch;
-          prev_state(f, hb, &in_frag, &scratch);
-          if (in_frag && scratch) break;
+      uint32_t steps = 0;
+      while (!hb_start(t, f, n_emit, hb)) {
+        if (++steps > kHashWalk) {
+          atomicAdd(hb_over, 1ull);
+          break;
         }
         --hb;
       }
@@ -1447,7 +1478,8 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   // count and the stop token (one sync)
   auto count_pass = [&]() -> hipError_t {
     hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
-                       q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr);
+                       q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr,
+                       nullptr, nullptr, nullptr);
     scan_u64(q.n_emit, n_tok, q.tiles2, q.emit_at, st);
     hipError_t r = hipMemcpyAsync(&tot[0], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
     scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (after the copy above, stream order)
@@ -1595,9 +1627,11 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     hash_begin = A4.take<uint64_t>(nr);
     last_tok = A4.take<uint64_t>(nr);
   }
+  unsigned long long* hb_over = q.live_over;  // (reused: rw_live is done with it)
+  (void)hipMemsetAsync(hb_over, 0, 8, st);
   hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
                      nullptr, q.emit_at, q.rep_at, cr, full, nr, reps, rep_cap, hash_begin,
-                     last_tok);
+                     last_tok, nullptr, nullptr, hb_over);
   if (nr) {
     // records that are exactly a candidate already have their hash (the
     // fused kernel); the rest are hashed here (sync: how many)
@@ -1612,14 +1646,36 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     uint64_t* tiles5 = A5.take<uint64_t>(nr / kScanTile + 2);
     Cand cm = q.c;
     if (!n_cand) cm.head = nullptr;
-    hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,
-                       last_tok, nr, cm, q.cpos, q.cand_hash, full.hash, need);
-    scan_u64(need, nr, tiles5, npos, st);
-    uint64_t n_need = 0;
-    if ((e = hipMemcpyAsync(&n_need, tiles5 + (nr + kScanTile - 1) / kScanTile, 8,
-                            hipMemcpyDeviceToHost, st)) != hipSuccess ||
-        (e = hipStreamSynchronize(st)) != hipSuccess)
-      return fail(e);
+    uint64_t n_need = 0, over = 0;
+    auto match = [&]() {
+      hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,
+                         last_tok, nr, cm, q.cpos, q.cand_hash, full.hash, need);
+      scan_u64(need, nr, tiles5, npos, st);
+      hipError_t r = hipMemcpyAsync(&n_need, tiles5 + (nr + kScanTile - 1) / kScanTile, 8,
+                                    hipMemcpyDeviceToHost, st);
+      if (r == hipSuccess) r = hipMemcpyAsync(&over, hb_over, 8, hipMemcpyDeviceToHost, st);
+      if (r == hipSuccess) r = hipStreamSynchronize(st);
+      return r;
+    };
+    if ((e = match()) != hipSuccess) return fail(e);
+    if (over) {  // a non-emitting run longer than the walk's cap: the linear form, again
+      const uint64_t nt1 = n_tok + 1;
+      void* hv = nullptr;
+      if ((e = alloc(up256(8 * nt1) * 3 + up256(8 * (nt1 / kScanTile + 2)), &hv)) != hipSuccess)
+        return fail(e);
+      Arena AH{static_cast<uint8_t*>(hv), 0};
+      uint64_t* fl = AH.take<uint64_t>(nt1);
+      uint64_t* cnt = AH.take<uint64_t>(nt1);
+      uint64_t* pos = AH.take<uint64_t>(nt1);
+      uint64_t* tl = AH.take<uint64_t>(nt1 / kScanTile + 2);
+      hipLaunchKernelGGL(rw_hb_flag_kernel, tg, dim3(kLanes), 0, st, t, f, n_tok, q.n_emit, fl);
+      scan_u64(fl, n_tok, tl, cnt, st);
+      hipLaunchKernelGGL(rw_hb_pos_kernel, tg, dim3(kLanes), 0, st, fl, cnt, n_tok, pos);
+      hipLaunchKernelGGL(rw_emit_kernel<true>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode,
+                         q.n_emit, nullptr, q.emit_at, q.rep_at, cr, full, nr, reps, rep_cap,
+                         hash_begin, last_tok, cnt, pos, hb_over);
+      if ((e = match()) != hipSuccess) return fail(e);
+    }
     if (n_need) {
       hipLaunchKernelGGL(rw_need_list_kernel, grid_for(nr), dim3(kLanes), 0, st, need, npos, nr,
                          sub);

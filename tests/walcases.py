@@ -342,7 +342,7 @@ def long_control_runs(recyclable, run=200, seed=41):
     ln = 7
     base = 4 if recyclable else 0
     ts_type = 11 if recyclable else 10
-    lens = np.full(3 * run + 60, 12, np.uint32)
+    lens = np.full(4 * run + 80, 12, np.uint32)
     buf, po, pl = frame_lens(lens, seed, recyclable, ln)
     assert len(po) == len(lens)
 
@@ -374,4 +374,9 @@ def long_control_runs(recyclable, run=200, seed=41):
     k += run + 10
     for i in range(run):                          # Full ... run ... Full
         control(k + i, i)
+    k += run + 10
+    for i in range(run):                          # Full ... run ... First Last
+        control(k + i, i)                         # (the Last's hash start walks back
+    set_type(buf, int(po[k + run]), 2 + base)     # over the run: rw_emit's capped walk)
+    set_type(buf, int(po[k + run + 1]), 4 + base)
     return [("long_ctl", buf, ln)]

@@ -72,26 +72,6 @@ __device__ __forceinline__ uint32_t chunk_step(const uint8_t* __restrict__ Lb, c
   return g_then(Lb, k, x, 0u);
 }
 
-// chunk_step on four independent chains at once: each dependent level issues
-// the table reads of all four chains before any of them is waited for
-__device__ __forceinline__ void chunk_step4(const uint8_t* __restrict__ Lb, const Lanes& k,
-                                            uint32_t (&s)[4], const uint32_t (&w)[4][4]) {
-  uint32_t x[4];
-#pragma unroll
-  for (int c = 0; c < 4; ++c) {
-    uint32_t lj[4], lg[4];
-    look<true>(Lb, k, s[c], lj);
-    look<false>(Lb, k, w[c][0], lg);
-    x[c] = xor3(xor3(lj[0], lj[1], lj[2]), xor3(lj[3], lg[0], lg[1]), xor3(lg[2], lg[3], w[c][1]));
-  }
-#pragma unroll
-  for (int c = 0; c < 4; ++c) x[c] = g_then(Lb, k, x[c], w[c][2]);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) x[c] = g_then(Lb, k, x[c], w[c][3]);
-#pragma unroll
-  for (int c = 0; c < 4; ++c) s[c] = g_then(Lb, k, x[c], 0u);
-}
-
 // the mask of dword i of a 16-byte chunk whose first n bytes are kept (n >=
 // 16: all): the high word of 0xffffffff << 8 clamp(n - 4 i, 0, 4)
 __device__ __forceinline__ uint32_t keep_word(uint32_t n, uint32_t i) {

@@ -42,11 +42,14 @@ constexpr uint32_t kXxWgChunk = FORST_XX_WG_CHUNK;
 #define FORST_XX_STAGE 1
 #endif
 constexpr uint32_t kXxStageW = 16384;
-// fused WAL recovery: the four CRC column chains of a step interleaved (1) or
-// one after the other (0, the round-3 form)
-#ifndef FORST_FRAG_CRC_IL
-#define FORST_FRAG_CRC_IL 0
+// fused WAL recovery: one CRC chain per lane through its four chunks of a
+// window (1: a 240-byte hop between chunks, J244, so a fragment's finish
+// needs no column merge), or one chain per chunk column (0: the round-3
+// form, a 1008-byte hop, J1012, and three C256 shifts in every finish)
+#ifndef FORST_FRAG_ONECHAIN
+#define FORST_FRAG_ONECHAIN 1
 #endif
+constexpr uint32_t kNC = FORST_FRAG_ONECHAIN ? 1 : 4;
 // the fragment kernel's lane constants recomputed where used (1) or left to
 // the compiler, which hoists and, at 168 VGPRs, spills them (0)
 #ifndef FORST_FRAG_FRESH
@@ -1218,7 +1221,9 @@ __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
   for (uint32_t k = 0; k < kN1; ++k) {
     const uint32_t i = tid + k * NT;
     const uint32_t e = (i >> 6) & 255, d = i & 63, t = (d >> 3) & 3;
-    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e] : kCrcJ1012[t * 256 + e]) : 0u;
+    v1[k] = i < 16384 ? (d < 32 ? kCrcG[t * 256 + e]
+                                : (kNC == 1 ? kCrcJ244[t * 256 + e] : kCrcJ1012[t * 256 + e]))
+                      : 0u;
   }
 #pragma unroll
   for (uint32_t k = 0; k < kN2; ++k) {
@@ -1363,7 +1368,9 @@ xxh3_frag_kernel(BlockArgs a) {
 #pragma unroll
   for (int d = 1; d < DEPTH; ++d) frag_issue<CRC>(a, lane, Q[d - 1], B[d]);
   uint64_t acc0 = 0, acc1 = 0;
-  uint32_t crc_s[4] = {0u, 0u, 0u, 0u};  // (fused CRC) the lane's column chains
+  uint32_t crc_s[kNC];  // (fused CRC) the lane's chain(s)
+#pragma unroll
+  for (uint32_t k = 0; k < kNC; ++k) crc_s[k] = 0u;
   const fcrc::Lanes FK = fcrc::lanes(lane);
   auto step = [&](FStep& cu, FStep& nx) -> bool {
     // no early return: both step copies issue on every path round the loop,
@@ -1455,15 +1462,9 @@ xxh3_frag_kernel(BlockArgs a) {
       const uint32_t W0 = 1024u * C.g;
       hiA = fe - W0 < 1024u ? fe - W0 : 1024u;
     }
-    uint32_t cs[4] = {crc_s[0], crc_s[1], crc_s[2], crc_s[3]};
-#if FORST_FRAG_CRC_IL
-    // (fused CRC) the four column chains advance together, one dependent
-    // LDS level at a time (fcrc::chunk_step4), and the bytes past the
-    // fragment end are masked in one wave-uniform branch ahead of them: with
-    // a mask branch per chunk every chain sat in its own basic block and the
-    // 4 chains' 16 table-read levels ran back to back
-    uint32_t cw[4][4];
-#endif
+    uint32_t cs[kNC];
+#pragma unroll
+    for (uint32_t k = 0; k < kNC; ++k) cs[k] = crc_s[k];
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k) {
       uint64_t d0, d1;
@@ -1473,18 +1474,13 @@ xxh3_frag_kernel(BlockArgs a) {
       const bool use = C.g < nbC || s4 + 4 * k < nbSC;
       sum0 += use ? c0 : 0ull;
       sum1 += use ? c1 : 0ull;
-#if FORST_FRAG_CRC_IL
-      cw[k][0] = static_cast<uint32_t>(d0);
-      cw[k][1] = static_cast<uint32_t>(d0 >> 32);
-      cw[k][2] = static_cast<uint32_t>(d1);
-      cw[k][3] = static_cast<uint32_t>(d1 >> 32);
-#else
       if (CRC) {
+        const uint32_t kc = kNC == 1 ? 0u : k;  // the chain: the lane's one, or column k's
         const uint32_t q = 16 * t + 256 * k;
 #if FORST_FRAG_MASK_LDS
         const uint32_t n = hiA > q ? (hiA - q < 16u ? hiA - q : 16u) : 0u;
         const u32x4 m = *reinterpret_cast<const u32x4*>(kmask + 4 * n);
-        cs[k] = fcrc::chunk_step(Lb, FK, cs[k], static_cast<uint32_t>(d0) & m.x,
+        cs[kc] = fcrc::chunk_step(Lb, FK, cs[kc], static_cast<uint32_t>(d0) & m.x,
                                  static_cast<uint32_t>(d0 >> 32) & m.y,
                                  static_cast<uint32_t>(d1) & m.z,
                                  static_cast<uint32_t>(d1 >> 32) & m.w);
@@ -1492,27 +1488,12 @@ xxh3_frag_kernel(BlockArgs a) {
         uint64_t m0 = ~0ull, m1 = ~0ull;
         if (hiA < q + 16) fcrc::keep_mask(0, hiA > q ? hiA - q : 0u, m0, m1);
         const uint64_t e0 = d0 & m0, e1 = d1 & m1;
-        cs[k] = fcrc::chunk_step(Lb, FK, cs[k], static_cast<uint32_t>(e0),
-                                 static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
-                                 static_cast<uint32_t>(e1 >> 32));
+        cs[kc] = fcrc::chunk_step(Lb, FK, cs[kc], static_cast<uint32_t>(e0),
+                                  static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
+                                  static_cast<uint32_t>(e1 >> 32));
 #endif
       }
-#endif
     }
-#if FORST_FRAG_CRC_IL
-    if (CRC) {
-      if (__ballot(hiA < 1024u)) {  // some row's fragment ends inside its window
-#pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
-          const uint32_t q = 16 * t + 256 * k;
-          const uint32_t n = hiA > q ? hiA - q : 0u;  // bytes of the chunk kept (>= 16: all)
-#pragma unroll
-          for (uint32_t i = 0; i < 4; ++i) cw[k][i] &= fcrc::keep_word(n, i);
-        }
-      }
-      fcrc::chunk_step4(Lb, FK, cs, cw);
-    }
-#endif
     if (CRC) {
       // the fragment's end in this window: finish it (and a fragment that
       // starts here: second pass); else carry the chain, E added at the end
@@ -1524,14 +1505,16 @@ xxh3_frag_kernel(BlockArgs a) {
       const uint32_t fs = C.jc == 0 ? 0u : l0 + (C.jc - 1) * (kWalBlock - C.hs());
       const bool started = (fs >> 10) == C.g;
       const bool carry = crow && !ends;
-      uint32_t ns[4];
+      uint32_t ns[kNC];
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) ns[k] = carry ? cs[k] : 0u;
-      if (carry && started && t == 15) ns[3] ^= cu.ez[0];
-      auto row_value = [&](const uint32_t (&c)[4]) {  // columns -> the row's value at the window end
-        uint32_t v = c[3] ^ fcrc::shift_at(Lb, kFcOffC256, c[2]) ^
-                     fcrc::shift_at(Lb, kFcOffC256 + 4096, c[1]) ^
-                     fcrc::shift_at(Lb, kFcOffC256 + 8192, c[0]);
+      for (uint32_t k = 0; k < kNC; ++k) ns[k] = carry ? cs[k] : 0u;
+      if (carry && started && t == 15) ns[kNC - 1] ^= cu.ez[0];
+      auto row_value = [&](const uint32_t (&c)[kNC]) {  // chains -> the row's value at the window end
+        uint32_t v = c[kNC - 1];
+        if (kNC == 4)  // columns 0..2 onto column 3 (256 (3 - k) bytes on)
+          v ^= fcrc::shift_at(Lb, kFcOffC256, c[kNC == 4 ? 2 : 0]) ^
+               fcrc::shift_at(Lb, kFcOffC256 + 4096, c[kNC == 4 ? 1 : 0]) ^
+               fcrc::shift_at(Lb, kFcOffC256 + 8192, c[0]);
         v = t == 15 ? v : fcrc::shift_at(Lb, kFcOffA16 + 4096 * (14 - t), v);
         v = fcrc::row_ror_xor<1>(v);
         v = fcrc::row_ror_xor<2>(v);
@@ -1547,7 +1530,9 @@ xxh3_frag_kernel(BlockArgs a) {
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
           const uint32_t B = C.bn - W0;
           const uint32_t hiB = L - W0 < 1024u ? L - W0 : 1024u;
-          uint32_t sb[4] = {0u, 0u, 0u, 0u};
+          uint32_t sb[kNC];
+#pragma unroll
+          for (uint32_t k = 0; k < kNC; ++k) sb[k] = 0u;
 #pragma unroll
           for (uint32_t k = 0; k < 4; ++k) {
             uint64_t d0, d1;
@@ -1559,16 +1544,18 @@ xxh3_frag_kernel(BlockArgs a) {
             // bytes [ka, kb): mask(kb) & ~mask(ka)
             const u32x4 mb = *reinterpret_cast<const u32x4*>(kmask + 4 * (kb > ka ? kb : ka));
             const u32x4 ma = *reinterpret_cast<const u32x4*>(kmask + 4 * ka);
-            sb[k] = fcrc::chunk_step(
-                Lb, FK, sb[k], __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d0), mb.x, ma.x, 0x40),
+            const uint32_t kc = kNC == 1 ? 0u : k;
+            sb[kc] = fcrc::chunk_step(
+                Lb, FK, sb[kc], __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d0), mb.x, ma.x, 0x40),
                 __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d0 >> 32), mb.y, ma.y, 0x40),
                 __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d1), mb.z, ma.z, 0x40),
                 __builtin_amdgcn_bitop3_b32(static_cast<uint32_t>(d1 >> 32), mb.w, ma.w, 0x40));
 #else
+            const uint32_t kc = kNC == 1 ? 0u : k;
             uint64_t m0, m1;
             fcrc::keep_mask(ka, kb > ka ? kb : ka, m0, m1);
             const uint64_t e0 = d0 & m0, e1 = d1 & m1;
-            sb[k] = fcrc::chunk_step(Lb, FK, sb[k], static_cast<uint32_t>(e0),
+            sb[kc] = fcrc::chunk_step(Lb, FK, sb[kc], static_cast<uint32_t>(e0),
                                      static_cast<uint32_t>(e0 >> 32), static_cast<uint32_t>(e1),
                                      static_cast<uint32_t>(e1 >> 32));
 #endif
@@ -1579,13 +1566,13 @@ xxh3_frag_kernel(BlockArgs a) {
             if (VB != cu.ez[3]) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = 0;
           if (pb && !endsB) {
 #pragma unroll
-            for (uint32_t k = 0; k < 4; ++k) ns[k] = sb[k];
-            if (t == 15) ns[3] ^= cu.ez[2];
+            for (uint32_t k = 0; k < kNC; ++k) ns[k] = sb[k];
+            if (t == 15) ns[kNC - 1] ^= cu.ez[2];
           }
         }
       }
 #pragma unroll
-      for (uint32_t k = 0; k < 4; ++k) crc_s[k] = ns[k];
+      for (uint32_t k = 0; k < kNC; ++k) crc_s[k] = ns[k];
     }
     sum0 += row_ror64<4>(sum0);
     sum1 += row_ror64<4>(sum1);

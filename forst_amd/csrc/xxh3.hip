@@ -1090,7 +1090,7 @@ __device__ __forceinline__ void frow_next(FRow& P) {  // window g -> g + 1
 template <bool CRC>
 __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, const FRow& P,
                                            FStep& d) {
-  const uint32_t t = lane & 15, s4 = t >> 2, p = t & 3;
+  const uint32_t t = lane & 15, s4 = t >> 2;
   const uint64_t P0 = P.off();
   const bool valid = P.rel != kNoMsg && P0 <= a.base_len;
   const bool lng = valid && P.size > 240;

@@ -90,6 +90,33 @@ def test_emu_wal():
     assert bad == 0 and (st == 0).all() and int(nrec.sum()) == len(poffs)
 
 
+@pytest.mark.parametrize("max_len", [200, 1100, 2000])
+def test_emu_wal_dense_blocks(max_len, monkeypatch):
+    """blocks of 30 to ~290 records (wal.hip wal_walk_kernel / wal_fill_kernel):
+    CRC failures early and late in a block == the serial per-block reader
+    (FORST_WAL_VARIANT=wave)."""
+    rng = np.random.default_rng(max_len)
+    lens = rng.integers(0, max_len, 32768 * 3 // (max_len // 2 + 7)).astype(np.uint32)
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens)
+    blk = (poffs // 32768).astype(np.int64)
+    per = np.bincount(blk)
+    assert per.max() > 32 or max_len > 1000
+    b = buf.copy()
+    for k in (int(np.nonzero(blk == 0)[0][5]), int(np.nonzero(blk == 1)[0][-1])):
+        if plens[k] > 0:
+            b[int(poffs[k]) + 7] ^= 0x10
+    got = emu.wal_verify(b)
+    monkeypatch.setenv("FORST_WAL_VARIANT", "wave")
+    want = emu.wal_verify(b)
+    monkeypatch.delenv("FORST_WAL_VARIANT")
+    for g, w in zip(got[:3], want[:3]):
+        assert (g == w).all()
+    assert got[3] == want[3]
+    st, nrec, fail, bad = emu.wal_verify(buf)
+    assert bad == 0 and int(nrec.sum()) == len(poffs)
+
+
 @pytest.mark.parametrize("recyclable,split", [(False, "0"), (True, "0"), (False, "1"),
                                                (True, "1")])
 def test_emu_wal_pipeline_statuses(recyclable, split, monkeypatch):

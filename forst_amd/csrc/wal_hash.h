@@ -141,17 +141,53 @@ __global__ void __launch_bounds__(kWhLanes) wh_select_kernel(const uint64_t* gle
   out[j] = glen[j] ? hb[gpos[j]] : ha[j];
 }
 
+// The gathered records' branch (list, gather, their XXH3) does not depend on
+// the in-place frag kernel, so it runs on a second stream beside it and fills
+// the frag kernel's launch tail (a14 9.66 -> 9.52 ms, A/B in
+// profiles/ab_r04/a14_gather_overlap.log).  The recovery's remainder batch
+// keeps one stream: there the fork and join cost more than the overlap gains
+// (C5 recovery +0.06..0.1 ms in the same A/B).
+// One non-blocking stream and two events per host thread and device, created
+// on first use; any failure there falls back to the caller's stream alone.
+#ifndef FORST_WH_OVERLAP
+#define FORST_WH_OVERLAP 1
+#endif
+struct WhAux {
+  hipStream_t s = nullptr;
+  hipEvent_t fork = nullptr, join = nullptr;
+  bool tried = false;
+};
+inline WhAux* wh_aux() {
+  constexpr int kMaxDev = 16;
+  thread_local WhAux aux[kMaxDev];
+  int d = 0;
+  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) return nullptr;
+  WhAux& a = aux[d];
+  if (!a.tried) {
+    a.tried = true;
+    if (hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess ||
+        hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess ||
+        hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) {
+      a.s = nullptr;
+      (void)hipGetLastError();
+    }
+  }
+  return a.s ? &a : nullptr;
+}
+
 inline size_t wh_up256(size_t b) { return (b + 255) & ~size_t(255); }
 inline dim3 wh_grid(uint64_t n) {
   const uint64_t g = (n + kWhLanes - 1) / kWhLanes;
   return dim3(static_cast<uint32_t>(g ? g : 1));
 }
 
-// out[j] = XXH3_64bits of logical record j (device array).  Synchronises the
-// stream once (the gathered byte total sizes the scratch).
+// out[j] = XXH3_64bits of logical record j (device array).  Waits once on the
+// host for the gathered byte total (it sizes the scratch): behind the queued
+// frag kernel when the second stream is used, else a stream synchronisation.
 template <class F>
 hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f, uint64_t n,
-                                uint64_t* out, hipStream_t st, const char** name) {
+                                uint64_t* out, hipStream_t st, const char** name,
+                                bool overlap = true) {
   if (n == 0) return hipSuccess;
   const uint64_t nt = n / kScanTile + 2;
   const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * nt);
@@ -180,13 +216,6 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
   scan_u64(boff, n, tiles2, gpos, st);
   uint64_t tot[2] = {0, 0};  // gathered bytes, gathered records
   const uint64_t ntl = (n + kScanTile - 1) / kScanTile;
-  if ((e = hipMemcpyAsync(&tot[0], tiles + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-      (e = hipMemcpyAsync(&tot[1], tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-      (e = hipStreamSynchronize(st)) != hipSuccess) {
-    (void)scratch_free(scratch, st);
-    return e;
-  }
-  const uint64_t gtotal = tot[0], ng = tot[1];
   // in place across the fragments (every record; gathered ones have length 0)
   BlockArgs fa{};
   fa.base = log;
@@ -196,16 +225,49 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
   fa.init_crcs = info;
   fa.out64 = ha;
   fa.n = n;
-  e = log_len >= 4096 ? launch_xxh3_frag(fa, st, name) : launch_xxh3_blocks(kModeRaw, fa, st, name);
+  auto frag = [&]() {
+    return log_len >= 4096 ? launch_xxh3_frag(fa, st, name)
+                           : launch_xxh3_blocks(kModeRaw, fa, st, name);
+  };
+  if ((e = hipMemcpyAsync(&tot[0], tiles + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
+      (e = hipMemcpyAsync(&tot[1], tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) {
+    (void)scratch_free(scratch, st);
+    return e;
+  }
+  // With the second stream the frag kernel is queued before the host waits
+  // for the two totals (on an event behind their copies), so the GPU does not
+  // idle through the host's turnaround, and the gathered branch starts on the
+  // second stream while the frag kernel runs.
+  WhAux* aux = FORST_WH_OVERLAP && overlap ? wh_aux() : nullptr;
+  if (aux && hipEventRecord(aux->fork, st) != hipSuccess) {
+    (void)hipGetLastError();
+    aux = nullptr;
+  }
+  if (aux) {
+    e = frag();
+    const hipError_t w = hipEventSynchronize(aux->fork);
+    if (e == hipSuccess) e = w;
+  } else {
+    e = hipStreamSynchronize(st);
+    if (e == hipSuccess) e = frag();
+  }
+  if (e != hipSuccess) {
+    (void)scratch_free(scratch, st);
+    return e;
+  }
+  const uint64_t gtotal = tot[0], ng = tot[1];
   void* gbuf = nullptr;
-  if (e == hipSuccess && ng) {
-    e = scratch_alloc(&gbuf, wh_up256(gtotal + 4096), st);
+  if (ng) {
+    hipStream_t gs = st;
+    const bool forked = aux && hipStreamWaitEvent(aux->s, aux->fork, 0) == hipSuccess;
+    if (forked) gs = aux->s;
+    e = scratch_alloc(&gbuf, wh_up256(gtotal + 4096), gs);
     if (e == hipSuccess) {
-      hipLaunchKernelGGL(wh_list_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, goff, gpos, n,
+      hipLaunchKernelGGL(wh_list_kernel, wh_grid(n), dim3(kWhLanes), 0, gs, glen, goff, gpos, n,
                          list, boff, blen);
       const uint32_t gg = static_cast<uint32_t>(ng < 65536 ? ng : 65536);
-      hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, st, log, f, list, boff,
-                         ng, static_cast<uint8_t*>(gbuf));
+      hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, gs, log, f, list,
+                         boff, ng, static_cast<uint8_t*>(gbuf));
       BlockArgs ga{};
       ga.base = static_cast<uint8_t*>(gbuf);
       ga.base_len = wh_up256(gtotal + 4096);
@@ -215,7 +277,14 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
       ga.n = ng;
       ga.kernel_hint = 3;  // few records (C5: 22 K of 10 M), long ones: one per wave
       const char* gname = nullptr;
-      e = launch_xxh3_blocks(kModeRaw, ga, st, &gname);
+      e = launch_xxh3_blocks(kModeRaw, ga, gs, &gname);
+    }
+    // join (also on failure: st must not run ahead of work queued on gs,
+    // which reads the scratch freed on st below)
+    if (forked && (hipEventRecord(aux->join, gs) != hipSuccess ||
+                   hipStreamWaitEvent(st, aux->join, 0) != hipSuccess)) {
+      if (e == hipSuccess) e = hipErrorUnknown;
+      (void)hipStreamSynchronize(gs);
     }
   }
   if (e == hipSuccess) {

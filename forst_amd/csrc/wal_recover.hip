@@ -1682,7 +1682,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       const RecFrags rf{hash_begin, last_tok, t.kind, t.item, q.it_off, q.ipack, q.seg, q.live,
                         q.seg_fl};
       const RecFragsSub rs{rf, sub};
-      e = hash_logical_records(log, log_len, rs, n_need, hsub, st, name);
+      e = hash_logical_records(log, log_len, rs, n_need, hsub, st, name, false);
       if (e == hipSuccess)
         hipLaunchKernelGGL(rw_scatter_kernel, grid_for(n_need), dim3(kLanes), 0, st, sub, hsub,
                            n_need, full.hash);

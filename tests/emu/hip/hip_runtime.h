@@ -38,6 +38,7 @@ struct dim3 {
 typedef int hipError_t;
 typedef void* hipStream_t;
 constexpr hipError_t hipSuccess = 0;
+constexpr hipError_t hipErrorUnknown = 999;
 struct hipDeviceProp_t {
   char gcnArchName[256];
   int multiProcessorCount;
@@ -258,6 +259,22 @@ inline hipError_t hipMemcpyAsync(void* d, const void* s, size_t n, hipMemcpyKind
   return hipSuccess;
 }
 inline hipError_t hipStreamSynchronize(hipStream_t) { return hipSuccess; }
+// streams and events: launches run to completion in order, so these are no-ops
+typedef void* hipEvent_t;
+constexpr unsigned hipStreamNonBlocking = 1, hipEventDisableTiming = 2;
+inline hipError_t hipStreamCreateWithFlags(hipStream_t* s, unsigned) {
+  static int dummy;
+  *s = &dummy;
+  return hipSuccess;
+}
+inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
+  static int dummy;
+  *e = &dummy;
+  return hipSuccess;
+}
+inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }
 inline hipError_t hipMemsetAsync(void* d, int v, size_t n, hipStream_t) {
   std::memset(d, v, n);
   return hipSuccess;

@@ -430,8 +430,13 @@ __global__ void __launch_bounds__(kLanes) rw_cand_flags_kernel(const Cand c, uin
                                                                uint64_t* fc, uint64_t* fr) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
-  fc[i] = c.head[i];
-  fr[i] = c.fused[i] || it_old[i] ? 0u : 1u;  // (skipped old records need no CRC)
+  const uint64_t r = c.fused[i] || it_old[i] ? 0u : 1u;  // (skipped old records need no CRC)
+  if (fr) {
+    fc[i] = c.head[i];
+    fr[i] = r;
+  } else {
+    fc[i] = c.head[i] | (r << 32);  // both flags in one word: one scan (ni < 2^32)
+  }
 }
 
 __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint64_t ni,
@@ -447,14 +452,14 @@ __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
   if (c.head[i]) {
-    const uint64_t k = cpos[i];
+    const uint64_t k = rpos ? cpos[i] : cpos[i] & 0xffffffffu;
     l_p0[k] = c.p0[i];
     l_len[k] = c.len[i];
     l_info[k] = c.info[i];
     l_first[k] = c.first[i];
   }
   if (!c.fused[i] && !it_old[i]) {
-    const uint64_t k = rpos[i];
+    const uint64_t k = rpos ? rpos[i] : cpos[i] >> 32;
     r_off[k] = crc_off[i];
     r_len[k] = crc_len[i];
     r_item[k] = i;
@@ -1099,6 +1104,7 @@ struct RecFrags {
 __global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const uint64_t* hb,
                                                           const uint64_t* lt, uint64_t nr,
                                                           const Cand c, const uint64_t* cpos,
+                                                          uint64_t cmask,
                                                           const uint64_t* cand_hash,
                                                           uint64_t* hash_out, uint64_t* need) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
@@ -1109,7 +1115,7 @@ __global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const
   if (m) {
     const uint64_t ih = t.item[h];
     m = c.head[ih] && c.last[ih] == t.item[i];
-    if (m) hash_out[j] = cand_hash[cpos[ih]];
+    if (m) hash_out[j] = cand_hash[cpos[ih] & cmask];  // (cmask: cpos packed with rpos)
   }
   need[j] = m ? 0u : 1u;
 }
@@ -1372,6 +1378,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   q.take(A, ni, nb, nt_max);
   const Tokens& t = q.t;
   uint64_t n_cand = 0;
+  uint64_t cpos_mask = ~0ull;  // 0xffffffff when cpos holds the packed positions
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q1.cnt,
                        q.it_off,
@@ -1387,20 +1394,31 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       hipLaunchKernelGGL(rw_cand_kernel, dim3(static_cast<uint32_t>(cg < ncu ? cg : ncu)),
                          dim3(kCandThreads), 0, st, a, ni, q.it_off, q.it_old, q.ipack,
                          q.crc_stored, q.c);
+      // both flags packed in one word and scanned once when the counts fit
+      // 32 bits (one scan instead of two)
+      const bool packed = ni < (uint64_t(1) << 32);
       hipLaunchKernelGGL(rw_cand_flags_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni,
-                         q.it_old, q.fc, q.fr);
+                         q.it_old, q.fc, packed ? nullptr : q.fr);
       const uint64_t nti = (ni + kScanTile - 1) / kScanTile;
       uint64_t cnt2[2] = {0, 0};
       scan_u64(q.fc, ni, q.tiles2, q.cpos, st);
       e = hipMemcpyAsync(&cnt2[0], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
-      scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
-      if (e == hipSuccess) e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      if (!packed) {
+        scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
+        if (e == hipSuccess)
+          e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      }
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (e != hipSuccess) return fail(e);
+      if (packed) {
+        cnt2[1] = cnt2[0] >> 32;
+        cnt2[0] &= 0xffffffffu;
+        cpos_mask = 0xffffffffu;
+      }
       n_cand = cnt2[0];
       const uint64_t n_raw = cnt2[1];
       hipLaunchKernelGGL(rw_cand_list_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni, q.it_old,
-                         q.cpos, q.rpos, q.crc_off, q.crc_len, q.l_p0, q.l_len, q.l_info,
+                         q.cpos, packed ? nullptr : q.rpos, q.crc_off, q.crc_len, q.l_p0, q.l_len, q.l_info,
                          q.l_first, q.r_off, q.r_len, q.r_item);
       if (n_cand) {
         BlockArgs fa{};
@@ -1649,7 +1667,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     uint64_t n_need = 0, over = 0;
     auto match = [&]() {
       hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,
-                         last_tok, nr, cm, q.cpos, q.cand_hash, full.hash, need);
+                         last_tok, nr, cm, q.cpos, cpos_mask, q.cand_hash, full.hash, need);
       scan_u64(need, nr, tiles5, npos, st);
       hipError_t r = hipMemcpyAsync(&n_need, tiles5 + (nr + kScanTile - 1) / kScanTile, 8,
                                     hipMemcpyDeviceToHost, st);

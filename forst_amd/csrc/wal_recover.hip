@@ -66,6 +66,10 @@
 #include "scan_common.h"
 #include "wal_hash.h"
 
+#ifndef FORST_REC_OVERLAP
+#define FORST_REC_OVERLAP 1
+#endif
+
 namespace forst {
 namespace {
 
@@ -1378,6 +1382,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   q.take(A, ni, nb, nt_max);
   const Tokens& t = q.t;
   uint64_t n_cand = 0;
+  WhAux* raw_aux = nullptr;  // second stream of the raw CRC (beside the fused kernel)
   uint64_t cpos_mask = ~0ull;  // 0xffffffff when cpos holds the packed positions
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q1.cnt,
@@ -1433,10 +1438,20 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         fa.out64 = q.cand_hash;
         fa.n = n_cand;
         if ((e = hipMemsetAsync(q.crc_ok, 1, ni, st)) != hipSuccess) return fail(e);
+        // the raw CRC of the other records does not depend on the fused
+        // kernel (disjoint items of crc_ok): on a second stream, forked after
+        // the memset, it runs in the fused kernel's launch tail
+        if (FORST_REC_OVERLAP && n_raw && (raw_aux = wh_aux()) != nullptr &&
+            (hipEventRecord(raw_aux->fork, st) != hipSuccess ||
+             hipStreamWaitEvent(raw_aux->s, raw_aux->fork, 0) != hipSuccess)) {
+          (void)hipGetLastError();
+          raw_aux = nullptr;
+        }
         const char* fname = nullptr;
         if ((e = launch_xxh3_frag_crc(fa, st, &fname)) != hipSuccess) return fail(e);
       }
       if (n_raw) {
+        const hipStream_t rs = raw_aux ? raw_aux->s : st;
         BlockArgs cb{};
         cb.base = log;
         cb.base_len = log_len;
@@ -1445,9 +1460,17 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         cb.out32 = q.computed;
         cb.n = n_raw;
         const char* crc_name = nullptr;
-        if ((e = launch_crc32c_blocks(kModeRaw, cb, st, &crc_name)) != hipSuccess) return fail(e);
-        hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_raw), dim3(kLanes), 0, st, q.r_item,
-                           q.computed, n_raw, q.crc_stored, q.crc_ok);
+        e = launch_crc32c_blocks(kModeRaw, cb, rs, &crc_name);
+        if (e == hipSuccess)
+          hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_raw), dim3(kLanes), 0, rs, q.r_item,
+                             q.computed, n_raw, q.crc_stored, q.crc_ok);
+        // join (also on failure: the scratch is freed on st)
+        if (raw_aux && (hipEventRecord(raw_aux->join, rs) != hipSuccess ||
+                        hipStreamWaitEvent(st, raw_aux->join, 0) != hipSuccess)) {
+          if (e == hipSuccess) e = hipErrorUnknown;
+          (void)hipStreamSynchronize(rs);
+        }
+        if (e != hipSuccess) return fail(e);
       }
     }
     void* fbv = nullptr;

@@ -58,9 +58,14 @@ CONFIGS = {
     "NS16X": (1 << 20, 16384, 4, "north-star 1 M x 16 KiB kXXH3 compute+verify"),
     "C3S": (1 << 20, ("sorted", (4096, 16384, 65536)), 4,
             "C3's blocks sorted by size (64 KiB, then 16 KiB, then 4 KiB) kXXH3 compute+verify"),
+    # the two legacy selector types (format.cc:573-576, 603-622) at the
+    # north-star shape
+    "NS16H32": (1 << 20, 16384, 2, "1 M x 16 KiB kxxHash (XXH32) compute+verify"),
+    "NS16H64": (1 << 20, 16384, 3, "1 M x 16 KiB kxxHash64 (XXH64) compute+verify"),
 }
 SEEDS = {"C2": 0xF0E5700002, "C3": 0xF0E5700003, "C4": 0xF0E5700004,
-         "NS16": 0xF0E5700002, "NS16X": 0xF0E5700002, "C3S": 0xF0E5700003}
+         "NS16": 0xF0E5700002, "NS16X": 0xF0E5700002, "C3S": 0xF0E5700003,
+         "NS16H32": 0xF0E5700002, "NS16H64": 0xF0E5700002}
 
 
 def algorithmic_bytes(kind, payload_bytes, n):
@@ -260,6 +265,116 @@ def run_wal(steps, warmup, n_records=10_000_000):
     return out
 
 
+def run_kv(steps, warmup, n=1 << 20):
+    """a15 per-KV protection (db/kv_checksum.h:296 ProtectKVO + ProtectS, the
+    WriteBatch / memtable shape; MemTable::VerifyEntryChecksum memtable.cc:273
+    for the read side) on 1 M memtable-shaped entries: 16-64 B keys, 0-1000 B
+    values, 8-byte protection stored after each value (the batch of
+    tests/test_gpu_parity.py test_kv_full_size_roundtrip).  Algorithmic bytes:
+    protect = key + value bytes + 33 B of descriptors (key/value offset 8+8,
+    sizes 4+4, op 1, seq 8) read + 8 B written; verify = the same + 8 B
+    checksum offset + 8 B stored protection read + 8 B computed + 1 B ok
+    written."""
+    from forst_amd import engine
+
+    rng = np.random.default_rng(99)
+    ks = rng.integers(16, 65, n).astype(np.int64)
+    vs = rng.integers(0, 1001, n).astype(np.int64)
+    ko = np.zeros(n, np.int64)
+    ko[1:] = np.cumsum(ks[:-1] + vs[:-1] + 8)
+    vo = ko + ks
+    co = vo + vs
+    total = int(co[-1]) + 8
+    base = torch.empty((total + 255) // 256 * 256, dtype=torch.uint8, device="cuda")
+    engine.fill_stream(base, 0, 0xF0E57000A15)
+    dev = lambda a: torch.from_numpy(a).cuda()  # noqa: E731
+    dko, dks, dvo, dvs, dco = dev(ko), dev(ks.astype(np.int32)), dev(vo), dev(vs.astype(np.int32)), dev(co)
+    ops = dev(rng.integers(0, 26, n).astype(np.uint8))
+    seqs = dev(rng.integers(0, 2**62, n).astype(np.int64))
+    prot = torch.empty(n, dtype=torch.uint64, device="cuda")
+    comp = torch.empty(n, dtype=torch.uint64, device="cuda")
+    okv = torch.empty(n, dtype=torch.uint8, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    engine.kv_protect_batch(base, dko, dks, dvo, dvs, ops, seqs, out=prot)
+    idx = dco[:, None] + torch.arange(8, device="cuda")[None, :]
+    base[idx.reshape(-1)] = prot.view(torch.uint8).view(n, 8).reshape(-1)  # Encode(8)
+    del idx
+
+    def protect():
+        engine.kv_protect_batch(base, dko, dks, dvo, dvs, ops, seqs, out=prot)
+
+    def verify():
+        engine.kv_verify_batch(base, dko, dks, dvo, dvs, 8, dco, ops, seqs, computed=comp, ok=okv,
+                               mismatches=bad)
+
+    for _ in range(max(1, warmup)):
+        protect()
+        verify()
+    torch.cuda.synchronize()
+    bad.zero_()
+    evs = [[torch.cuda.Event(enable_timing=True) for _ in range(3)] for _ in range(steps)]
+    for e in evs:
+        e[0].record()
+        protect()
+        e[1].record()
+        verify()
+        e[2].record()
+    torch.cuda.synchronize()
+    assert int(bad.item()) == 0, "KV entries failed verification in the timed region"
+    t_p = np.mean([e[0].elapsed_time(e[1]) for e in evs]) / 1e3
+    t_v = np.mean([e[1].elapsed_time(e[2]) for e in evs]) / 1e3
+    kvb = int((ks + vs).sum())
+    alg_p = kvb + 41 * n
+    alg_v = kvb + 74 * n
+    name_v = engine.last_kernel()
+    return {"desc": f"{n} entries, keys 16-64 B, values 0-1000 B, ProtectKVO + ProtectS, "
+                    f"8-byte protection ({kvb / GIB:.2f} GiB of key+value bytes)",
+            "protect_ms": round(t_p * 1e3, 4), "verify_ms": round(t_v * 1e3, 4),
+            "protect_Mentries_per_s": round(n / t_p / 1e6, 1),
+            "verify_Mentries_per_s": round(n / t_v / 1e6, 1),
+            "protect_roofline_frac": round(alg_p / t_p / 1e9 / HBM_PEAK_GBS, 4),
+            "verify_roofline_frac": round(alg_v / t_v / 1e9 / HBM_PEAK_GBS, 4),
+            "verify_kernel": name_v}
+
+
+def cpu_info():
+    """the host CPU the baseline ran on: model, current clock of the CPUs the
+    process may use (/proc/cpuinfo, MHz as the kernel reports it at the time),
+    and the affinity list"""
+    aff = sorted(os.sched_getaffinity(0)) if hasattr(os, "sched_getaffinity") else []
+    model, mhz = None, {}
+    try:
+        cpu = None
+        with open("/proc/cpuinfo") as f:
+            for line in f:
+                k, _, v = line.partition(":")
+                k, v = k.strip(), v.strip()
+                if k == "processor":
+                    cpu = int(v)
+                elif k == "model name" and model is None:
+                    model = v
+                elif k == "cpu MHz" and cpu is not None:
+                    mhz[cpu] = float(v)
+    except OSError:
+        pass
+    mine = [mhz[c] for c in aff if c in mhz]
+
+    def ranges(xs):
+        out, i = [], 0
+        while i < len(xs):
+            j = i
+            while j + 1 < len(xs) and xs[j + 1] == xs[j] + 1:
+                j += 1
+            out.append(f"{xs[i]}-{xs[j]}" if j > i else str(xs[i]))
+            i = j + 1
+        return ",".join(out)
+
+    return {"cpu_model": model, "affinity": ranges(aff), "affinity_count": len(aff),
+            "mhz_median": round(float(np.median(mine)), 0) if mine else None,
+            "mhz_min": round(min(mine), 0) if mine else None,
+            "mhz_max": round(max(mine), 0) if mine else None}
+
+
 def cpu_threads():
     """(threads to use, how the count was found): every CPU this process may
     run on (sched_getaffinity), capped by a cgroup CPU quota when one is set;
@@ -310,13 +425,24 @@ def cpu_baseline(b, ctype, budget_s=12.0):
             dt = one_pass(nt)
             best, spent, reps = min(best, dt), spent + dt, reps + 1
         res[nt] = 2 * sample_bytes / best / GIB
+    # one thread on the first 256 blocks (~1 MiB, cache-resident), repeated:
+    # the core's own rate, to tell a slow core from a memory-bound sample
+    nc = min(ns, 256)
+    cb = int(sizes[:nc].astype(np.int64).sum()) + nc
+    best_c = 1e30
+    for _ in range(200):
+        t = time.perf_counter()
+        O.block_verify_batch(ctype, hb, offs[:nc], sizes[:nc], nthreads=1)
+        best_c = min(best_c, time.perf_counter() - t)
     return {"value": round(res[nthreads], 3), "unit": "GiB/s", "cores": nthreads, "kind": "port",
             "cores_from": how, "host_os_cpu_count": os.cpu_count(),
             "sample": f"first {ns} blocks of the same batch ({sample_bytes / GIB:.2f} GiB "
                       f"checksummed per pass), compute+verify, best of <=5, "
                       f"oracle/oracle.c -O3 x86-64-v3 (SSE4.2 crc32 3-way, AVX2 XXH3), "
                       f"one std::thread per core over contiguous block ranges",
-            "single_thread_GiBps": round(res[1], 3)}
+            "single_thread_GiBps": round(res[1], 3),
+            "single_thread_cached_GiBps": round(cb / best_c / GIB, 3),
+            "host": cpu_info()}
 
 
 def end_to_end_pcie(b, ctype, chunk_blocks=1 << 16):
@@ -379,30 +505,57 @@ def host_paths(b, ctype, sample_blocks=1 << 18):
     out = {"sample": f"first {ns} blocks ({nbytes / GIB:.2f} GiB checksummed)",
            "devices": list(range(ndev))}
 
-    def rate(base, devices):
+    first = {}
+
+    def rate(base, devices, key=None):
         best = 1e30
-        for _ in range(3):
+        for k in range(3):
             t0 = time.perf_counter()
             _, _, ok, bad = hostpath.block_verify_host(ctype, base, offs, sizes, devices=devices)
-            best = min(best, time.perf_counter() - t0)
+            dt = time.perf_counter() - t0
+            if k == 0 and key:
+                first[key] = round(nbytes / dt / GIB, 2)
+            best = min(best, dt)
             assert bad == 0
         return round(nbytes / best / GIB, 2)
 
-    out["pageable_GiBps"] = rate(pageable, list(range(ndev)))
+    # (the first call of the process also creates the device's host context:
+    # worker thread, stream, windows and pinned staging)
+    out["pageable_GiBps"] = rate(pageable, list(range(ndev)), "pageable_incl_context_creation")
     out["pageable_2streams_per_gpu_GiBps"] = rate(pageable, [d for d in range(ndev) for _ in (0, 1)])
+    t0 = time.perf_counter()
     pinned = torch.from_numpy(pageable).pin_memory()
-    out["pinned_GiBps"] = rate(pinned.numpy(), list(range(ndev)))
+    out["pin_memory_s"] = round(time.perf_counter() - t0, 4)
+    out["pinned_GiBps"] = rate(pinned.numpy(), list(range(ndev)), "pinned")
     del pinned
     d = os.environ.get("TMPDIR", tempfile.gettempdir())
     path = os.path.join(d, f"forst_bench_{os.getpid()}.sst")
     try:
         pageable.tofile(path)
-        m = hostpath.MappedFile(path, register=True)
+        # a fresh mapping of the file (in the page cache: just written), the
+        # way a one-shot VerifyChecksum sees an SST: map, register, verify once
+        t0 = time.perf_counter()
+        m = hostpath.MappedFile(path, register=False)
+        t1 = time.perf_counter()
+        from forst_amd._lib import lib
+        rc = lib().forst_host_register(m.address, m.size)
+        t2 = time.perf_counter()
+        m.registered = rc == 0
         out["mmap_registered"] = m.registered
         if not m.registered:
-            out["mmap_register_error"] = m.register_error
-        out["mmap_GiBps"] = rate(m, list(range(ndev)))
+            out["mmap_register_error"] = lib().forst_host_last_error().decode(errors="replace")
+        out["mmap_GiBps"] = rate(m, list(range(ndev)), "mmap_registered_verify")
         m.close()
+        # the same without registration: staged through pinned memory
+        m = hostpath.MappedFile(path, register=False)
+        out["mmap_unregistered_GiBps"] = rate(m, list(range(ndev)), "mmap_unregistered")
+        m.close()
+        out["cold"] = {
+            "mmap_populate_s": round(t1 - t0, 4), "register_s": round(t2 - t1, 4),
+            "register_GiBps": round(m.size / (t2 - t1) / GIB, 2),
+            "first_call_GiBps": first,
+            "mmap_register_plus_first_verify_GiBps": round(
+                nbytes / ((t2 - t1) + nbytes / first["mmap_registered_verify"] / GIB) / GIB, 2)}
     except OSError as e:  # pragma: no cover
         out["mmap_error"] = str(e)
     finally:
@@ -531,7 +684,7 @@ def main():
     del b
     torch.cuda.empty_cache()
     if world == 1 and not args.no_extras and args.config == "C2":
-        for nm in ("NS16", "NS16X", "C3", "C3S", "C4"):
+        for nm in ("NS16", "NS16X", "C3", "C3S", "C4", "NS16H32", "NS16H64"):
             # every extra config with the headline's step and warmup counts
             r = run_config(nm, args.steps, args.warmup, rank, world)
             r.pop("batch")
@@ -550,6 +703,8 @@ def main():
                 "trailer_roofline_frac": round(kt["frac"], 4),
                 "verify_kernel": kv["name"], "trailer_kernel": kt["name"]}
         extras["C5_wal"] = run_wal(max(3, args.steps // 2), 1)
+        torch.cuda.empty_cache()
+        extras["a15_kv"] = run_kv(args.steps, args.warmup)
         torch.cuda.empty_cache()
     if rank != 0:
         if world > 1:

@@ -94,6 +94,7 @@ def lib():
         "forst_host_last_error": (ctypes.c_char_p, []),
         "forst_host_context_stats": (i, [vp, vp, vp]),
         "forst_host_context_trim": (i, [vp]),
+        "forst_aux_stream_stats": (i, [vp, vp]),
         "forst_block_uncompress": (i, [ctypes.c_uint8, u32, vp, u64, vp, u64, vp, vp]),
         "forst_trailer_writer_open": (i, [i, u32, u64, u32, u64, vp, vp, vp, vp]),
         "forst_trailer_writer_add": (i, [vp, vp, u64, ctypes.c_uint8, i, vp, vp]),

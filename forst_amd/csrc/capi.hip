@@ -14,6 +14,7 @@
 #include <cstring>
 #include <mutex>
 #include <string>
+#include <vector>
 
 #include "../../include/forst_checksum.h"
 #include "engine.h"
@@ -88,6 +89,99 @@ hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream) {
 }
 
 hipError_t scratch_free(void* p, hipStream_t stream) { return p ? hipFreeAsync(p, stream) : hipSuccess; }
+
+// ---- auxiliary streams (engine.h AuxStream) --------------------------------
+// One pool per device, shared by every host thread: a call takes an idle
+// entry (or creates one), forks its second branch onto it and gives it back
+// before returning, so the number of streams is bounded by the calls in
+// flight at once, not by the threads that ever called (ForSt calls from JNI
+// and pool threads that come and go).  forst_host_context_trim destroys the
+// idle ones.
+namespace {
+std::mutex g_aux_mu;
+std::vector<AuxStream*> g_aux_idle[kMaxDevices];
+uint32_t g_aux_live = 0;  // created and not destroyed
+
+int stream_device(hipStream_t st) {
+  int dev = -1;
+  if (st != nullptr && hipStreamGetDevice(st, &dev) == hipSuccess && dev >= 0) return dev;
+  (void)hipGetLastError();
+  return hipGetDevice(&dev) == hipSuccess ? dev : -1;
+}
+}  // namespace
+
+AuxStream* aux_acquire(hipStream_t st) {
+  const int dev = stream_device(st);
+  if (dev < 0 || dev >= kMaxDevices) return nullptr;
+  {
+    std::lock_guard<std::mutex> g(g_aux_mu);
+    auto& idle = g_aux_idle[dev];
+    if (!idle.empty()) {
+      AuxStream* a = idle.back();
+      idle.pop_back();
+      return a;
+    }
+  }
+  // created on the stream's device (the caller's current device restored)
+  int cur = -1;
+  const bool have_cur = hipGetDevice(&cur) == hipSuccess;
+  if (have_cur && cur != dev && hipSetDevice(dev) != hipSuccess) {
+    (void)hipGetLastError();
+    return nullptr;
+  }
+  AuxStream* a = new AuxStream{nullptr, nullptr, nullptr, dev};
+  if (hipStreamCreateWithFlags(&a->s, hipStreamNonBlocking) != hipSuccess ||
+      hipEventCreateWithFlags(&a->fork, hipEventDisableTiming) != hipSuccess ||
+      hipEventCreateWithFlags(&a->join, hipEventDisableTiming) != hipSuccess) {
+    (void)hipGetLastError();
+    if (a->join) (void)hipEventDestroy(a->join);
+    if (a->fork) (void)hipEventDestroy(a->fork);
+    if (a->s) (void)hipStreamDestroy(a->s);
+    delete a;
+    a = nullptr;
+  }
+  if (have_cur && cur != dev) (void)hipSetDevice(cur);
+  if (a) {
+    std::lock_guard<std::mutex> g(g_aux_mu);
+    ++g_aux_live;
+  }
+  return a;
+}
+
+void aux_release(AuxStream* a) {
+  if (!a) return;
+  std::lock_guard<std::mutex> g(g_aux_mu);
+  g_aux_idle[a->device].push_back(a);
+}
+
+void aux_pool_trim() {
+  std::vector<AuxStream*> gone;
+  {
+    std::lock_guard<std::mutex> g(g_aux_mu);
+    for (auto& idle : g_aux_idle) {
+      gone.insert(gone.end(), idle.begin(), idle.end());
+      idle.clear();
+    }
+    g_aux_live -= static_cast<uint32_t>(gone.size());
+  }
+  for (AuxStream* a : gone) {
+    // (work still queued on the stream completes before its resources go)
+    (void)hipStreamSynchronize(a->s);
+    (void)hipEventDestroy(a->join);
+    (void)hipEventDestroy(a->fork);
+    (void)hipStreamDestroy(a->s);
+    delete a;
+  }
+  (void)hipGetLastError();
+}
+
+void aux_pool_stats(uint32_t* live, uint32_t* idle) {
+  std::lock_guard<std::mutex> g(g_aux_mu);
+  uint32_t n = 0;
+  for (auto& v : g_aux_idle) n += static_cast<uint32_t>(v.size());
+  if (live) *live = g_aux_live;
+  if (idle) *idle = n;
+}
 
 #ifdef FORST_DIAG
 const char* diag_env(const char* name) {
@@ -250,6 +344,11 @@ FORST_API const char* forst_last_error(void) { return g_last_error.c_str(); }
 FORST_API const char* forst_last_kernel(void) { return g_last_kernel; }
 
 FORST_API int forst_init_device(void) { return check_device(); }
+
+FORST_API int forst_aux_stream_stats(uint32_t* live, uint32_t* idle) {
+  aux_pool_stats(live, idle);
+  return FORST_OK;
+}
 
 FORST_API int forst_block_checksum_batch(int checksum_type, const uint8_t* base,
                                          uint64_t base_len, const uint64_t* offsets,

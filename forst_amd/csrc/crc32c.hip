@@ -2067,11 +2067,15 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream
                     ? CrcKernel::kRows
                     : CrcKernel::kV2;
 #ifdef FORST_DIAG
-  if (a.base_len >= kRB) k = diag_crc_kernel(k, mode);
+  // (never for the WAL writer mode: only the rows kernel masks its CRCs)
+  if (a.base_len >= kRB && !a.wal_hs) k = diag_crc_kernel(k, mode);
   if (k == CrcKernel::kRows || k == CrcKernel::kRowsD2) {
     if (a.n >= 0xffffffffull) k = CrcKernel::kV2;
   }
 #endif
+  // the WAL writer mode (wal_hs: header offsets + payload lengths, masked
+  // output) exists in the rows kernel only
+  if (a.wal_hs && (mode != kModeRaw || k != CrcKernel::kRows)) return hipErrorInvalidValue;
   *name = crc_kernel_name(k, mode);
   if (k == CrcKernel::kRows && mode == kModeRaw && a.n < uint64_t(64) * grid * kWaves)
     *name = "crc32c_rows_raw_small_kernel";

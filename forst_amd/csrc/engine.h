@@ -126,6 +126,21 @@ const char* diag_env(const char* name);
 // stream-ordered scratch from a per-device pool that keeps freed memory
 hipError_t scratch_alloc(void** p, size_t bytes, hipStream_t stream);
 hipError_t scratch_free(void* p, hipStream_t stream);
+// A second stream with fork / join events on the device of a caller's stream
+// (the WAL calls run a side branch on it beside their main kernel).  Taken
+// from a per-device pool and given back before the call returns, so the pool
+// holds at most as many as there were calls in flight at once; idle ones are
+// destroyed by aux_pool_trim (forst_host_context_trim).  nullptr: none could
+// be made (the caller then runs everything on its own stream).
+struct AuxStream {
+  hipStream_t s;
+  hipEvent_t fork, join;
+  int device;
+};
+AuxStream* aux_acquire(hipStream_t caller);
+void aux_release(AuxStream* a);
+void aux_pool_trim();
+void aux_pool_stats(uint32_t* live, uint32_t* idle);
 // work feed of a rows-kernel launch over nw waves (stream_common.h): sets
 // share1 and a zeroed ticket counter that the caller releases with
 // scratch_free(a.ticket) after the launch (diagnostics build:

@@ -39,6 +39,7 @@
 #include <vector>
 
 #include "../../include/forst_checksum.h"
+#include "engine.h"
 
 namespace {
 
@@ -533,19 +534,29 @@ FORST_API int forst_host_context_stats(uint32_t* contexts, uint64_t* device_byte
 // the driver (contexts, threads and streams stay; the next call that takes
 // one grows it again)
 FORST_API int forst_host_context_trim(uint64_t* released_bytes) {
-  std::lock_guard<std::mutex> lk(g_pool_mu);
+  // the releases run on the caller's thread: its current device is restored
+  // afterwards, so the caller's later HIP (or torch) work keeps its device
+  int prev_dev = -1;
+  const bool have_prev = hipGetDevice(&prev_dev) == hipSuccess;
   uint64_t freed = 0;
-  for (auto& kv : *g_free)
-    for (DeviceCtx* c : kv.second) {
-      std::lock_guard<std::mutex> rl(c->res_mu);
-      (void)hipSetDevice(c->device);
-      for (Slot& s : c->slot) {
-        if (s.d) freed += s.dbytes + s.blocks * kPerBlock + 64;
-        if (s.hbase) freed += s.blocks * kPerBlock + 128 + s.hbytes;
-        s.release();
-        s.win = -1;
+  {
+    std::lock_guard<std::mutex> lk(g_pool_mu);
+    for (auto& kv : *g_free)
+      for (DeviceCtx* c : kv.second) {
+        std::lock_guard<std::mutex> rl(c->res_mu);
+        (void)hipSetDevice(c->device);
+        for (Slot& s : c->slot) {
+          if (s.d) freed += s.dbytes + s.blocks * kPerBlock + 64;
+          if (s.hbase) freed += s.blocks * kPerBlock + 128 + s.hbytes;
+          s.release();
+          s.win = -1;
+        }
       }
-    }
+  }
+  // the WAL calls' idle auxiliary streams and events (engine.h aux_pool_trim)
+  forst::aux_pool_trim();
+  if (have_prev) (void)hipSetDevice(prev_dev);
+  (void)hipGetLastError();
   if (released_bytes) *released_bytes = freed;
   return FORST_OK;
 }

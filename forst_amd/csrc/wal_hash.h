@@ -147,33 +147,20 @@ __global__ void __launch_bounds__(kWhLanes) wh_select_kernel(const uint64_t* gle
 // profiles/ab_r04/a14_gather_overlap.log).  The recovery's remainder batch
 // keeps one stream: there the fork and join cost more than the overlap gains
 // (C5 recovery +0.06..0.1 ms in the same A/B).
-// One non-blocking stream and two events per host thread and device, created
-// on first use; any failure there falls back to the caller's stream alone.
+// The second stream and its fork / join events come from the per-device pool
+// of engine.h (aux_acquire: the device of the caller's stream), held for the
+// call only; any failure there falls back to the caller's stream alone.
 #ifndef FORST_WH_OVERLAP
 #define FORST_WH_OVERLAP 1
 #endif
-struct WhAux {
-  hipStream_t s = nullptr;
-  hipEvent_t fork = nullptr, join = nullptr;
-  bool tried = false;
+// holds a pool entry for one call (given back on every exit)
+struct AuxHold {
+  AuxStream* a = nullptr;
+  AuxHold() = default;
+  AuxHold(const AuxHold&) = delete;
+  AuxHold& operator=(const AuxHold&) = delete;
+  ~AuxHold() { aux_release(a); }
 };
-inline WhAux* wh_aux() {
-  constexpr int kMaxDev = 16;
-  thread_local WhAux aux[kMaxDev];
-  int d = 0;
-  if (hipGetDevice(&d) != hipSuccess || d < 0 || d >= kMaxDev) return nullptr;
-  WhAux& a = aux[d];
-  if (!a.tried) {
-    a.tried = true;
-    if (hipStreamCreateWithFlags(&a.s, hipStreamNonBlocking) != hipSuccess ||
-        hipEventCreateWithFlags(&a.fork, hipEventDisableTiming) != hipSuccess ||
-        hipEventCreateWithFlags(&a.join, hipEventDisableTiming) != hipSuccess) {
-      a.s = nullptr;
-      (void)hipGetLastError();
-    }
-  }
-  return a.s ? &a : nullptr;
-}
 
 inline size_t wh_up256(size_t b) { return (b + 255) & ~size_t(255); }
 inline dim3 wh_grid(uint64_t n) {
@@ -238,7 +225,9 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
   // for the two totals (on an event behind their copies), so the GPU does not
   // idle through the host's turnaround, and the gathered branch starts on the
   // second stream while the frag kernel runs.
-  WhAux* aux = FORST_WH_OVERLAP && overlap ? wh_aux() : nullptr;
+  AuxHold hold;
+  if (FORST_WH_OVERLAP && overlap) hold.a = aux_acquire(st);
+  AuxStream* aux = hold.a;
   if (aux && hipEventRecord(aux->fork, st) != hipSuccess) {
     (void)hipGetLastError();
     aux = nullptr;

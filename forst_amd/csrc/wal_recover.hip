@@ -1382,7 +1382,8 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   q.take(A, ni, nb, nt_max);
   const Tokens& t = q.t;
   uint64_t n_cand = 0;
-  WhAux* raw_aux = nullptr;  // second stream of the raw CRC (beside the fused kernel)
+  AuxHold raw_hold;  // second stream of the raw CRC (beside the fused kernel)
+  AuxStream* raw_aux = nullptr;
   uint64_t cpos_mask = ~0ull;  // 0xffffffff when cpos holds the packed positions
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q1.cnt,
@@ -1434,14 +1435,14 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         fa.init_crcs = q.l_info;
         fa.modifiers = q.l_first;
         fa.crc_ez = q.c.ez;
-        fa.crc_ok = q.crc_ok;  // pre-filled with 1: the fused kernel stores mismatches only
+        fa.crc_ok = q.crc_ok;  // pre-filled with 0 (fail-closed): the fused kernel stores every verdict
         fa.out64 = q.cand_hash;
         fa.n = n_cand;
-        if ((e = hipMemsetAsync(q.crc_ok, 1, ni, st)) != hipSuccess) return fail(e);
+        if ((e = hipMemsetAsync(q.crc_ok, 0, ni, st)) != hipSuccess) return fail(e);
         // the raw CRC of the other records does not depend on the fused
         // kernel (disjoint items of crc_ok): on a second stream, forked after
         // the memset, it runs in the fused kernel's launch tail
-        if (FORST_REC_OVERLAP && n_raw && (raw_aux = wh_aux()) != nullptr &&
+        if (FORST_REC_OVERLAP && n_raw && (raw_aux = raw_hold.a = aux_acquire(st)) != nullptr &&
             (hipEventRecord(raw_aux->fork, st) != hipSuccess ||
              hipStreamWaitEvent(raw_aux->s, raw_aux->fork, 0) != hipSuccess)) {
           (void)hipGetLastError();

@@ -1523,8 +1523,9 @@ xxh3_frag_kernel(BlockArgs a) {
       };
       if (__ballot(ends)) {
         const uint32_t V = row_value(cs) ^ (started ? cu.ez[0] : 0u);
-        // (the caller pre-fills crc_ok with 1: only mismatches are stored)
-        if (ends && t == 0 && V != cu.ez[1]) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = 0;
+        // every verdict is stored (the caller pre-fills crc_ok with 0: a
+        // fragment whose row never reaches its end reads as a mismatch)
+        if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
 
         const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
@@ -1563,7 +1564,7 @@ xxh3_frag_kernel(BlockArgs a) {
           const bool endsB = pb && L - W0 <= 1024u;
           const uint32_t VB = row_value(sb) ^ cu.ez[2];
           if (endsB && t == 0)
-            if (VB != cu.ez[3]) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = 0;
+            a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = VB == cu.ez[3] ? 1 : 0;
           if (pb && !endsB) {
 #pragma unroll
             for (uint32_t k = 0; k < kNC; ++k) ns[k] = sb[k];
@@ -1891,8 +1892,8 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
       !a.crc_ok)
     return hipErrorInvalidValue;
 // 3 waves per SIMD (one 12-wave workgroup per CU, its 136 KiB of tables):
-// 168 VGPRs with 9 spilled dwords; A/B against 2 waves (8-wave workgroups,
-// 203 VGPRs, no spills): C5 recovery 22.95 -> 21.77 ms
+// 164 VGPRs, no spills (round 4); A/B against 2 waves (8-wave workgroups):
+// 2 waves ran the kernel 5 % slower
 #ifndef FORST_FRAG_CRC_WPE
 #define FORST_FRAG_CRC_WPE 3
 #endif

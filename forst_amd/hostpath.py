@@ -127,3 +127,11 @@ def context_trim():
     r = ctypes.c_uint64()
     _check(lib().forst_host_context_trim(ctypes.byref(r)))
     return r.value
+
+
+def aux_stream_stats():
+    """(live, idle): the WAL calls' second streams in the per-device pool
+    (forst_aux_stream_stats); forst_host_context_trim destroys the idle ones"""
+    live, idle = ctypes.c_uint32(), ctypes.c_uint32()
+    _check(lib().forst_aux_stream_stats(ctypes.byref(live), ctypes.byref(idle)))
+    return live.value, idle.value

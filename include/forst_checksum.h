@@ -431,6 +431,13 @@ const char* forst_host_last_error(void);
 int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
                              uint64_t* pinned_bytes);
 int forst_host_context_trim(uint64_t* released_bytes);
+/* The WAL calls (forst_wal_record_xxh3_batch, forst_wal_recover_batch) run a
+ * side branch on a second stream of the caller's device, taken from a
+ * per-device pool for the duration of the call: the pool never holds more
+ * streams than there were such calls in flight at once, whatever the number
+ * of host threads that made them.  *live = streams created and not destroyed,
+ * *idle = those not in use; forst_host_context_trim destroys the idle ones. */
+int forst_aux_stream_stats(uint32_t* live, uint32_t* idle);
 /* BlockFetcher's decompression of one block (table/block_fetcher.cc:333-345,
  * UncompressSerializedBlock, table/format.cc:637-700), host only: the
  * structural blocks the whole-file verify decodes.  compression_type =

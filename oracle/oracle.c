@@ -885,11 +885,46 @@ typedef struct {
   uint8_t* ok;
   size_t lo, hi;
   uint64_t bad;
+  /* kind 4 (logical WAL records): first physical record of each of the
+   * n_all records, n_phys physical records with hs-byte headers */
+  const uint64_t* first;
+  uint64_t n_phys;
+  size_t n_all;
+  uint32_t hs;
 } batch_job;
+
+/* kind 4: XXH3_64bits of each logical record's payload, its fragments
+ * gathered back to back (log::Reader::ReadRecord's record checksum,
+ * db/log_reader.cc:95-165, over the scratch it assembles at :129-156) */
+static void logical_xxh3_range(batch_job* j) {
+  size_t cap = (size_t)1 << 16;
+  uint8_t* buf = (uint8_t*)malloc(cap);
+  for (size_t i = j->lo; i < j->hi; i++) {
+    const uint64_t b = j->first[i];
+    const uint64_t e = i + 1 < j->n_all ? j->first[i + 1] : j->n_phys;
+    size_t len = 0;
+    for (uint64_t q = b; q < e; q++) len += j->sizes[q];
+    if (len > cap) {
+      while (cap < len) cap *= 2;
+      buf = (uint8_t*)realloc(buf, cap);
+    }
+    size_t at = 0;
+    for (uint64_t q = b; q < e; q++) {
+      memcpy(buf + at, j->base + j->offsets[q] + j->hs, j->sizes[q]);
+      at += j->sizes[q];
+    }
+    j->out64[i] = oracle_xxh3_64_fast(buf, len);
+  }
+  free(buf);
+}
 
 static void* batch_worker(void* arg) {
   batch_job* j = (batch_job*)arg;
   uint64_t bad = 0;
+  if (j->kind == 4) {
+    logical_xxh3_range(j);
+    return NULL;
+  }
   for (size_t i = j->lo; i < j->hi; i++) {
     const uint8_t* p = j->base + j->offsets[i];
     uint32_t m = j->modifiers ? j->modifiers[i] : 0;
@@ -1003,6 +1038,23 @@ void oracle_xxh3_batch(const uint8_t* base, const uint64_t* offsets,
   j.base = base;
   j.offsets = offsets;
   j.sizes = lengths;
+  j.out64 = out;
+  run_batch(j, n, nthreads);
+}
+
+void oracle_wal_record_xxh3_batch(const uint8_t* log, const uint64_t* phys_offsets,
+                                  const uint32_t* phys_lengths, uint64_t n_phys, uint32_t hs,
+                                  const uint64_t* first, uint64_t* out, size_t n, int nthreads) {
+  batch_job j;
+  memset(&j, 0, sizeof j);
+  j.kind = 4;
+  j.base = log;
+  j.offsets = phys_offsets;
+  j.sizes = phys_lengths;
+  j.n_phys = n_phys;
+  j.hs = hs;
+  j.first = first;
+  j.n_all = n;
   j.out64 = out;
   run_batch(j, n, nthreads);
 }
@@ -1134,6 +1186,15 @@ typedef struct {
   uint64_t nbytes;
   uint64_t blo, bhi;
   uint64_t nrec, bad;
+  /* per-block outputs (oracle_wal_verify_blocks; NULL for the totals form):
+   * status (0 ok, 1 checksum, 2 length, 3 zero record, 4 old record),
+   * records verified before the first failure, offset in the block of the
+   * failing header or of the end of parsing; log_number for recyclable
+   * headers (log_reader.cc:497-503) */
+  uint8_t* status;
+  uint32_t* nrec_out;
+  uint32_t* fail_out;
+  uint32_t log_number;
 } wal_job;
 
 static void* wal_worker(void* arg) {
@@ -1144,6 +1205,8 @@ static void* wal_worker(void* arg) {
     uint64_t end = start + LOG_BLOCK;
     if (end > j->nbytes) end = j->nbytes;
     uint64_t pos = start;
+    uint32_t blk_ok = 0;
+    uint8_t st = 0;
     while (end - pos >= LOG_HDR) {
       const uint8_t* h = j->buf + pos;
       uint32_t length = (uint32_t)h[4] | ((uint32_t)h[5] << 8);
@@ -1153,18 +1216,49 @@ static void* wal_worker(void* arg) {
                   type == kRecyclableUserDefinedTimestampSizeType;
       if (recyc) hs = LOG_RHDR;
       if (end - pos < hs) break;
-      if (hs + length > end - pos) { bad++; break; } /* kBadRecordLen */
-      if (type == kZeroType && length == 0) break;    /* preallocated */
+      if (hs + length > end - pos) { bad++; st = 2; break; } /* kBadRecordLen */
+      if (recyc && ld32(h + 7) != j->log_number) { st = 4; break; } /* kOldRecord */
+      if (type == kZeroType && length == 0) { st = 3; break; } /* preallocated */
       uint32_t expected = oracle_crc32c_unmask(ld32(h));
       uint32_t actual = ~crc_raw_update_fast(~0u, h + 6, length + hs - 6);
       nrec++;
-      if (actual != expected) { bad++; break; }
+      if (actual != expected) { bad++; st = 1; break; }
+      blk_ok++;
       pos += hs + length;
     }
+    if (j->status) j->status[b] = st;
+    if (j->nrec_out) j->nrec_out[b] = blk_ok;
+    if (j->fail_out) j->fail_out[b] = (uint32_t)(pos - start);
   }
   j->nrec = nrec;
   j->bad = bad;
   return NULL;
+}
+
+/* per log block: status / verified records / failing offset (see wal_job) */
+void oracle_wal_verify_blocks(const uint8_t* buf, uint64_t nbytes, uint32_t log_number,
+                              uint8_t* status, uint32_t* nrec, uint32_t* fail_off, int nthreads) {
+  crc_once();
+  uint64_t nblocks = (nbytes + LOG_BLOCK - 1) / LOG_BLOCK;
+  if (nthreads < 1) nthreads = 1;
+  wal_job* jobs = (wal_job*)calloc((size_t)nthreads, sizeof(wal_job));
+  pthread_t* th = (pthread_t*)calloc((size_t)nthreads, sizeof(pthread_t));
+  for (int t = 0; t < nthreads; t++) {
+    jobs[t].buf = buf;
+    jobs[t].nbytes = nbytes;
+    jobs[t].blo = nblocks * (uint64_t)t / (uint64_t)nthreads;
+    jobs[t].bhi = nblocks * (uint64_t)(t + 1) / (uint64_t)nthreads;
+    jobs[t].status = status;
+    jobs[t].nrec_out = nrec;
+    jobs[t].fail_out = fail_off;
+    jobs[t].log_number = log_number;
+  }
+  for (int t = 1; t < nthreads; t++)
+    pthread_create(&th[t], NULL, wal_worker, &jobs[t]);
+  wal_worker(&jobs[0]);
+  for (int t = 1; t < nthreads; t++) pthread_join(th[t], NULL);
+  free(jobs);
+  free(th);
 }
 
 uint64_t oracle_wal_verify(const uint8_t* buf, uint64_t nbytes, uint8_t* ok,

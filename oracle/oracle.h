@@ -88,6 +88,15 @@ void oracle_xxh3_batch(const uint8_t* base, const uint64_t* offsets,
                        const uint32_t* lengths, uint64_t* out, size_t n,
                        int nthreads);
 
+/* XXH3_64bits of logical WAL records as log::Reader::ReadRecord computes its
+ * record checksum (db/log_reader.cc:95-165): record j is the payloads of the
+ * physical records [first[j], first[j+1]) (the last: up to n_phys) back to
+ * back; physical record q has its hs-byte header at phys_offsets[q] and
+ * phys_lengths[q] payload bytes after it. */
+void oracle_wal_record_xxh3_batch(const uint8_t* log, const uint64_t* phys_offsets,
+                                  const uint32_t* phys_lengths, uint64_t n_phys, uint32_t hs,
+                                  const uint64_t* first, uint64_t* out, size_t n, int nthreads);
+
 /* ---- WAL (db/log_format.h, db/log_writer.cc, db/log_reader.cc) ---- */
 /* masked record CRC as EmitPhysicalRecord writes it (db/log_writer.cc:228) */
 uint32_t oracle_wal_record_crc(int type, uint32_t log_number,
@@ -110,6 +119,14 @@ uint64_t oracle_wal_frame(const uint8_t* payloads, const uint32_t* lengths,
  * *bad receives the count of CRC mismatches. */
 uint64_t oracle_wal_verify(const uint8_t* buf, uint64_t nbytes, uint8_t* ok,
                            uint64_t ok_cap, uint64_t* bad, int nthreads);
+
+/* The same check per log block, with forst_wal_verify_batch's outputs:
+ * status[b] (0 ok, 1 checksum mismatch, 2 bad length, 3 zero record, 4 old
+ * record: a recyclable header whose log number is not log_number), nrec[b] =
+ * records verified before the first failure, fail_off[b] = offset in the
+ * block of the failing header or of the end of parsing. */
+void oracle_wal_verify_blocks(const uint8_t* buf, uint64_t nbytes, uint32_t log_number,
+                              uint8_t* status, uint32_t* nrec, uint32_t* fail_off, int nthreads);
 
 /* ---- synthetic data ---- */
 uint64_t oracle_splitmix64(uint64_t x);

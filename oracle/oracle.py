@@ -51,9 +51,11 @@ def lib():
             "oracle_crc32c_batch": (None, [vp, vp, vp, vp, sz, i]),
             "oracle_xxh3_batch": (None, [vp, vp, vp, vp, sz, i]),
             "oracle_wal_record_crc": (u32, [i, u32, vp, sz]),
+            "oracle_wal_record_xxh3_batch": (None, [vp, vp, vp, u64, u32, vp, vp, sz, i]),
             "oracle_wal_framed_size": (u64, [vp, sz, i]),
             "oracle_wal_frame": (u64, [vp, vp, sz, i, u32, vp, vp, vp, vp]),
             "oracle_wal_verify": (u64, [vp, u64, vp, u64, vp, i]),
+            "oracle_wal_verify_blocks": (None, [vp, u64, u32, vp, vp, vp, i]),
             "oracle_hash64": (u64, [vp, sz, u64]),
             "oracle_kv_protect": (u64, [vp, sz, vp, sz, i, i, u64, i, u32]),
             "oracle_kv_verify": (i, [u64, u32, vp]),
@@ -183,6 +185,32 @@ def xxh3_batch(base, offsets, lengths, nthreads=1):
     return out
 
 
+def wal_record_xxh3_batch(log, phys_offsets, phys_lengths, first, hs=7, nthreads=1):
+    """XXH3 of every logical record: record j = payloads of physical records
+    [first[j], first[j+1]) (db/log_reader.cc:95-165)"""
+    po = np.ascontiguousarray(phys_offsets, np.uint64)
+    pl = np.ascontiguousarray(phys_lengths, np.uint32)
+    fi = np.ascontiguousarray(first, np.uint64)
+    out = np.zeros(len(fi), dtype=np.uint64)
+    lib().oracle_wal_record_xxh3_batch(_ptr(log), _ptr(po), _ptr(pl), len(po), hs, _ptr(fi),
+                                       _ptr(out), len(fi), nthreads)
+    return out
+
+
+def host_threads():
+    """CPU threads this process may use: the cgroup cpu.max quota where one is
+    set (the GPU box: 16), else the affinity mask"""
+    n = len(os.sched_getaffinity(0))
+    try:
+        with open("/sys/fs/cgroup/cpu.max") as f:
+            q, per = f.read().split()[:2]
+        if q != "max":
+            n = min(n, max(1, int(q) // int(per)))
+    except (OSError, ValueError):
+        pass
+    return max(1, n)
+
+
 def wal_record_crc(rtype, log_number, payload):
     p, n, _k = _buf(payload)
     return lib().oracle_wal_record_crc(rtype, log_number, p, n)
@@ -211,6 +239,19 @@ def wal_verify(buf, nthreads=1):
     bad = ctypes.c_uint64()
     n = lib().oracle_wal_verify(_ptr(buf), buf.nbytes, None, 0, ctypes.byref(bad), nthreads)
     return n, bad.value
+
+
+def wal_verify_blocks(buf, log_number=0, nthreads=1):
+    """per 32 KiB log block: (status, records verified before the first
+    failure, offset of the failing header / end of parsing), as
+    forst_wal_verify_batch reports them (db/log_reader.cc:450-531)"""
+    nb = (buf.nbytes + 32767) // 32768
+    st = np.zeros(nb, np.uint8)
+    nr = np.zeros(nb, np.uint32)
+    fo = np.zeros(nb, np.uint32)
+    lib().oracle_wal_verify_blocks(_ptr(buf), buf.nbytes, log_number, _ptr(st), _ptr(nr), _ptr(fo),
+                                   nthreads)
+    return st, nr, fo
 
 
 KV_SEED_K, KV_SEED_V = 0, 0xD28AAD72F49BD50B  # db/kv_checksum.h:84-88

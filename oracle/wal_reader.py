@@ -276,7 +276,7 @@ class Reader:
             in_frag, scratch = False, b""
 
 
-def resume_at(reader, pos):
+def resume_at(reader, pos, recycled=False):
     """TEST-INFRASTRUCTURE shortcut (no reference counterpart): put `reader`
     in the state ReadRecord leaves behind after returning a complete record
     whose last fragment ends at `pos` -- the 32 KiB block holding `pos` in the
@@ -285,7 +285,9 @@ def resume_at(reader, pos):
     window of a large log (starting at the block boundary below `pos`) can be
     checked against the serial reader without replaying everything before
     it.  Valid only when the log before `pos` holds no control records
-    (SetCompressionType, timestamp-size) and no recycled headers."""
+    (SetCompressionType, timestamp-size); `recycled` = whether the log's
+    first header is a recyclable one (the reader's recycled_ flag,
+    log_reader.cc:476-479)."""
     blk = pos // kBlockSize * kBlockSize
     reader.file_pos = blk
     reader.end_of_buffer_offset = blk
@@ -293,6 +295,7 @@ def resume_at(reader, pos):
     reader.read_more()
     reader.buf_lo = pos
     reader.first_record_read = True
+    reader.recycled = recycled
     return reader
 
 

@@ -272,6 +272,13 @@ inline hipError_t hipEventCreateWithFlags(hipEvent_t* e, unsigned) {
   *e = &dummy;
   return hipSuccess;
 }
+inline hipError_t hipStreamDestroy(hipStream_t) { return hipSuccess; }
+inline hipError_t hipEventDestroy(hipEvent_t) { return hipSuccess; }
+inline hipError_t hipStreamGetDevice(hipStream_t, int* d) {
+  *d = 0;
+  return hipSuccess;
+}
+inline hipError_t hipSetDevice(int) { return hipSuccess; }
 inline hipError_t hipEventRecord(hipEvent_t, hipStream_t) { return hipSuccess; }
 inline hipError_t hipEventSynchronize(hipEvent_t) { return hipSuccess; }
 inline hipError_t hipStreamWaitEvent(hipStream_t, hipEvent_t, unsigned) { return hipSuccess; }

@@ -149,6 +149,9 @@ def test_emu_wal_pipeline_statuses(recyclable, split, monkeypatch):
     for g, w in zip(got[:3], want[:3]):
         assert (g == w).all()
     assert got[3] == want[3] and got[3] >= 2
+    # the oracle's per-block form (the full-size GPU tests' checker) agrees
+    for g, w in zip(got[:3], O.wal_verify_blocks(b, 9, nthreads=2)):
+        assert (np.asarray(g) == w).all()
     assert got[0][blk[k0]] == 1 and got[0][blk[k1]] == 2 and got[0][blk[k3]] == 3
     if recyclable:
         assert got[0][blk[k2]] == 4

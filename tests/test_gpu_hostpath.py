@@ -152,3 +152,67 @@ def test_out_of_order_descriptors_and_partial_registration():
         lib().forst_host_unregister(ptr)
         del buf
         mm.close()
+
+
+def test_aux_streams_bounded_by_calls_in_flight():
+    """64 short-lived host threads, 8 at a time, each on its own torch stream,
+    through forst_wal_record_xxh3_batch and forst_wal_recover_batch (their
+    side branches run on a second stream, db_impl_open.cc:1206-1245 calls
+    from whichever thread recovers): the second streams come from the
+    per-device pool, so no more exist than calls were in flight at once,
+    results are unchanged, and forst_host_context_trim destroys the idle ones
+    and leaves the caller's current device as it was"""
+    import threading
+    PIT = 2  # WALRecoveryMode::kPointInTimeRecovery (options.h:1192)
+    w = workload.make_wal_batch(20000, workload.SEEDS["C5"])
+    offs = torch.from_numpy(w.rec_offsets.view(np.int64)).cuda()
+    want = engine.wal_record_xxh3_batch(w.log, offs)[0].cpu()
+    rec0, _, res0 = engine.wal_recover_batch(w.log, 0, PIT)
+    want_rec = rec0["hash"][:res0.n_records].cpu()
+    torch.cuda.synchronize()
+    live0, _ = hostpath.aux_stream_stats()
+    errs = []
+
+    def work(k):
+        try:
+            torch.cuda.set_device(0)
+            s = torch.cuda.Stream()
+            with torch.cuda.stream(s):
+                if k % 2:
+                    h, _ = engine.wal_record_xxh3_batch(w.log, offs)
+                    ok = torch.equal(h.cpu(), want)
+                else:
+                    rec, _, res = engine.wal_recover_batch(w.log, 0, PIT)
+                    ok = torch.equal(rec["hash"][:res.n_records].cpu(), want_rec)
+            if not ok:
+                errs.append(f"thread {k}: wrong result")
+        except Exception as e:  # noqa: BLE001 (reported below)
+            errs.append(f"thread {k}: {e!r}")
+
+    for wave in range(8):
+        ts = [threading.Thread(target=work, args=(8 * wave + i,)) for i in range(8)]
+        for t in ts:
+            t.start()
+        for t in ts:
+            t.join()
+    assert not errs, errs[:3]
+    live, idle = hostpath.aux_stream_stats()
+    assert live <= max(live0, 8) and idle == live, (live0, live, idle)
+    dev = torch.cuda.current_device()
+    hostpath.context_trim()
+    assert hostpath.aux_stream_stats() == (0, 0)
+    assert torch.cuda.current_device() == dev
+    # the next call creates one again and gives it back
+    assert torch.equal(engine.wal_record_xxh3_batch(w.log, offs)[0].cpu(), want)
+    assert hostpath.aux_stream_stats() == (1, 1)
+
+
+@pytest.mark.skipif(torch.cuda.device_count() < 2, reason="needs two GPUs")
+def test_trim_keeps_the_callers_device():
+    """a context on device 1, trimmed from a thread whose current device is 0:
+    the thread's device stays 0 (forst_host_context_trim restores it)"""
+    b, hb, offs, sizes = batch(500, 4096, CT.kCRC32c, 0xF0E57000B1)
+    hostpath.block_verify_host(CT.kCRC32c, hb, offs, sizes, devices=(1,))
+    torch.cuda.set_device(0)
+    hostpath.context_trim()
+    assert torch.cuda.current_device() == 0

@@ -119,11 +119,13 @@ def test_recover_dense_tiny_records():
 
 
 
-def clean_expectation(rec_offsets, rec_lengths, rec_types, hashes):
+def clean_expectation(rec_offsets, rec_lengths, rec_types, hashes, hs=7):
     """the records a clean, writer-laid-out log recovers to: (offset, length,
-    hash, n_fragments) per logical record, and the first-fragment indices"""
+    hash, n_fragments) per logical record, and the first-fragment indices
+    (hs: the header size, 7 or 11 for recyclable headers)"""
     nphys = len(rec_offsets)
-    starts = np.nonzero((rec_types == 1) | (rec_types == 2))[0]
+    starts = np.nonzero((rec_types == 1) | (rec_types == 2) | (rec_types == 5) |
+                        (rec_types == 6))[0]
     ends = np.concatenate([starts[1:], [nphys]])
     cum = np.concatenate([[0], np.cumsum(rec_lengths.astype(np.int64))])
     # Reader::LastRecordOffset is where the reader stood when it went for the
@@ -134,15 +136,19 @@ def clean_expectation(rec_offsets, rec_lengths, rec_types, hashes):
     offs = rec_offsets.astype(np.int64)
     hdr = offs[starts]
     prev = np.maximum(starts - 1, 0)
-    prev_end = np.where(starts > 0, offs[prev] + 7 + rec_lengths[prev].astype(np.int64), 0)
-    reported = np.where(hdr % 32768 == 0, prev_end, hdr)
+    prev_end = np.where(starts > 0, offs[prev] + hs + rec_lengths[prev].astype(np.int64), 0)
+    # -- a tail of 7..10 bytes (recyclable logs pad < 11) is first read as a
+    # zero-type header (kBadRecord, log_reader.cc:509-518) that consumes it, so
+    # there the offset is the block start again
+    reported = np.where((hdr % 32768 == 0) & (hdr - prev_end < 7), prev_end, hdr)
     return {"offset": reported,
             "length": cum[ends] - cum[starts],
             "hash": np.asarray(hashes).view(np.int64),
             "n_fragments": (ends - starts).astype(np.int32)}, starts, ends
 
 
-def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode):
+def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode, log_number=0,
+                         recycled=False):
     """What the serial reader returns on a writer-laid-out log after one
     payload flip in each of the log blocks `vblocks` (physical records
     `victims`, >= 8 blocks apart): the clean records outside the damaged
@@ -150,7 +156,10 @@ def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode
     replayed from the start of the logical record holding the flip
     (wal_reader.resume_at) to four blocks past it, cut at the first record
     start at least two blocks past the flip (where the reader's state is
-    clean again).  Returns (offsets, lengths, hashes as uint64, reports)."""
+    clean again).  On a recycled log in kTolerateCorruptedTailRecords the
+    first mismatch ends the log (log_reader.cc:291-296 / :265 of the
+    restatement): then only the records in front of it remain.  Returns
+    (offsets, lengths, hashes as uint64, reports, outside mask)."""
     n = len(exp["offset"])
     windows = []
     for i, v in zip(victims, vblocks):
@@ -160,13 +169,18 @@ def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode
         cutoff = int(exp["offset"][j]) if j < n else total
         windows.append((o_start, cutoff, min(total, (int(v) + 4) * 32768)))
     assert all(windows[k][1] <= windows[k + 1][0] for k in range(len(windows) - 1))
+    stop_first = recycled and mode == R.kTolerateCorruptedTailRecords
     outside = np.ones(n, bool)
+    if stop_first:
+        windows = windows[:1]
+        outside[exp["offset"] >= windows[0][0]] = False
     for o_start, cutoff, _ in windows:
         outside[(exp["offset"] >= o_start) & (exp["offset"] < cutoff)] = False
     win_recs, want_reps = [], []
     for o_start, cutoff, end in windows:
         b0 = o_start // 32768 * 32768
-        r = R.resume_at(R.Reader(read_window(b0, end)), o_start - b0)
+        r = R.resume_at(R.Reader(read_window(b0, end), log_number), o_start - b0,
+                        recycled=recycled)
         while True:
             got = r.read_record(mode)
             if got is None:
@@ -183,93 +197,108 @@ def windowed_expectation(read_window, exp, starts, victims, vblocks, total, mode
     return wo[order], wl[order], wh[order], want_reps, outside
 
 
-def pick_flips(rng, rec_offsets, rec_lengths, n_log_blocks, k):
+def pick_flips(rng, rec_offsets, rec_lengths, n_log_blocks, k, hs=7):
     """k log blocks >= 8 apart, a physical record with payload in each, and
     one payload byte of it: (victims, blocks, byte positions)"""
     vblocks = np.sort(rng.choice(np.arange(4, n_log_blocks - 8, 8), k, replace=False))
     blk_of = (rec_offsets // 32768).astype(np.int64)
     victims = np.array([int(rng.choice(np.nonzero((blk_of == v) & (rec_lengths > 0))[0]))
                         for v in vblocks])
-    pos = rec_offsets[victims].astype(np.int64) + 7 + \
+    pos = rec_offsets[victims].astype(np.int64) + hs + \
         rng.integers(0, rec_lengths[victims].astype(np.int64))
     return victims, vblocks, pos
 
 
-@pytest.mark.parametrize("mode", [R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords])
-def test_windowed_expectation_equals_full_replay(mode):
+@pytest.mark.parametrize("recyclable", [False, True])
+@pytest.mark.parametrize("mode", MODES)
+def test_windowed_expectation_equals_full_replay(mode, recyclable):
     """the composition the full-size GPU test relies on, checked on a log the
     serial reader replays whole: clean records + per-flip windows replayed
-    from resume_at == read_all over the entire corrupted log"""
+    from resume_at == read_all over the entire corrupted log (legacy and
+    recyclable headers, every WALRecoveryMode); the clean log replays to the
+    clean expectation with no report"""
     from oracle import oracle as O
     rng = np.random.default_rng(8)
+    ln = 0x5EED if recyclable else 0
+    hs = 11 if recyclable else 7
     lens = (np.exp(rng.uniform(np.log(32), np.log(32768), 2500))).astype(np.uint32)
     payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), np.uint8)
-    log, po, pl = O.wal_frame(payload, lens)
+    log, po, pl = O.wal_frame(payload, lens, recyclable=recyclable, log_number=ln)
     types = np.array([log[int(o) + 6] for o in po], np.uint8)
+    starts0 = np.nonzero((types == 1) | (types == 2) | (types == 5) | (types == 6))[0]
+    hashes = O.wal_record_xxh3_batch(log, po, pl, starts0, hs=hs)
     cuml = np.concatenate([[0], np.cumsum(lens.astype(np.int64))])
-    hashes = np.array([O.xxh3_64(payload[cuml[j]:cuml[j + 1]].tobytes())
-                       for j in range(len(lens))], np.uint64)
-    exp, starts, _ = clean_expectation(po.astype(np.uint64), pl, types, hashes)
+    assert all(int(hashes[j]) == O.xxh3_64(payload[cuml[j]:cuml[j + 1]].tobytes())
+               for j in range(0, len(lens), 97))
+    exp, starts, _ = clean_expectation(po.astype(np.uint64), pl, types, hashes, hs)
+    recs, want_reps = R.read_all(log, ln, mode)
+    assert want_reps == [] and recs == [(int(a), int(b), int(c) & (2**64 - 1)) for a, b, c in
+                                        zip(exp["offset"], exp["length"], exp["hash"])]
     nblk = (len(log) + 32767) // 32768
-    victims, vblocks, pos = pick_flips(rng, po.astype(np.uint64), pl, nblk, 6)
+    victims, vblocks, pos = pick_flips(rng, po.astype(np.uint64), pl, nblk, 6, hs)
     bad = log.copy()
     bad[pos] ^= 1
     wo, wl, wh, reps, _ = windowed_expectation(lambda a, b: bad[a:b], exp, starts, victims,
-                                               vblocks, len(bad), mode)
-    recs, want_reps = R.read_all(bad, 0, mode)
+                                               vblocks, len(bad), mode, ln, recyclable)
+    recs, want_reps = R.read_all(bad, ln, mode)
     assert [(int(a), int(b), int(c)) for a, b, c in zip(wo, wl, wh)] == recs
     assert reps == want_reps
 
 
 @pytest.mark.gpu
-def test_full_size_c5_recovery():
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_full_size_c5_recovery(recyclable):
     """f2 at the bench's size (C5: 10 M logical records, ~44 GiB log, the log
-    bench.py times).  Clean log, PIT and skip modes: every record's (offset,
-    length, XXH3, fragment count) equals the writer's layout plus the a14
-    kernel's hashes (forst_wal_record_xxh3_batch), and 2000 sampled hashes the
-    oracle's XXH3 over the gathered payload.  Then one payload byte flipped in
-    each of 48 log blocks (>= 8 blocks apart): every record and every report
-    equals the serial reader's (oracle/wal_reader.py, db/log_reader.cc:69-531)
-    -- around each flip the reader is replayed from the start of the logical
-    record holding it to past the recovery point, elsewhere the clean
-    expectation holds."""
+    bench.py times; and the same records with recyclable 11-byte headers, as
+    recycle_log_file_num > 0 writes them, options.h:806, log_format.h:52).
+    Clean log, all four WALRecoveryModes (options.h:1192): every record's
+    (offset, length, XXH3, fragment count) equals the writer's layout and the
+    threaded oracle's XXH3 of EVERY record over a host copy of the log.  Then
+    one payload byte flipped in each of 48 log blocks (>= 8 blocks apart),
+    all four modes again: every record and every report equals the serial
+    reader's (oracle/wal_reader.py, db/log_reader.cc:69-531) -- around each
+    flip the reader is replayed from the start of the logical record holding
+    it to past the recovery point, elsewhere the clean expectation holds (on
+    the recycled log in kTolerateCorruptedTailRecords the first mismatch ends
+    the log)."""
     import torch
     from forst_amd import engine, workload
+    from oracle import oracle as O
     n = 10_000_000
-    w = workload.make_wal_batch(n, workload.SEEDS["C5"])
+    ln = 0x5EED if recyclable else 0
+    hs = 11 if recyclable else 7
+    w = workload.make_wal_batch(n, workload.SEEDS["C5"], recyclable=recyclable, log_number=ln)
     DEV = w.log.device
     nphys = len(w.rec_offsets)
-    h_a14, _ = engine.wal_record_xxh3_batch(w.log, torch.from_numpy(
-        w.rec_offsets.view(np.int64)).to(DEV))
-    exp, starts, ends = clean_expectation(w.rec_offsets, w.rec_lengths, w.rec_types,
-                                          h_a14.cpu().numpy())
+    logh = w.log[:w.total].cpu().numpy()
+    rt = w.rec_types
+    starts0 = np.nonzero((rt == 1) | (rt == 2) | (rt == 5) | (rt == 6))[0]
+    hashes = O.wal_record_xxh3_batch(logh, w.rec_offsets, w.rec_lengths, starts0, hs=hs,
+                                     nthreads=O.host_threads())
+    exp, starts, ends = clean_expectation(w.rec_offsets, w.rec_lengths, rt, hashes, hs)
     assert len(starts) == n
     keys = ("offset", "length", "hash", "n_fragments")
 
     def recover(mode):
-        rec, rep, res = engine.wal_recover_batch(w.log, 0, mode, record_capacity=n + 1024)
+        rec, rep, res = engine.wal_recover_batch(w.log, ln, mode, record_capacity=n + 1024)
         assert res.n_physical == nphys
         return ({k: rec[k].cpu().numpy() for k in keys},
                 [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")], res)
 
-    for mode in (R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords):
+    for mode in MODES:
         got, _, res = recover(mode)
-        assert res.n_records == n and res.n_reports == 0
+        assert res.n_records == n and res.n_reports == 0, (mode, res.n_records, res.n_reports)
         for k in keys:
             assert (got[k] == exp[k]).all(), (mode, k)
-    from oracle import oracle as O
-    rng = np.random.default_rng(3)
-    for j in rng.choice(n, 2000, replace=False):
-        parts = [w.log[int(w.rec_offsets[i]) + 7:int(w.rec_offsets[i]) + 7 +
-                       int(w.rec_lengths[i])].cpu().numpy() for i in range(starts[j], ends[j])]
-        assert int(exp["hash"][j]) & (2**64 - 1) == O.xxh3_64(np.concatenate(parts).tobytes())
 
     # ---- 48 flipped payload bytes, one per chosen log block ----------------
-    victims, vblocks, pos = pick_flips(rng, w.rec_offsets, w.rec_lengths, w.n_log_blocks, 48)
+    rng = np.random.default_rng(3)
+    victims, vblocks, pos = pick_flips(rng, w.rec_offsets, w.rec_lengths, w.n_log_blocks, 48, hs)
     w.log[torch.from_numpy(pos).to(DEV)] ^= 0x01
-    for mode in (R.kPointInTimeRecovery, R.kSkipAnyCorruptedRecords):
+    logh[pos] ^= 0x01
+    for mode in MODES:
         wo, wl, wh, want_reps, outside = windowed_expectation(
-            lambda a, b: w.log[a:b].cpu().numpy(), exp, starts, victims, vblocks, w.total, mode)
+            lambda a, b: logh[a:b], exp, starts, victims, vblocks, w.total, mode, ln, recyclable)
         got, reps, res = recover(mode)
         assert len(got["offset"]) == len(wo), (mode, len(got["offset"]), len(wo))
         assert np.array_equal(got["offset"], wo), mode
@@ -282,7 +311,9 @@ def test_full_size_c5_recovery():
         gr = [(int(b), reason_text(int(r_), int(t) & 0xFFFFFFFF), int(o))
               for o, b, r_, t in zip(po, pb, pr, pt)]
         assert gr == want_reps, (mode, gr[:4], want_reps[:4])
-        assert sum(1 for g in gr if g[1] == "checksum mismatch") == len(victims)
+        n_mis = sum(1 for g in gr if g[1] == "checksum mismatch")
+        assert n_mis == (0 if recyclable and mode == R.kTolerateCorruptedTailRecords
+                         else len(victims)), mode
 
 
 @pytest.mark.parametrize("recyclable", [False, True])

@@ -24,8 +24,12 @@ Also reported: per-kernel roofline (HIP events on the launch stream, and the
 kernel-trace average of the committed rocprofv3 profile of the same config),
 HBM traffic from the committed PMC summary, the CPU baseline (oracle = our
 restatement, timed on this host), the north-star point (1 M x 16 KiB, CRC32C
-and XXH3), C3/C4, the WAL config C5 and the PCIe-inclusive end-to-end rates
-(DESIGN.md §6).
+and XXH3), C3/C4, the legacy kxxHash / kxxHash64 types, the WAL config C5,
+per-KV protection (a15) and the PCIe-inclusive end-to-end rates (DESIGN.md
+§6).  At N = 1 with extras, bench.py runs the headline config and each extra
+in a child process of its own (this process never touches the GPU) and prints
+the merged line: each measurement starts from a fresh device allocation
+state.
 """
 import argparse
 import glob
@@ -637,6 +641,68 @@ def dry_run(args, world, rank):
         dist.destroy_process_group()
 
 
+def run_child(argv, timeout=600):
+    """bench.py <argv> in a child process (this process has not touched the
+    GPU); returns its last stdout line as JSON"""
+    env = dict(os.environ)
+    env.setdefault("HSA_ENABLE_IPC_MODE_LEGACY", "0")
+    r = subprocess.run([sys.executable, os.path.abspath(__file__)] + argv, env=env,
+                       stdout=subprocess.PIPE, stderr=subprocess.PIPE, text=True, timeout=timeout)
+    sys.stderr.write(r.stderr[-4000:])
+    if r.returncode != 0:
+        raise RuntimeError(f"bench.py {' '.join(argv)} failed ({r.returncode})")
+    return json.loads(r.stdout.strip().splitlines()[-1])
+
+
+EXTRA_SST = ("NS16", "NS16X", "C3", "C3S", "C4", "NS16H32", "NS16H64")
+
+
+def orchestrate(args):
+    """N = 1 with extras: the headline config (plus the CPU baseline and the
+    host-memory paths) and every extra run in a child process of its own, one
+    after the other, so each starts from a fresh device allocation state (in
+    one process, a 28 GiB batch allocated after another one measured 3-7 %
+    slower: C3 / C3S in BENCH_r04, bench_r05a).  This process never touches
+    the GPU; it merges the children's lines into the one JSON line."""
+    common = ["--steps", str(args.steps), "--warmup", str(args.warmup)]
+    line = run_child(["--config", args.config, "--child"] + common +
+                     (["--no-cpu-baseline"] if args.no_cpu_baseline else []))
+    extras = line.setdefault("extras", {})
+    for nm in EXTRA_SST + ("C5_wal", "a15_kv"):
+        try:
+            extras[nm] = run_child(["--extra", nm] + common)
+        except Exception as e:  # pragma: no cover
+            extras[nm + "_error"] = str(e)
+    print(json.dumps(line), flush=True)
+    return 0
+
+
+def run_extra(name, steps, warmup):
+    """one extra of the N = 1 bench line (a child of orchestrate)"""
+    from forst_amd import engine
+
+    engine.init_device()
+    if name == "C5_wal":
+        return run_wal(max(3, steps // 2), 1)
+    if name == "a15_kv":
+        return run_kv(steps, warmup)
+    r = run_config(name, steps, warmup, 0, 1)
+    r.pop("batch")
+    kv, kt = r["kernels"]["verify"], r["kernels"]["trailer"]
+    ns, _, _, tns = load_profile(kv["name"], name)
+    return {
+        "desc": r["desc"], "GiBps": round(r["gibs_total"], 1),
+        "verify_kernel_GiBps": round(kv["gibs_checksummed"], 1),
+        "verify_roofline_frac": round(kv["frac"], 4),
+        "verify_roofline_frac_kernel_trace": (
+            round(kv["alg_bytes"] / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if ns else None),
+        "verify_roofline_frac_kernel_trace_timed_steps": (
+            round(kv["alg_bytes"] / (tns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if tns else None),
+        "trailer_kernel_GiBps": round(kt["gibs_checksummed"], 1),
+        "trailer_roofline_frac": round(kt["frac"], 4),
+        "verify_kernel": kv["name"], "trailer_kernel": kt["name"]}
+
+
 def main():
     ap = argparse.ArgumentParser()
     ap.add_argument("--gpus", type=int, default=1)
@@ -648,7 +714,18 @@ def main():
                     help="skip north-star, C3/C4, C5 and end-to-end extras")
     ap.add_argument("--dry-run", action="store_true",
                     help="shard the described batch on the CPU (gloo) without a GPU")
+    ap.add_argument("--child", action="store_true",
+                    help="(orchestrate) the headline config + CPU baseline + host-memory paths")
+    ap.add_argument("--extra", default=None,
+                    help="(orchestrate) one extra: an SST config, C5_wal or a15_kv")
     args = ap.parse_args()
+
+    if args.extra:
+        print(json.dumps(run_extra(args.extra, args.steps, args.warmup)), flush=True)
+        return
+    if (args.gpus == 1 and "WORLD_SIZE" not in os.environ and not args.dry_run and
+            not args.child and not args.no_extras and args.config == "C2"):
+        sys.exit(orchestrate(args))
 
     if args.gpus > 1 and "WORLD_SIZE" not in os.environ:
         sys.exit(spawn_ranks(args))
@@ -668,7 +745,7 @@ def main():
     cpu = None
     if rank == 0 and world == 1 and not args.no_cpu_baseline:
         cpu = cpu_baseline(b, main_res["ctype"])
-    if world == 1 and not args.no_extras:
+    if world == 1 and (args.child or not args.no_extras):
         try:
             # the first pass pays one-time costs (host pinning, first touch of
             # the staging buffers): best of 3 passes, the first reported too
@@ -683,29 +760,6 @@ def main():
             extras["host_memory_verify_error"] = str(e)
     del b
     torch.cuda.empty_cache()
-    if world == 1 and not args.no_extras and args.config == "C2":
-        for nm in ("NS16", "NS16X", "C3", "C3S", "C4", "NS16H32", "NS16H64"):
-            # every extra config with the headline's step and warmup counts
-            r = run_config(nm, args.steps, args.warmup, rank, world)
-            r.pop("batch")
-            torch.cuda.empty_cache()
-            kv, kt = r["kernels"]["verify"], r["kernels"]["trailer"]
-            ns, _, _, tns = load_profile(kv["name"], nm)
-            extras[nm] = {
-                "desc": r["desc"], "GiBps": round(r["gibs_total"], 1),
-                "verify_kernel_GiBps": round(kv["gibs_checksummed"], 1),
-                "verify_roofline_frac": round(kv["frac"], 4),
-                "verify_roofline_frac_kernel_trace": (
-                    round(kv["alg_bytes"] / (ns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if ns else None),
-                "verify_roofline_frac_kernel_trace_timed_steps": (
-                    round(kv["alg_bytes"] / (tns * 1e-9) / 1e9 / HBM_PEAK_GBS, 4) if tns else None),
-                "trailer_kernel_GiBps": round(kt["gibs_checksummed"], 1),
-                "trailer_roofline_frac": round(kt["frac"], 4),
-                "verify_kernel": kv["name"], "trailer_kernel": kt["name"]}
-        extras["C5_wal"] = run_wal(max(3, args.steps // 2), 1)
-        torch.cuda.empty_cache()
-        extras["a15_kv"] = run_kv(args.steps, args.warmup)
-        torch.cuda.empty_cache()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()

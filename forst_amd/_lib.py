@@ -89,6 +89,7 @@ def lib():
         "forst_partition_bytes": (i, [vp, u64, u32, vp]),
         "forst_block_verify_host": (i, [i, vp, u64, vp, vp, vp, vp, vp, vp, vp, u64, vp, i]),
         "forst_block_checksum_host": (i, [i, vp, u64, vp, vp, vp, vp, vp, u64, vp, i]),
+        "forst_wal_verify_host": (i, [vp, u64, u32, vp, vp, vp, vp, vp, i]),
         "forst_host_register": (i, [vp, u64]),
         "forst_host_unregister": (i, [vp]),
         "forst_host_last_error": (ctypes.c_char_p, []),

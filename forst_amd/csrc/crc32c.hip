@@ -1956,6 +1956,9 @@ const char* crc_kernel_name(CrcKernel k, int mode) {
   return kNames[static_cast<int>(k)][mode & 3];
 }
 
+#ifndef FORST_CRC_BLOCK_COST
+#define FORST_CRC_BLOCK_COST 0
+#endif
 template <int M>
 hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipStream_t s) {
   switch (k) {
@@ -1963,7 +1966,11 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
       return launch_kernel(crc32c_block_kernel_simple<M>, grid, kThreads, a, s);
     case CrcKernel::kRows:
       // block modes: the workgroup feed (stream_common.h), no ticket counter
-      if (M != kModeRaw) return launch_kernel(crc32c_rows_kernel<M>, grid, 64 * kWaves, a, s);
+      if (M != kModeRaw) {
+        BlockArgs b = a;
+        b.wg_cost = FORST_CRC_BLOCK_COST;  // (stream_common.h wg_range)
+        return launch_kernel(crc32c_rows_kernel<M>, grid, 64 * kWaves, b, s);
+      }
       if (a.n < uint64_t(64) * grid * kWaves)
         return launch_kernel(crc32c_rows_raw_small_kernel, grid, 64 * kWaves, a, s);
       return launch_fed(crc32c_rows_kernel<M>, grid, kWaves, a, s);

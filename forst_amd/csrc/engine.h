@@ -17,11 +17,30 @@ enum BlockMode : int {
   kModeRaw = 3,      // crc32c::Extend(init, data, len) / XXH3_64bits
 };
 
-// The fragment XXH3 kernel (xxh3.hip xxh3_frag_kernel) loads whole windows
-// of a long record: records whose last byte lies within kFragTail bytes of
-// the log end are hashed from a gathered copy instead (wal_hash.h, and the
-// fused recovery's candidates, wal_recover.hip)
-constexpr uint64_t kFragTail = 1088;
+// The fragment XXH3 kernel (xxh3.hip xxh3_frag_kernel) walks a record in
+// windows of 256 K bytes per 16-lane row and step: lane t holds the K
+// 16-byte chunks at window offsets 16 t + 256 k.  K = FORST_FRAG_K for the
+// XXH3-only kernel (a14 and the recovery's remainder) and FORST_FRAG_CRC_K
+// for the fused recovery kernel, whose E / Z constants (wal_recover.hip
+// rw_cand_kernel) are taken at the same window ends.  A/B on one box
+// (profiles/ab_r05/frag_2k_windows_k8_C5.log): K = 8 took a14 from
+// 9.66-9.83 to 9.48-9.54 ms, but the fused kernel at K = 8 needs 211 VGPRs
+// (2 waves per SIMD) and the recovery went from 18.3 to 20.7 ms.
+#ifndef FORST_FRAG_K
+#define FORST_FRAG_K 8
+#endif
+#ifndef FORST_FRAG_CRC_K
+#define FORST_FRAG_CRC_K 4
+#endif
+constexpr uint32_t kFragKA14 = FORST_FRAG_K, kFragKFused = FORST_FRAG_CRC_K;
+static_assert((kFragKA14 == 4 || kFragKA14 == 8) && (kFragKFused == 4 || kFragKFused == 8),
+              "4 or 8 chunks per lane");
+constexpr uint32_t kFragWinFused = 256 * kFragKFused;
+constexpr uint32_t kFragWinFusedShift = kFragKFused == 8 ? 11 : 10;
+// The kernel loads whole windows of a long record: records whose last byte
+// lies within kFragTail bytes of the log end are hashed from a gathered copy
+// instead (wal_hash.h, and the fused recovery's candidates, wal_recover.hip)
+constexpr uint64_t kFragTail = 256 * (kFragKA14 > kFragKFused ? kFragKA14 : kFragKFused) + 64;
 
 struct BlockArgs {
   const uint8_t* base;
@@ -59,6 +78,10 @@ struct BlockArgs {
   // differs (the caller pre-fills out32 with them), so a clean verify stores
   // nothing from the streaming loop (stores share vmcnt with its loads)
   const uint32_t* expect;
+  // workgroup feed (stream_common.h wg_range): bytes each descriptor weighs
+  // on top of its own in the byte-balanced workgroup ranges (set by the
+  // launcher)
+  uint32_t wg_cost;
 };
 
 struct WalArgs {

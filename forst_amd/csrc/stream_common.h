@@ -119,8 +119,12 @@ __device__ __forceinline__ uint64_t frac_point(uint64_t off0, uint64_t span, uin
 __device__ __forceinline__ void wg_range(const BlockArgs& a, uint32_t lane, uint64_t* lo_out,
                                          uint64_t* hi_out) {
   const uint64_t n = a.n, G = gridDim.x, b = blockIdx.x;
+  // key of descriptor i: offsets[i] + c i -- each block weighs its bytes plus
+  // c bytes for its per-block work (set-up, finish), so a range of small
+  // blocks gets fewer bytes than a range of large ones
+  const uint64_t c = a.wg_cost;
   const uint64_t off0 = a.offsets[0];
-  const uint64_t last = a.offsets[n - 1] + a.sizes[n - 1];
+  const uint64_t last = a.offsets[n - 1] + a.sizes[n - 1] + c * (n - 1);
   if (last <= off0 || G == 1) {  // no byte span to split: by count
     const uint64_t W = (n + G - 1) / G;
     *lo_out = b * W < n ? b * W : n;
@@ -135,7 +139,7 @@ __device__ __forceinline__ void wg_range(const BlockArgs& a, uint32_t lane, uint
     const uint64_t q0 = lo0 + lane * st0, q1 = lo1 + lane * st1;
     const bool v0 = len0 > 64 && lane > 0 && q0 < lo0 + len0;
     const bool v1 = len1 > 64 && lane > 0 && q1 < lo1 + len1;
-    const uint64_t k0 = a.offsets[v0 ? q0 : 0], k1 = a.offsets[v1 ? q1 : 0];
+    const uint64_t k0 = a.offsets[v0 ? q0 : 0] + c * q0, k1 = a.offsets[v1 ? q1 : 0] + c * q1;
     const uint64_t c0 = static_cast<uint64_t>(__popcll(__ballot(v0 && k0 < t0)));
     const uint64_t c1 = static_cast<uint64_t>(__popcll(__ballot(v1 && k1 < t1)));
     if (len0 > 64) {
@@ -150,7 +154,8 @@ __device__ __forceinline__ void wg_range(const BlockArgs& a, uint32_t lane, uint
     }
   }
   const bool f0 = lane < len0, f1 = lane < len1;
-  const uint64_t k0 = a.offsets[f0 ? lo0 + lane : 0], k1 = a.offsets[f1 ? lo1 + lane : 0];
+  const uint64_t k0 = a.offsets[f0 ? lo0 + lane : 0] + c * (lo0 + lane),
+                 k1 = a.offsets[f1 ? lo1 + lane : 0] + c * (lo1 + lane);
   const uint64_t L0 = lo0 + static_cast<uint64_t>(__popcll(__ballot(f0 && k0 < t0)));
   const uint64_t L1 = lo1 + static_cast<uint64_t>(__popcll(__ballot(f1 && k1 < t1)));
   *lo_out = b == 0 ? 0 : uniform64(L0);

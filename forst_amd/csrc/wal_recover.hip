@@ -303,6 +303,14 @@ struct ShiftLds {
     for (uint32_t i = 0; i < r; ++i) v = (v >> 8) ^ g3[v & 0xffu];
     return v;
   }
+  // n <= 2048 (a window of the fragment kernel)
+  __device__ __forceinline__ uint32_t shift_w(uint32_t v, uint32_t n) const {
+    if (n > 1024) {
+      v = shift(v, 1024);
+      n -= 1024;
+    }
+    return shift(v, n);
+  }
   // the CRC state after header[6..hs): the type byte, then (recyclable) the
   // log number -- both known from the walk (the packed word; a non-old
   // recyclable record carries the reader's log number), so no header read
@@ -393,16 +401,18 @@ __device__ __forceinline__ void cand_one(const RecoverArgs& a, uint64_t ni, uint
   c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
   c.first[i] = static_cast<uint32_t>(first);
   c.last[i] = static_cast<uint32_t>(q);
-  // E / Z of every non-empty fragment (xxh3.hip, the fused CRC)
+  // E / Z of every non-empty fragment (xxh3.hip, the fused CRC): E = H moved
+  // from the fragment start to the end of its first window, Z = ~stored moved
+  // from the fragment end to the end of its last window (windows of kFragWinFused)
   uint32_t b = 0;
   for (uint64_t r = first; r <= q; ++r) {
     const uint32_t l = ipack[r] & 0xffffu;
     if (l == 0) continue;  // (an empty trailing fragment: the rows kernel's CRC)
     const uint32_t H = T.header_state((ipack[r] >> 16) & 0xffu, a.log_number, hs);
     const uint32_t e = b + l;
-    const uint32_t ws = b >> 10, we = (e - 1) >> 10;
-    const uint32_t E = T.shift(H, 1024u * (ws + 1) - b);
-    const uint32_t Z = T.shift(~crc_stored[r], 1024u * (we + 1) - e);
+    const uint32_t ws = b >> kFragWinFusedShift, we = (e - 1) >> kFragWinFusedShift;
+    const uint32_t E = T.shift_w(H, kFragWinFused * (ws + 1) - b);
+    const uint32_t Z = T.shift_w(~crc_stored[r], kFragWinFused * (we + 1) - e);
     c.ez[r] = static_cast<uint64_t>(E) | (static_cast<uint64_t>(Z) << 32);
     c.fused[r] = 1;
     b = e;

@@ -42,6 +42,15 @@ constexpr uint32_t kXxWgChunk = FORST_XX_WG_CHUNK;
 #define FORST_XX_STAGE 1
 #endif
 constexpr uint32_t kXxStageW = 16384;
+// bytes a block weighs in the workgroup ranges on top of its own (its
+// set-up and finish): see wg_range.  A/B on one box, 3 alternating runs
+// (profiles/ab_r05/c3s_block_cost_staging.log): C3 sorted by size (C3S)
+// verify 0.758 (0) -> 0.766 (512) / 0.760 (1536) / 0.748 (4096), shuffled
+// C3 0.7665 unchanged -- a range of 4 KiB blocks is slower per byte than one
+// of 64 KiB blocks
+#ifndef FORST_XX_BLOCK_COST
+#define FORST_XX_BLOCK_COST 512
+#endif
 // fused WAL recovery: one CRC chain per lane through its four chunks of a
 // window (1: a 240-byte hop between chunks, J244, so a fragment's finish
 // needs no column merge), or one chain per chunk column (0: the round-3
@@ -73,7 +82,7 @@ constexpr uint32_t kFragThreads = kFragWaves * 64;
 // ... with the fused physical-record CRC (WAL recovery): 124 KiB of CRC
 // tables in LDS, so one 12-wave workgroup per CU
 #ifndef FORST_FRAG_CRC_WAVES
-#define FORST_FRAG_CRC_WAVES 12
+#define FORST_FRAG_CRC_WAVES (FORST_FRAG_CRC_K == 8 ? 8 : 12)
 #endif
 constexpr uint32_t kFragCrcWaves = FORST_FRAG_CRC_WAVES;
 constexpr uint32_t kFragCrcThreads = kFragCrcWaves * 64;
@@ -1058,15 +1067,30 @@ struct FRow {
   __device__ __forceinline__ uint32_t hs() const { return info & 0xffu; }
 };
 
+// the window geometry of K chunks per lane (engine.h)
+template <uint32_t K>
+struct FragGeo {
+  static constexpr uint32_t kWin = 256 * K, kShift = K == 8 ? 11 : 10;
+  static constexpr uint32_t kXB = kWin / 1024;  // XXH3-blocks (1 KiB) per window
+  // FStep::fm bits after m0..m(K-1)
+  static constexpr uint32_t kStr = 2 * K, kKs = kStr + 1, kCut = kKs + 3, kOwn = kCut + 5,
+                            kQuad = kOwn + 2;
+  static_assert(kQuad < 32, "fm bits");
+};
+template <bool CRC>
+constexpr uint32_t frag_k() { return CRC ? kFragKFused : kFragKA14; }
+
+template <uint32_t K>
 struct FStep {
   // chunk k's 16 bytes in x[k][0..3]; x[k][4] (the dword after them, for the
-  // realignment) is loaded for k = 3 only and made in the step for k < 3:
-  // lane t's next dword is lane t+1's first (lane 15: lane 0's next chunk)
-  uint32_t x[4][5];
+  // realignment) is loaded for the last chunk only and made in the step for
+  // the others: lane t's next dword is lane t+1's first (lane 15: lane 0's
+  // next chunk)
+  uint32_t x[K][5];
   uint32_t aux[5];  // the row's last stripe (one quad), or the straddling chunk's own frame
   uint32_t ez[4];  // (fused CRC) E, Z of the window's fragment and of the next one
-  // m0..m3 (2 bits each) | straddle:1 @8 | ks:2 @9 | cut:5 @11 (1..16) |
-  // m_own:2 @16 | last-stripe quad:1 @18 (0: lanes 0-3, 1: lanes 4-7)
+  // m0..m(K-1) (2 bits each) | straddle:1 | ks:3 | cut:5 (1..16) | m_own:2 |
+  // last-stripe quad:1 (0: lanes 0-3, 1: lanes 4-7), at FragGeo's bits
   uint32_t fm;
 };
 
@@ -1078,9 +1102,10 @@ __device__ __forceinline__ void frow_start(FRow& P) {
   P.bn = (hs && l0 < P.size) ? l0 : kNoBound;
 }
 
+template <uint32_t K>
 __device__ __forceinline__ void frow_next(FRow& P) {  // window g -> g + 1
   ++P.g;
-  if (P.bn != kNoBound && 1024u * P.g >= P.bn) {
+  if (P.bn != kNoBound && FragGeo<K>::kWin * P.g >= P.bn) {
     ++P.jc;
     const uint32_t nb = P.bn + (kWalBlock - P.hs());
     P.bn = nb < P.size ? nb : kNoBound;
@@ -1089,12 +1114,14 @@ __device__ __forceinline__ void frow_next(FRow& P) {  // window g -> g + 1
 
 template <bool CRC>
 __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, const FRow& P,
-                                           FStep& d) {
+                                           FStep<frag_k<CRC>()>& d) {
+  constexpr uint32_t kFragK = frag_k<CRC>();
+  using G = FragGeo<kFragK>;
   const uint32_t t = lane & 15, s4 = t >> 2;
   const uint64_t P0 = P.off();
   const bool valid = P.rel != kNoMsg && P0 <= a.base_len;
   const bool lng = valid && P.size > 240;
-  const uint32_t nb = (P.size - 1) >> 10;
+  const uint32_t nb = (P.size - 1) >> G::kShift;
   const uint32_t hs = P.hs();
   const bool shrt = valid && !lng;  // one fragment (wal_hash.h gathers the others)
   // Chunk k of lane t sits at window offset 16 t + 256 k, logical offset
@@ -1103,9 +1130,9 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   // dword-aligned starts differ by dA.  bn >= wpos always (frow_next), so dl
   // (the boundary's offset from the lane's chunk 0) fits in 32 bits.
   const uint32_t lof = 16 * t;
-  const uint32_t wpos = 1024u * P.g;
+  const uint32_t wpos = G::kWin * P.g;
   const uint32_t dw = P.bn - wpos;
-  const int32_t dl = static_cast<int32_t>(dw < 2048u ? dw : 2048u) - static_cast<int32_t>(lof);
+  const int32_t dl = static_cast<int32_t>(dw < 4096u ? dw : 4096u) - static_cast<int32_t>(lof);
   const uint64_t B = P0 + wpos + lof + static_cast<uint64_t>(hs) * P.jc;
   const uint32_t m0 = static_cast<uint32_t>(B) & 3u;
   const uint32_t m1 = (static_cast<uint32_t>(B) + hs) & 3u;
@@ -1132,12 +1159,12 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t rem4 = (valid ? P.size - wpos : 0u) + 4u;
   uint32_t fm = 0;
 #pragma unroll
-  for (uint32_t k = 0; k < 4; ++k) {
+  for (uint32_t k = 0; k < kFragK; ++k) {
     const bool past = lng && dl <= static_cast<int32_t>(256 * k + 16);
     const bool need = CRC || (valid && 16 * t + 256 * k < rem4);
     const uint8_t* pq = (need ? R : a.base) + (past ? dA : 0u) + 256 * k;
     uint32_t mm = past ? m1 : m0;
-    if (k >= 2 && __ballot(shrt)) {
+    if (k >= 2 && k < 4 && __ballot(shrt)) {
       // a short record: its window layout in x[0], x[1] (the fused CRC reads
       // it), its XXH3 chunk (xxh3_short_row) in x[2] and the 16 bytes after
       // that in x[3], whose first dword realigns it (the record ends >=
@@ -1153,7 +1180,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
     d.x[k][1] = v.y;
     d.x[k][2] = v.z;
     d.x[k][3] = v.w;
-    if (k == 3) d.x[3][4] = ld4_a4(pq + 16);
+    if (k == kFragK - 1) d.x[k][4] = ld4_a4(pq + 16);
     fm |= mm << (2 * k);
   }
   // The chunk that straddles the boundary or ends at it (0 < dl - 256 ks <=
@@ -1162,11 +1189,13 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   // front of it takes its realignment dword from this aux, see the step.)
   bool straddle = false;
   uint32_t ks = 0;
-  if (__ballot(lng && dw <= 1024u)) {  // a boundary in, or at the end of, some row's window
+  if (__ballot(lng && dw <= G::kWin)) {  // a boundary in, or at the end of, some row's window
     ks = static_cast<uint32_t>(dl - 1) >> 8;
     const int32_t cut = dl - static_cast<int32_t>(256 * ks);
-    straddle = lng && dl > 0 && dl <= 784 && cut <= 16;
-    if (straddle) fm |= (1u << 8) | (ks << 9) | (static_cast<uint32_t>(cut) << 11) | (m0 << 16);
+    straddle = lng && dl > 0 && dl <= static_cast<int32_t>(256 * (kFragK - 1) + 16) && cut <= 16;
+    if (straddle)
+      fm |= (1u << G::kStr) | (ks << G::kKs) | (static_cast<uint32_t>(cut) << G::kCut) |
+            (m0 << G::kOwn);
   }
   // The last stripe at L - 64, inside the last fragment (fragment j_last):
   // every quad of the row would compute the same merge, so one quad loads
@@ -1178,7 +1207,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   if (__ballot(lastp || straddle)) {
     const uint32_t rowm = static_cast<uint32_t>(__ballot(straddle) >> (lane & 48u)) & 0xffffu;
     const uint32_t ql = (rowm & 0xfu) ? 1u : 0u;
-    if (lastp && ql) fm |= 1u << 18;
+    if (lastp && ql) fm |= 1u << G::kQuad;
     if (straddle) {
       q0 = R + 256 * ks;
       q4 = q0 + 16;
@@ -1265,6 +1294,9 @@ template <int WPE, bool CRC, int DEPTH = 1>
 __global__ void __launch_bounds__(CRC ? kFragCrcThreads : kFragThreads) FORST_WAVES_PER_EU(WPE)
 xxh3_frag_kernel(BlockArgs a) {
   static_assert(DEPTH >= 1 && DEPTH <= 3, "1..3 steps in flight");
+  constexpr uint32_t kFragK = frag_k<CRC>();
+  using G = FragGeo<kFragK>;
+  using FStep = forst::FStep<kFragK>;
   // cold per-pair constants and the accumulate keys live in LDS (registers
   // go to the fragment bookkeeping): key of stripe s, pair p = secret64[s + 2p]
   __shared__ uint64_t cold[4 * kColdN];
@@ -1328,12 +1360,12 @@ xxh3_frag_kernel(BlockArgs a) {
   fetch(row, C);
   auto advance = [&](const FRow& P, FRow& I) {
     const bool lng = P.rel != kNoMsg && P.size > 240;
-    const uint32_t nbP = (P.size - 1) >> 10;
+    const uint32_t nbP = (P.size - 1) >> G::kShift;
     const bool more = lng && P.g < nbP;
     const bool need = P.rel != kNoMsg && !more;
     const uint64_t rows = __ballot(need && t == 0);
     I = P;
-    if (more) frow_next(I);
+    if (more) frow_next<kFragK>(I);
     if (rows) {  // descriptor work only in steps where some row takes a record
       const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
       FRow F;
@@ -1388,6 +1420,7 @@ xxh3_frag_kernel(BlockArgs a) {
 #endif
     const bool valid = C.rel != kNoMsg && C.off() <= a.base_len;
     const bool lng = valid && C.size > 240;
+    // XXH3-blocks: nbC full ones (scrambled), then nbSC stripes of the last
     const uint32_t nbC = (C.size - 1) >> 10, nbSC = ((C.size - 1) & 1023) >> 6;
     if (C.g == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)
       const uint64_t* ci = cold + kColdN * (FR(lane) & 3u);
@@ -1400,7 +1433,7 @@ xxh3_frag_kernel(BlockArgs a) {
     // first, lane 15's is lane 0's in the next chunk (DPP row_ror 15 reads
     // lane t+1 of the row); a short row's chunk 0 is followed by its x[1]
 #pragma unroll
-    for (uint32_t k = 0; k < 3; ++k) {
+    for (uint32_t k = 0; k + 1 < kFragK; ++k) {
       const uint32_t nx = __builtin_amdgcn_mov_dpp(cu.x[k][0], 0x12F, 0xf, 0xf, true);
       const uint32_t nn = __builtin_amdgcn_mov_dpp(cu.x[k + 1][0], 0x12F, 0xf, 0xf, true);
       cu.x[k][4] = t == 15 ? nn : nx;
@@ -1411,26 +1444,26 @@ xxh3_frag_kernel(BlockArgs a) {
     // from the shifted frame (x), merged once, out of line, into that chunk's
     // words (realigned, m := 0), so the chunk loop below carries no
     // per-chunk test.  The lane in front of it realigns with the aux frame.
-    if (__ballot((fm >> 8) & 1u)) {
+    if (__ballot((fm >> G::kStr) & 1u)) {
       uint32_t f2 = fm;
 #ifndef FORST_HOST_EMULATION
       asm volatile("" : "+v"(f2));  // nothing of the merge is hoisted out of the branch
 #endif
-      const uint32_t sk = ((f2 >> 8) & 1u) ? (f2 >> 9) & 3u : 7u;
+      const uint32_t sk = ((f2 >> G::kStr) & 1u) ? (f2 >> G::kKs) & 7u : 31u;
       const uint32_t nsk = __builtin_amdgcn_mov_dpp(sk, 0x12F, 0xf, 0xf, true);
       const uint32_t na0 = __builtin_amdgcn_mov_dpp(cu.aux[0], 0x12F, 0xf, 0xf, true);
 #pragma unroll
-      for (uint32_t k = 0; k < 3; ++k)
+      for (uint32_t k = 0; k + 1 < kFragK; ++k)
         if (nsk == (t == 15 ? k + 1 : k)) cu.x[k][4] = na0;
-      if ((f2 >> 8) & 1u) {
+      if ((f2 >> G::kStr) & 1u) {
         uint64_t a0, a1;
-        xx_words(cu.aux, (f2 >> 16) & 3u, a0, a1);
-        const uint32_t cut = (f2 >> 11) & 31u;  // bytes before the boundary, 1..16
+        xx_words(cu.aux, (f2 >> G::kOwn) & 3u, a0, a1);
+        const uint32_t cut = (f2 >> G::kCut) & 31u;  // bytes before the boundary, 1..16
         const uint64_t mlo = cut >= 8 ? ~0ull : ((1ull << (8 * cut)) - 1);
         const uint64_t mhi = cut >= 16 ? ~0ull : (cut > 8 ? ((1ull << (8 * (cut - 8))) - 1) : 0ull);
-        const uint32_t ks = (f2 >> 9) & 3u;
+        const uint32_t ks = (f2 >> G::kKs) & 7u;
 #pragma unroll
-        for (uint32_t k = 0; k < 4; ++k) {
+        for (uint32_t k = 0; k < kFragK; ++k) {
           if (ks == k) {
             uint64_t d0, d1;
             xx_words(cu.x[k], (f2 >> (2 * k)) & 3u, d0, d1);
@@ -1456,24 +1489,32 @@ xxh3_frag_kernel(BlockArgs a) {
     // (short records: their one fragment from the window layout in x[0], x[1];
     // an empty one is CRC'd by the rows kernel, rw_cand_kernel)
     const bool crow = CRC && valid && C.size > 0;
-    uint32_t hiA = 1024u;
+    uint32_t hiA = G::kWin;
     if (CRC) {
       const uint32_t fe = C.bn < C.size ? C.bn : C.size;
-      const uint32_t W0 = 1024u * C.g;
-      hiA = fe - W0 < 1024u ? fe - W0 : 1024u;
+      const uint32_t W0 = G::kWin * C.g;
+      hiA = fe - W0 < G::kWin ? fe - W0 : G::kWin;
     }
     uint32_t cs[kNC];
 #pragma unroll
     for (uint32_t k = 0; k < kNC; ++k) cs[k] = crc_s[k];
+    uint64_t sumB0 = 0, sumB1 = 0;  // (kFragK = 8) the window's second XXH3-block
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
+    for (uint32_t k = 0; k < kFragK; ++k) {
       uint64_t d0, d1;
       xx_words(cu.x[k], (fm >> (2 * k)) & 3u, d0, d1);
-      const uint64_t c0 = mul32to64(d0 ^ kq[4 * k]) + d1;  // acc[2p] (xxhash.h:4926-4927)
-      const uint64_t c1 = d0 + mul32to64(d1 ^ kq[4 * k + 1]);  // acc[2p+1]
-      const bool use = C.g < nbC || s4 + 4 * k < nbSC;
-      sum0 += use ? c0 : 0ull;
-      sum1 += use ? c1 : 0ull;
+      const uint32_t kk = k & 3u;  // stripe s4 + 4 kk of XXH3-block kFragXB g + k / 4
+      const uint64_t c0 = mul32to64(d0 ^ kq[4 * kk]) + d1;  // acc[2p] (xxhash.h:4926-4927)
+      const uint64_t c1 = d0 + mul32to64(d1 ^ kq[4 * kk + 1]);  // acc[2p+1]
+      const uint32_t xb = G::kXB * C.g + (k >> 2);
+      const bool use = xb < nbC || (xb == nbC && s4 + 4 * kk < nbSC);
+      if (k < 4) {
+        sum0 += use ? c0 : 0ull;
+        sum1 += use ? c1 : 0ull;
+      } else {
+        sumB0 += use ? c0 : 0ull;
+        sumB1 += use ? c1 : 0ull;
+      }
       if (CRC) {
         const uint32_t kc = kNC == 1 ? 0u : k;  // the chain: the lane's one, or column k's
         const uint32_t q = 16 * t + 256 * k;
@@ -1498,12 +1539,12 @@ xxh3_frag_kernel(BlockArgs a) {
       // the fragment's end in this window: finish it (and a fragment that
       // starts here: second pass); else carry the chain, E added at the end
       // of the fragment's first window
-      const uint32_t W0 = 1024u * C.g, L = C.size;
+      const uint32_t W0 = G::kWin * C.g, L = C.size;
       const uint32_t fe = C.bn < L ? C.bn : L;
-      const bool ends = crow && fe - W0 <= 1024u;
+      const bool ends = crow && fe - W0 <= G::kWin;
       const uint32_t l0 = kWalBlock - static_cast<uint32_t>(C.off() & (kWalBlock - 1));
       const uint32_t fs = C.jc == 0 ? 0u : l0 + (C.jc - 1) * (kWalBlock - C.hs());
-      const bool started = (fs >> 10) == C.g;
+      const bool started = (fs >> G::kShift) == C.g;
       const bool carry = crow && !ends;
       uint32_t ns[kNC];
 #pragma unroll
@@ -1527,15 +1568,15 @@ xxh3_frag_kernel(BlockArgs a) {
         // fragment whose row never reaches its end reads as a mismatch)
         if (ends && t == 0) a.crc_ok[static_cast<uint64_t>(C.item) + C.jc] = V == cu.ez[1] ? 1 : 0;
 
-        const bool pb = ends && C.bn < L && C.bn - W0 < 1024u;
+        const bool pb = ends && C.bn < L && C.bn - W0 < G::kWin;
         if (__ballot(pb)) {  // fragment jc + 1 starts in this window: [B, hiB)
           const uint32_t B = C.bn - W0;
-          const uint32_t hiB = L - W0 < 1024u ? L - W0 : 1024u;
+          const uint32_t hiB = L - W0 < G::kWin ? L - W0 : G::kWin;
           uint32_t sb[kNC];
 #pragma unroll
           for (uint32_t k = 0; k < kNC; ++k) sb[k] = 0u;
 #pragma unroll
-          for (uint32_t k = 0; k < 4; ++k) {
+          for (uint32_t k = 0; k < kFragK; ++k) {
             uint64_t d0, d1;
             xx_words(cu.x[k], (fm >> (2 * k)) & 3u, d0, d1);
             const uint32_t q = 16 * t + 256 * k;
@@ -1561,7 +1602,7 @@ xxh3_frag_kernel(BlockArgs a) {
                                      static_cast<uint32_t>(e1 >> 32));
 #endif
           }
-          const bool endsB = pb && L - W0 <= 1024u;
+          const bool endsB = pb && L - W0 <= G::kWin;
           const uint32_t VB = row_value(sb) ^ cu.ez[2];
           if (endsB && t == 0)
             a.crc_ok[static_cast<uint64_t>(C.item) + C.jc + 1] = VB == cu.ez[3] ? 1 : 0;
@@ -1581,11 +1622,24 @@ xxh3_frag_kernel(BlockArgs a) {
     sum1 += row_ror64<8>(sum1);
     acc0 += sum0;
     acc1 += sum1;
-    const bool full = C.g < nbC;
-    if (full) {
+    if (G::kXB * C.g < nbC) {  // a full XXH3-block: scrambled (xxhash.h:5129-5133)
       acc0 = scramble(acc0, kq[16 - s4]);  // keys[16 + 2p] (kq = keys + s4 + 2p)
       acc1 = scramble(acc1, kq[17 - s4]);
     }
+    if (G::kXB == 2) {  // the window's second XXH3-block
+      sumB0 += row_ror64<4>(sumB0);
+      sumB1 += row_ror64<4>(sumB1);
+      sumB0 += row_ror64<8>(sumB0);
+      sumB1 += row_ror64<8>(sumB1);
+      acc0 += sumB0;
+      acc1 += sumB1;
+      if (G::kXB * C.g + 1 < nbC) {
+        acc0 = scramble(acc0, kq[16 - s4]);
+        acc1 = scramble(acc1, kq[17 - s4]);
+      }
+    }
+    // the record's last XXH3-block (nbC) is in this window: finish it
+    const bool full = (nbC >> (G::kShift - 10)) > C.g;
     const bool fin = C.rel != kNoMsg && !(lng && full);
     if (__ballot(fin)) {
       uint64_t h;
@@ -1610,7 +1664,7 @@ xxh3_frag_kernel(BlockArgs a) {
         if (fin && valid && !lng) h = hs2;
       }
       // (the quad that loaded the last stripe: fm bit 18)
-      if (fin && (FR(lane) & 15u) == 4 * ((fm >> 18) & 1u) && a.out64)
+      if (fin && (FR(lane) & 15u) == 4 * ((fm >> G::kQuad) & 1u) && a.out64)
         a.out64[C.rel] = valid ? h : 0ull;
 
     }
@@ -1814,7 +1868,11 @@ hipError_t launch_xxh3_mode(XxKernel k, const BlockArgs& a, hipStream_t s, const
           1, std::min<uint64_t>((a.n + 4 * kRowsWaves - 1) / (4 * kRowsWaves),
                                 uint64_t(di.num_cus) * rows_occupancy<M>())));
       // block modes: the workgroup feed (stream_common.h), no ticket counter
-      if (M != kModeRaw) return launch_kernel(xxh3_rows_kernel<M>, grid, a, s, kRowsThreads);
+      if (M != kModeRaw) {
+        BlockArgs b = a;
+        b.wg_cost = FORST_XX_BLOCK_COST;
+        return launch_kernel(xxh3_rows_kernel<M>, grid, b, s, kRowsThreads);
+      }
       BlockArgs b = a;
       hipError_t e = feed_setup(b, uint64_t(grid) * kRowsWaves, s);
       if (e != hipSuccess) return e;
@@ -1895,7 +1953,7 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 // 164 VGPRs, no spills (round 4); A/B against 2 waves (8-wave workgroups):
 // 2 waves ran the kernel 5 % slower
 #ifndef FORST_FRAG_CRC_WPE
-#define FORST_FRAG_CRC_WPE 3
+#define FORST_FRAG_CRC_WPE (FORST_FRAG_CRC_K == 8 ? 2 : 3)
 #endif
 #ifndef FORST_FRAG_CRC_DEPTH
 #define FORST_FRAG_CRC_DEPTH 1

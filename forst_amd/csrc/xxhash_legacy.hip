@@ -230,6 +230,283 @@ __global__ void __launch_bounds__(kThreads) xxhash_legacy_kernel(BlockArgs a) {
   }
 }
 
+// ---- one message per lane (round 5) ------------------------------------------
+// The group kernel above gives each accumulator its own lane: every chain
+// step waits for a 4/8-byte load of its own, and the 16 messages of a wave
+// cover 16 x 16 bytes per load instruction -- 0.21 (XXH32) / 0.31 (XXH64) of
+// the HBM peak on 1 M x 16 KiB (bench round 5).  Here one LANE hashes one
+// message with its four accumulators in registers (four independent chains),
+// reading 64 bytes per step with four 16-byte loads and one realignment
+// dword; a wave works on 64 messages, and a lane that is done takes the next
+// message of the wave's batch at once, so no lane waits for the wave's
+// longest message (batches of 64 descriptors: the first static, the rest
+// claimed from a ticket).  The last <= 68 bytes (the stripes the 64-byte
+// steps leave, the tail and the virtual type byte of compute mode) are
+// copied into the lane's LDS slot with independent loads and finished there.
+constexpr uint32_t kLWaves = 4;
+constexpr uint32_t kLThreads = kLWaves * 64;
+constexpr uint32_t kLSlot = 80;  // LDS bytes per lane (20 KiB per workgroup)
+
+// little-endian word at byte o of a lane's slot (o + 8 <= kLSlot)
+__device__ __forceinline__ uint32_t slot32(const uint8_t* sl, uint32_t o) {
+  const uint32_t* w = reinterpret_cast<const uint32_t*>(sl + (o & ~3u));
+  return __builtin_amdgcn_alignbyte(w[1], w[0], o & 3u);
+}
+__device__ __forceinline__ uint64_t slot64(const uint8_t* sl, uint32_t o) {
+  return static_cast<uint64_t>(slot32(sl, o)) | (static_cast<uint64_t>(slot32(sl, o + 4)) << 32);
+}
+
+template <int MODE, bool X64>
+__global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
+  __shared__ uint32_t slots[kLThreads * kLSlot / 4];
+  constexpr uint32_t S = X64 ? 32 : 16;  // stripe bytes
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  uint8_t* sl = reinterpret_cast<uint8_t*>(slots) + threadIdx.x * kLSlot;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kLWaves;
+  const uint64_t gw = static_cast<uint64_t>(blockIdx.x) * kLWaves + wave;
+  // the wave's batch [bcur, bend) of descriptors not yet taken by a lane
+  uint64_t bcur = gw * 64 < a.n ? gw * 64 : a.n;
+  uint64_t bend = bcur + 64 < a.n ? bcur + 64 : a.n;
+  bool more = bcur < a.n;  // (wave-uniform) batches may remain
+  // per lane: its message
+  bool have = false;
+  uint64_t i = 0, off = 0;
+  const uint8_t* pa = a.base;
+  uint32_t m = 0, nmem = 0, nv = 0, vb = 0, pos = 0, vend = 0, size = 0, stored = 0, mod = 0;
+  bool valid = false;
+  uint64_t v0 = 0, v1 = 0, v2 = 0, v3 = 0;
+  for (;;) {
+    // ---- lanes without a message take the next ones of the batch
+    uint64_t need = __ballot(!have);
+    while (need && more) {
+      const uint32_t rank = static_cast<uint32_t>(__popcll(need & ((1ull << lane) - 1)));
+      const uint64_t avail = bend - bcur;
+      if (!have && rank < avail) {
+        i = bcur + rank;
+        have = true;
+        off = a.offsets[i];
+        size = a.sizes[i];
+        uint64_t nd = size;
+        if (MODE == kModeVerify || MODE == kModeTrailer) nd += 5;
+        if (MODE == kModeCompute && a.last_bytes == nullptr) nd += 1;
+        valid = off <= a.base_len && nd <= a.base_len - off;
+        mod = valid && a.modifiers ? a.modifiers[i] : 0u;
+        const uint8_t* p = a.base + (valid ? off : 0);
+        m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3u);
+        pa = p - m;
+        nv = 0;
+        vb = 0;
+        stored = 0;
+        if (!valid) {
+          nmem = 0;
+        } else if (MODE == kModeVerify) {
+          nmem = size + 1;  // ComputeBuiltinChecksum(type, data, size+1)
+          stored = ldu32(p + size + 1);
+        } else if (MODE == kModeRaw) {
+          nmem = size;
+        } else {
+          nmem = size;
+          nv = 1;
+          vb = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
+        }
+        // 64-byte steps whose aligned window [pa + pos, +68) lies in the
+        // message's own bytes
+        vend = nmem + m >= 68 ? ((nmem + m - 4) & ~63u) : 0u;
+        pos = 0;
+        if (X64) {
+          v0 = Q64_1 + Q64_2;
+          v1 = Q64_2;
+          v2 = 0;
+          v3 = 0 - Q64_1;
+        } else {
+          v0 = static_cast<uint32_t>(Q32_1 + Q32_2);
+          v1 = Q32_2;
+          v2 = 0;
+          v3 = static_cast<uint32_t>(0u - Q32_1);
+        }
+      }
+      const uint64_t took = static_cast<uint64_t>(__popcll(need)) < avail
+                                ? static_cast<uint64_t>(__popcll(need)) : avail;
+      bcur += took;
+      need = __ballot(!have);
+      if (bcur >= bend) {  // the batch is used up: claim the next one
+        uint64_t nb = 0;
+        if (lane == 0) nb = nw + atomicAdd(a.ticket, 1ull);
+        nb = uniform64(nb) * 64;
+        if (nb >= a.n) {
+          more = false;
+        } else {
+          bcur = nb;
+          bend = nb + 64 < a.n ? nb + 64 : a.n;
+        }
+      }
+    }
+    if (!__ballot(have)) break;
+    // ---- one 64-byte step of every lane that has one left
+    const bool vec = have && pos < vend;
+    if (__ballot(vec)) {
+      const uint8_t* q = (vec ? pa + pos : a.base) + vzero();
+      uint32_t d[17];
+#pragma unroll
+      for (int k = 0; k < 4; ++k) {
+        const u32x4a4 x = ld16_a4(q + 16 * k);
+        d[4 * k] = x.x;
+        d[4 * k + 1] = x.y;
+        d[4 * k + 2] = x.z;
+        d[4 * k + 3] = x.w;
+      }
+      d[16] = ld4_a4(q + 64);
+      if (vec) {
+        uint32_t w[16];
+#pragma unroll
+        for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], m);
+        if (X64) {
+#pragma unroll
+          for (int st = 0; st < 2; ++st) {
+            const uint32_t* x = w + 8 * st;
+            v0 = r64(v0, static_cast<uint64_t>(x[0]) | (static_cast<uint64_t>(x[1]) << 32));
+            v1 = r64(v1, static_cast<uint64_t>(x[2]) | (static_cast<uint64_t>(x[3]) << 32));
+            v2 = r64(v2, static_cast<uint64_t>(x[4]) | (static_cast<uint64_t>(x[5]) << 32));
+            v3 = r64(v3, static_cast<uint64_t>(x[6]) | (static_cast<uint64_t>(x[7]) << 32));
+          }
+        } else {
+#pragma unroll
+          for (int st = 0; st < 4; ++st) {
+            v0 = r32(static_cast<uint32_t>(v0), w[4 * st]);
+            v1 = r32(static_cast<uint32_t>(v1), w[4 * st + 1]);
+            v2 = r32(static_cast<uint32_t>(v2), w[4 * st + 2]);
+            v3 = r32(static_cast<uint32_t>(v3), w[4 * st + 3]);
+          }
+        }
+        pos += 64;
+      }
+    }
+    // ---- lanes whose steps are done: the rest from the LDS slot, then store
+    const bool fin = have && pos >= vend;
+    if (!__ballot(fin)) continue;
+    if (fin) {
+      // bytes [vend, nmem) as the dword-aligned words from pa + vend (at slot
+      // byte m + x for message byte vend + x); words past the message are 0
+      const uint32_t span = m + (nmem - vend);  // <= 70
+      const uint8_t* q = pa + vend;
+      uint32_t t[18];
+#pragma unroll
+      for (int k = 0; k < 18; ++k) t[k] = 4u * k < span ? ld4_a4(q + 4 * k + vzero()) : 0u;
+      uint32_t* sw = reinterpret_cast<uint32_t*>(sl);
+#pragma unroll
+      for (int k = 0; k < 18; ++k) sw[k] = t[k];
+      sw[18] = 0u;
+      sw[19] = 0u;
+      if (nv) sl[span] = static_cast<uint8_t>(vb);
+    }
+    if (fin) {
+      const uint32_t total = nmem + nv;
+      const uint32_t nst = total / S;  // stripes of the whole message
+      uint32_t o = vend;               // message offset; slot byte m + (o - vend)
+      auto w32 = [&](uint32_t at) { return slot32(sl, m + (at - vend)); };
+      auto w64 = [&](uint32_t at) { return slot64(sl, m + (at - vend)); };
+      for (; o + S <= nst * S; o += S) {  // the stripes after the 64-byte steps
+        if (X64) {
+          v0 = r64(v0, w64(o));
+          v1 = r64(v1, w64(o + 8));
+          v2 = r64(v2, w64(o + 16));
+          v3 = r64(v3, w64(o + 24));
+        } else {
+          v0 = r32(static_cast<uint32_t>(v0), w32(o));
+          v1 = r32(static_cast<uint32_t>(v1), w32(o + 4));
+          v2 = r32(static_cast<uint32_t>(v2), w32(o + 8));
+          v3 = r32(static_cast<uint32_t>(v3), w32(o + 12));
+        }
+      }
+      uint32_t h;
+      if (X64) {  // XXH64_finalize (util/xxhash.h ~:2750-2990)
+        uint64_t hh;
+        if (total >= 32) {
+          hh = rotl64(v0, 1) + rotl64(v1, 7) + rotl64(v2, 12) + rotl64(v3, 18);
+          hh = (hh ^ r64(0, v0)) * Q64_1 + Q64_4;
+          hh = (hh ^ r64(0, v1)) * Q64_1 + Q64_4;
+          hh = (hh ^ r64(0, v2)) * Q64_1 + Q64_4;
+          hh = (hh ^ r64(0, v3)) * Q64_1 + Q64_4;
+        } else {
+          hh = Q64_5;
+        }
+        hh += total;
+        for (; total - o >= 8; o += 8) {
+          hh ^= r64(0, w64(o));
+          hh = rotl64(hh, 27) * Q64_1 + Q64_4;
+        }
+        if (total - o >= 4) {
+          hh ^= static_cast<uint64_t>(w32(o)) * Q64_1;
+          hh = rotl64(hh, 23) * Q64_2 + Q64_3;
+          o += 4;
+        }
+        for (; o < total; ++o) {
+          hh ^= (w32(o) & 0xffu) * Q64_5;
+          hh = rotl64(hh, 11) * Q64_1;
+        }
+        hh ^= hh >> 33;
+        hh *= Q64_2;
+        hh ^= hh >> 29;
+        hh *= Q64_3;
+        hh ^= hh >> 32;
+        h = static_cast<uint32_t>(hh);  // Lower32of64 (format.cc:576)
+      } else {  // XXH32_finalize
+        if (total >= 16) {
+          h = rotl32(static_cast<uint32_t>(v0), 1) + rotl32(static_cast<uint32_t>(v1), 7) +
+              rotl32(static_cast<uint32_t>(v2), 12) + rotl32(static_cast<uint32_t>(v3), 18);
+        } else {
+          h = Q32_5;
+        }
+        h += total;
+        for (; total - o >= 4; o += 4) {
+          h += w32(o) * Q32_3;
+          h = rotl32(h, 17) * Q32_4;
+        }
+        for (; o < total; ++o) {
+          h += (w32(o) & 0xffu) * Q32_5;
+          h = rotl32(h, 11) * Q32_1;
+        }
+        h ^= h >> 15;
+        h *= Q32_2;
+        h ^= h >> 13;
+        h *= Q32_3;
+        h ^= h >> 16;
+      }
+      if (!valid) {
+        if (a.out32) a.out32[i] = 0;
+        if (MODE == kModeVerify) {
+          if (a.ok_out) a.ok_out[i] = 0;
+          if (a.stored_out) a.stored_out[i] = 0;
+          if (a.mismatches) atomicAdd(a.mismatches, 1ull);
+        }
+      } else if (MODE == kModeRaw) {
+        a.out32[i] = h;
+      } else if (MODE == kModeVerify) {
+        const uint32_t st = stored - mod;
+        const bool ok = st == h;
+        if (a.out32) a.out32[i] = h;
+        if (a.stored_out) a.stored_out[i] = st;
+        if (a.ok_out) a.ok_out[i] = ok ? 1 : 0;
+        if (!ok && a.mismatches) atomicAdd(a.mismatches, 1ull);
+      } else {
+        const uint32_t c = h + mod;
+        if (a.out32) a.out32[i] = c;
+        if (MODE == kModeTrailer) {
+          uint8_t* wp = a.base_w + off + size;
+          wp[0] = static_cast<uint8_t>(vb);
+          stu32_bytes(wp + 1, c);
+        }
+      }
+      have = false;
+    }
+  }
+}
+
+#ifndef FORST_LEGACY_LANE
+#define FORST_LEGACY_LANE 1
+#endif
+
 template <bool X64>
 hipError_t launch_mode(int mode, const BlockArgs& a, hipStream_t stream, uint32_t grid,
                        const char** name) {
@@ -260,10 +537,57 @@ hipError_t launch_mode(int mode, const BlockArgs& a, hipStream_t stream, uint32_
 
 }  // namespace
 
+template <bool X64>
+hipError_t launch_lane(int mode, const BlockArgs& a, hipStream_t stream, const char** name) {
+  const DeviceInfo& di = device_info();
+  const uint64_t batches = (a.n + 63) / 64;
+  const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
+      1, std::min<uint64_t>((batches + kLWaves - 1) / kLWaves, uint64_t(di.num_cus) * 8)));
+  // (8 workgroups of 4 waves per CU: 160 KiB of slots)
+  BlockArgs b = a;
+  void* t = nullptr;
+  hipError_t e = scratch_alloc(&t, 256, stream);
+  if (e != hipSuccess) return e;
+  if ((e = hipMemsetAsync(t, 0, 8, stream)) != hipSuccess) {
+    (void)scratch_free(t, stream);
+    return e;
+  }
+  b.ticket = static_cast<unsigned long long*>(t);
+  switch (mode) {
+    case kModeCompute:
+      *name = X64 ? "xxhash64_lane_kernel<compute>" : "xxhash32_lane_kernel<compute>";
+      hipLaunchKernelGGL((xxhash_lane_kernel<kModeCompute, X64>), dim3(grid), dim3(kLThreads), 0,
+                         stream, b);
+      break;
+    case kModeTrailer:
+      *name = X64 ? "xxhash64_lane_kernel<trailer>" : "xxhash32_lane_kernel<trailer>";
+      hipLaunchKernelGGL((xxhash_lane_kernel<kModeTrailer, X64>), dim3(grid), dim3(kLThreads), 0,
+                         stream, b);
+      break;
+    case kModeVerify:
+      *name = X64 ? "xxhash64_lane_kernel<verify>" : "xxhash32_lane_kernel<verify>";
+      hipLaunchKernelGGL((xxhash_lane_kernel<kModeVerify, X64>), dim3(grid), dim3(kLThreads), 0,
+                         stream, b);
+      break;
+    default:
+      *name = X64 ? "xxhash64_lane_kernel<raw>" : "xxhash32_lane_kernel<raw>";
+      hipLaunchKernelGGL((xxhash_lane_kernel<kModeRaw, X64>), dim3(grid), dim3(kLThreads), 0,
+                         stream, b);
+      break;
+  }
+  e = hipGetLastError();
+  const hipError_t f = scratch_free(t, stream);
+  return e != hipSuccess ? e : f;
+}
+
 hipError_t launch_xxhash_legacy_blocks(bool x64, int mode, const BlockArgs& a,
                                        hipStream_t stream, const char** name) {
   const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
+  // (the lane kernel's realignment loads read the 4 bytes in front of an
+  // unaligned block start: buffers shorter than 4 KiB keep the group kernel)
+  if (FORST_LEGACY_LANE && a.base_len >= 4096)
+    return x64 ? launch_lane<true>(mode, a, stream, name) : launch_lane<false>(mode, a, stream, name);
   const uint64_t per_wg = uint64_t(kWaves) * kMsgsPerWave;
   const uint32_t grid = static_cast<uint32_t>(
       std::max<uint64_t>(1, std::min<uint64_t>((a.n + per_wg - 1) / per_wg,

@@ -81,6 +81,23 @@ def block_checksum_host(ctype, base, offsets, sizes, last_bytes=None, modifiers=
     return out
 
 
+def wal_verify_host(log, log_number=0, devices=(0,)):
+    """forst_wal_verify_batch over a log in host memory (numpy uint8 array or a
+    MappedFile), its log blocks split over `devices`: per 32 KiB log block
+    (status, verified records, failing offset) and the failing-block count
+    (db/log_reader.cc:450-531)."""
+    bp, blen = _base_ptr(log)
+    nb = (blen + 32767) // 32768
+    st = np.zeros(nb, np.uint8)
+    nr = np.zeros(nb, np.uint32)
+    fo = np.zeros(nb, np.uint32)
+    bad = ctypes.c_uint64()
+    dev = _arr(devices, np.int32)
+    _check(lib().forst_wal_verify_host(bp, blen, log_number, _ptr(st), _ptr(nr), _ptr(fo),
+                                       ctypes.byref(bad), _ptr(dev), len(dev)))
+    return st, nr, fo, bad.value
+
+
 class MappedFile:
     """A read-only mmap of a file (as PosixMmapReadableFile, env/io_posix.cc:958),
     optionally hipHostRegister'd so the host-memory calls read it by DMA."""

@@ -414,6 +414,17 @@ int forst_block_checksum_host(int checksum_type, const uint8_t* host_base, uint6
                               const uint64_t* offsets, const uint32_t* sizes,
                               const uint8_t* last_bytes, const uint32_t* modifiers, uint32_t* out,
                               uint64_t n_blocks, const int* devices, int n_devices);
+/* forst_wal_verify_batch over a log in host memory (the reader's file
+ * buffer, or a forst_host_register'ed mmap of the log file), spread over
+ * several devices: the log blocks split into equal contiguous ranges, one per
+ * device, each streamed through that device's host context in 64 MiB windows
+ * (db/log_reader.cc:450-531 checks every 32 KiB log block on its own,
+ * log_writer.cc:86-102).  Host outputs (each may be NULL), one entry per log
+ * block as forst_wal_verify_batch gives them; *bad_blocks = blocks with a
+ * failing status other than FORST_WAL_ZERO_RECORD. */
+int forst_wal_verify_host(const uint8_t* host_log, uint64_t log_len, uint32_t log_number,
+                          uint8_t* status_out, uint32_t* nrec_out, uint32_t* fail_off_out,
+                          uint64_t* bad_blocks, const int* devices, int n_devices);
 /* hipHostRegister / hipHostUnregister of a host range (e.g. an mmap'd SST
  * file) so the host-memory calls read it by DMA without staging.  A batch is
  * DMA'd in place only when ONE registration (or one pinned allocation) covers

@@ -216,3 +216,43 @@ def test_trim_keeps_the_callers_device():
     torch.cuda.set_device(0)
     hostpath.context_trim()
     assert torch.cuda.current_device() == 0
+
+
+@pytest.mark.parametrize("devices", [(0,), (0, 0), (0, 0, 0)])
+def test_wal_verify_host_matches_device_call(devices):
+    """a WAL log in host memory (pageable, then a registered mmap of the log
+    file) verified over a device list -- one context per entry, equal
+    contiguous log-block ranges, 64 MiB windows -- gives per block exactly the
+    device-resident forst_wal_verify_batch's status / records / offset, with
+    flips in every range detected (db/log_reader.cc:450-531)"""
+    import tempfile
+
+    w = workload.make_wal_batch(60000, workload.SEEDS["C5"] + 1)  # ~260 MiB: several windows
+    rng = np.random.default_rng(31)
+    cand = np.nonzero(w.rec_lengths > 0)[0]
+    victims = rng.choice(cand, 9, replace=False)
+    pos = w.rec_offsets[victims].astype(np.int64) + 7 + \
+        rng.integers(0, w.rec_lengths[victims].astype(np.int64))
+    w.log[torch.from_numpy(pos).cuda()] ^= 0x04
+    st, nr, fo, bad = engine.wal_verify_batch(w.log)
+    want = (st.cpu().numpy(), nr.cpu().numpy(), fo.cpu().numpy(), int(bad.item()))
+    assert want[3] == len(set((w.rec_offsets[victims] // 32768).tolist()))
+    logh = w.log.cpu().numpy()
+    got = hostpath.wal_verify_host(logh, 0, devices)
+    for g, x in zip(got[:3], want[:3]):
+        assert np.array_equal(g, x)
+    assert got[3] == want[3]
+    d = tempfile.mkdtemp()
+    path = d + "/000007.log"
+    logh.tofile(path)
+    m = hostpath.MappedFile(path, register=True)
+    try:
+        got = hostpath.wal_verify_host(m, 0, devices)
+        for g, x in zip(got[:3], want[:3]):
+            assert np.array_equal(g, x)
+        assert got[3] == want[3]
+    finally:
+        m.close()
+        import os
+        os.unlink(path)
+        os.rmdir(d)

@@ -269,6 +269,61 @@ def run_wal(steps, warmup, n_records=10_000_000):
     return out
 
 
+def run_wal_sharded(steps, warmup, rank, world, n_per_gpu=10_000_000):
+    """C5 at N GPUs: ONE WAL of N x 10 M records (weak
+    scaling) whose 32 KiB log blocks are split into N equal contiguous ranges,
+    rank r verifying range r (forst_wal_verify_batch; db/log_reader.cc:450-531
+    checks each log block on its own, physical records never straddle one,
+    log_writer.cc:86-102).  No collective on the data path: barrier +
+    synchronize around the timed steps, max over ranks; value = the whole
+    log's bytes / that time."""
+    from forst_amd import engine, workload
+
+    lengths = workload.log_uniform_lengths(n_per_gpu * world, 32, 32768, workload.SEEDS["C5"])
+    _, _, _, _, _, total = workload.wal_layout(lengths)
+    nb = (total + 32767) // 32768
+    b0, b1 = nb * rank // world, nb * (rank + 1) // world
+    w = workload.make_wal_batch(0, workload.SEEDS["C5"], lengths=lengths, block_range=(b0, b1))
+    del lengths
+    n = b1 - b0
+    st = torch.empty(n, dtype=torch.uint8, device="cuda")
+    nrec = torch.empty(n, dtype=torch.uint32, device="cuda")
+    fail = torch.empty(n, dtype=torch.uint32, device="cuda")
+    bad = torch.zeros(1, dtype=torch.int64, device="cuda")
+    L = engine.lib()
+    s0 = engine._stream(None)
+
+    def verify():
+        engine.check(L.forst_wal_verify_batch(w.log.data_ptr(), w.total, 0, n, 0, st.data_ptr(),
+                                              nrec.data_ptr(), fail.data_ptr(), bad.data_ptr(), s0))
+
+    for _ in range(max(1, warmup)):
+        verify()
+    torch.cuda.synchronize()
+    bad.zero_()
+    shard.barrier(world)
+    torch.cuda.synchronize()
+    t0 = time.perf_counter()
+    for _ in range(steps):
+        verify()
+    torch.cuda.synchronize()
+    t1 = time.perf_counter()
+    shard.barrier(world)
+    elapsed = shard.max_over_ranks(t1 - t0, world)
+    assert shard.sum_over_ranks(int(bad.item()), world) == 0, "WAL blocks failed verification"
+    assert shard.sum_over_ranks(int(nrec.sum().item()), world) == \
+        shard.sum_over_ranks(len(w.rec_offsets), world)
+    out = {"desc": f"one WAL of {n_per_gpu * world} records log-uniform 32..32768 B "
+                   f"({total / GIB:.1f} GiB), its log blocks in {world} equal contiguous ranges, "
+                   "one per GPU, forst_wal_verify_batch",
+           "GiBps": round(total * steps / elapsed / GIB, 1),
+           "ms_per_step": round(elapsed / steps * 1e3, 3),
+           "roofline_frac_per_gpu": round((total + 9 * nb) * steps / elapsed / 1e9 /
+                                          HBM_PEAK_GBS / world, 4)}
+    del w
+    return out
+
+
 def run_kv(steps, warmup, n=1 << 20):
     """a15 per-KV protection (db/kv_checksum.h:296 ProtectKVO + ProtectS, the
     WriteBatch / memtable shape; MemTable::VerifyEntryChecksum memtable.cc:273
@@ -760,6 +815,10 @@ def main():
             extras["host_memory_verify_error"] = str(e)
     del b
     torch.cuda.empty_cache()
+    if world > 1 and not args.no_extras:
+        # (no try: every rank takes part in its barriers; a failure ends the run)
+        extras["C5_wal_verify_sharded"] = run_wal_sharded(max(3, args.steps // 2), 1, rank, world)
+        torch.cuda.empty_cache()
     if rank != 0:
         if world > 1:
             dist.destroy_process_group()
@@ -785,7 +844,7 @@ def main():
         "config": {"workload": f"{args.config}: {main_res['desc']}",
                    "blocks_per_gpu": main_res["n"],
                    "blocks_total": main_res["n_total"],
-                   "checksum": {1: "kCRC32c", 4: "kXXH3"}[main_res["ctype"]],
+                   "checksum": {1: "kCRC32c", 2: "kxxHash", 3: "kxxHash64", 4: "kXXH3"}[main_res["ctype"]],
                    "step": "trailer pass (write side) + verify pass (read side)",
                    "parallelism": f"byte-balanced block shards of one batch x{world}, "
                                   "no data-path collective"},

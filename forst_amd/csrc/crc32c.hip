@@ -1340,6 +1340,11 @@ __device__ __forceinline__ void crow_issue(const BlockArgs& a, uint32_t lane, co
     s0 = s0 < 0 ? 0 : s0;
     s1 = s1 < 0 ? 0 : s1;
   }
+  // (Loading the round-0 segments in front of a raw record's head from the
+  // buffer's first KiB instead, to save their HBM bytes -- 1.07x the log on
+  // C5 -- measured no faster: C5 verify 0.604-0.608 vs 0.606-0.609,
+  // profiles/ab_r05/raw_pre_head_redirect_C5.log.  They are mostly the
+  // previous record's bytes, which its own row reads at about the same time.)
 #pragma unroll
   for (uint32_t c = 0; c < 2; ++c) {
     const uint8_t* sp = a.base + (c ? s1 : s0);

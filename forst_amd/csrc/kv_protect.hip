@@ -187,6 +187,69 @@ __device__ uint64_t wave_xxph3_long(const uint8_t* p, uint32_t len, uint64_t see
   return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
 }
 
+// The same on one 16-lane row (t = lane & 15), four fields per wave at once
+// (round 5): lane t takes the 16-byte chunks at 16 t + 256 k of each 1 KiB
+// block (stripe t/4 + 4k, accumulator pair t%4), and the last stripe's load
+// is issued with them, so a field under 1 KiB (a value of 240..1000 bytes,
+// the memtable shape) costs one round trip to memory instead of two, and
+// four of them overlap.  Every lane of the row returns the hash.
+__device__ uint64_t row_xxph3_long(const uint8_t* p, uint32_t len, uint64_t seed, uint32_t t) {
+  const uint32_t s4 = t >> 2, pp = t & 3;
+  uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;
+  uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
+  const uint32_t nb = len / 1024;
+  const uint32_t nbS = (len - 1024 * nb) / 64;
+  const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3);
+  const uint8_t* q = p - m + 16 * t;
+  const uint64_t ks0 = psec64(128 + 16 * pp, seed), ks1 = psec64(136 + 16 * pp, seed);
+  // the last stripe (xxph3.h:1539-1542), loaded up front
+  uint64_t l0 = 0, l1 = 0;
+  {
+    const uint8_t* lp = p + len - 64 + 16 * pp;
+    const uint32_t ml = static_cast<uint32_t>(reinterpret_cast<uint64_t>(lp) & 3);
+    ld16u(lp - ml, ml, l0, l1);
+  }
+  // (rows of one wave may have different block counts: the loop runs to the
+  // wave's largest, wave-uniform around the row sums)
+  for (uint32_t g = 0; __ballot(g <= nb); ++g) {
+    uint64_t c0 = 0, c1 = 0;
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) {
+      const uint32_t st = s4 + 4 * k;
+      if (g < nb || (g == nb && st < nbS)) {
+        uint64_t d0, d1;
+        ld16u(q + 1024 * g + 256 * k, m, d0, d1);
+        c0 += d0 + mul32to64(d0 ^ psec64(8 * st + 16 * pp, seed));  // acc_64bits
+        c1 += d1 + mul32to64(d1 ^ psec64(8 * st + 16 * pp + 8, seed));
+      }
+    }
+    c0 += row_ror64<4>(c0);
+    c1 += row_ror64<4>(c1);
+    c0 += row_ror64<8>(c0);
+    c1 += row_ror64<8>(c1);
+    if (g <= nb) {
+      acc0 += c0;
+      acc1 += c1;
+    }
+    if (g < nb) {
+      acc0 = scramble_acc(acc0, ks0);
+      acc1 = scramble_acc(acc1, ks1);
+    }
+  }
+  if (len & 63) {
+    acc0 += l0 + mul32to64(l0 ^ psec64(121 + 16 * pp, seed));
+    acc1 += l1 + mul32to64(l1 ^ psec64(129 + 16 * pp, seed));
+  }
+  uint64_t h = mul128_fold64(acc0 ^ psec64(11 + 16 * pp, seed), acc1 ^ psec64(19 + 16 * pp, seed));
+  h += quad_xor64<1>(h);
+  h += quad_xor64<2>(h);
+  return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + h);
+}
+
+#ifndef FORST_KV_ROWS
+#define FORST_KV_ROWS 1
+#endif
+
 __device__ __forceinline__ bool in_range(uint64_t off, uint64_t len, uint64_t base_len) {
   return off <= base_len && len <= base_len - off;
 }
@@ -234,8 +297,59 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
         h ^= xxph3_4to8(cf | (cf << 32), 4, kSeedC);
       }
     }
+    if (FORST_KV_ROWS) {
+      // fields > 240 bytes: four at a time, one per 16-lane row (keys first)
+      uint64_t lk = __ballot(valid && kl > 240);
+      uint64_t lv = MODE != kKvHash ? __ballot(valid && vl > 240) : 0ull;
+      const uint32_t row = lane >> 4, t = lane & 15;
+      while (lk | lv) {
+        uint32_t src = 64, isv = 0;
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+          uint32_t sr = 64, vr = 0;
+          if (lk) {
+            sr = static_cast<uint32_t>(__builtin_ctzll(lk));
+            lk &= lk - 1;
+          } else if (lv) {
+            sr = static_cast<uint32_t>(__builtin_ctzll(lv));
+            lv &= lv - 1;
+            vr = 1;
+          }
+          if (row == r) {
+            src = sr;
+            isv = vr;
+          }
+        }
+        const uint32_t sl = src < 64 ? src : 0;
+        // (the source lane's key and value fields, the row picks one)
+        const uint32_t klo = __shfl(static_cast<uint32_t>(ko), sl);
+        const uint32_t khi = __shfl(static_cast<uint32_t>(ko >> 32), sl);
+        const uint32_t kln = __shfl(kl, sl);
+        uint32_t vlo = 0, vhi = 0, vln = 0;
+        if (MODE != kKvHash) {
+          vlo = __shfl(static_cast<uint32_t>(vo), sl);
+          vhi = __shfl(static_cast<uint32_t>(vo >> 32), sl);
+          vln = __shfl(vl, sl);
+        }
+        const uint32_t flo = isv ? vlo : klo, fhi = isv ? vhi : khi, fl = isv ? vln : kln;
+        const uint32_t slo = __shfl(static_cast<uint32_t>(kseed), sl);
+        const uint32_t shi = __shfl(static_cast<uint32_t>(kseed >> 32), sl);
+        const uint64_t o = src < 64 ? (static_cast<uint64_t>(fhi) << 32) | flo : 0ull;
+        const uint64_t sd = isv ? kSeedV : (static_cast<uint64_t>(shi) << 32) | slo;
+        // (a row without a field hashes the buffer's first 241 bytes, discarded: a
+        // long field exists, so base_len > 240)
+        const uint64_t hv = row_xxph3_long(a.base + o, src < 64 ? fl : 241u, sd, t);
+#pragma unroll
+        for (uint32_t r = 0; r < 4; ++r) {
+          const uint32_t sr = readlane32(src, 16 * r);
+          const uint64_t vr = readlane64(static_cast<uint32_t>(hv), static_cast<uint32_t>(hv >> 32),
+                                         16 * r);
+          if (lane == sr) h ^= vr;
+        }
+      }
+    }
     // fields > 240 bytes: the whole wave hashes them one after the other
-    uint64_t lk = __ballot(valid && kl > 240);
+    uint64_t lk = FORST_KV_ROWS ? 0ull : __ballot(valid && kl > 240);
     while (lk) {
       const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lk));
       lk &= lk - 1;
@@ -245,7 +359,7 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       const uint64_t hv = wave_xxph3_long(a.base + o, n, sd, lane);
       h ^= lane == l ? hv : 0ull;
     }
-    if (MODE != kKvHash) {
+    if (MODE != kKvHash && !FORST_KV_ROWS) {
       uint64_t lv = __ballot(valid && vl > 240);
       while (lv) {
         const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lv));

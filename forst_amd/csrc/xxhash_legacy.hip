@@ -236,16 +236,33 @@ __global__ void __launch_bounds__(kThreads) xxhash_legacy_kernel(BlockArgs a) {
 // cover 16 x 16 bytes per load instruction -- 0.21 (XXH32) / 0.31 (XXH64) of
 // the HBM peak on 1 M x 16 KiB (bench round 5).  Here one LANE hashes one
 // message with its four accumulators in registers (four independent chains),
-// reading 64 bytes per step with four 16-byte loads and one realignment
+// reading kLStep bytes per step with 16-byte loads and one realignment
 // dword; a wave works on 64 messages, and a lane that is done takes the next
 // message of the wave's batch at once, so no lane waits for the wave's
 // longest message (batches of 64 descriptors: the first static, the rest
-// claimed from a ticket).  The last <= 68 bytes (the stripes the 64-byte
+// claimed from a ticket).  The last < kLStep + 4 bytes (the stripes the
 // steps leave, the tail and the virtual type byte of compute mode) are
 // copied into the lane's LDS slot with independent loads and finished there.
 constexpr uint32_t kLWaves = 4;
 constexpr uint32_t kLThreads = kLWaves * 64;
-constexpr uint32_t kLSlot = 80;  // LDS bytes per lane (20 KiB per workgroup)
+// 256 bytes per lane and step (64 dwords in flight per lane), one 4-wave
+// workgroup per CU: each lane consumes whole cache lines per step, and the
+// CU streams 256 messages at once.  A/B on one box, 1 M x 16 KiB, verify /
+// trailer fraction of the HBM peak (profiles/ab_r05/
+// xxhash_lane_step_occupancy.log): the group kernel 0.21 / 0.21 (XXH32),
+// 0.32 / 0.31 (XXH64); 64-byte steps at 8 workgroups per CU 0.41 / 0.40;
+// 128 B at 2 per CU 0.53 / 0.50, at 1 per CU 0.56 / 0.57; 256 B at 2 per CU
+// 0.61 / 0.58, at 1 per CU 0.61-0.62 / 0.62 (both hashes) -- with 64-byte
+// steps thousands of lanes each read half a line at a time, and the other
+// half was gone from the caches by the next step.
+#ifndef FORST_LANE_STEP
+#define FORST_LANE_STEP 256
+#endif
+#ifndef FORST_LANE_WG_PER_CU
+#define FORST_LANE_WG_PER_CU 1
+#endif
+constexpr uint32_t kLStep = FORST_LANE_STEP;  // bytes per lane and step (64 or 128)
+constexpr uint32_t kLSlot = kLStep + 16;      // LDS bytes per lane: the < kLStep + 4 tail bytes
 
 // little-endian word at byte o of a lane's slot (o + 8 <= kLSlot)
 __device__ __forceinline__ uint32_t slot32(const uint8_t* sl, uint32_t o) {
@@ -310,9 +327,9 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
           nv = 1;
           vb = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
         }
-        // 64-byte steps whose aligned window [pa + pos, +68) lies in the
+        // steps whose aligned window [pa + pos, + kLStep + 4) lies in the
         // message's own bytes
-        vend = nmem + m >= 68 ? ((nmem + m - 4) & ~63u) : 0u;
+        vend = nmem + m >= kLStep + 4 ? ((nmem + m - 4) & ~(kLStep - 1)) : 0u;
         pos = 0;
         if (X64) {
           v0 = Q64_1 + Q64_2;
@@ -343,27 +360,28 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
       }
     }
     if (!__ballot(have)) break;
-    // ---- one 64-byte step of every lane that has one left
+    // ---- one kLStep-byte step of every lane that has one left
     const bool vec = have && pos < vend;
     if (__ballot(vec)) {
       const uint8_t* q = (vec ? pa + pos : a.base) + vzero();
-      uint32_t d[17];
+      constexpr int kW = kLStep / 4;  // dwords per step
+      uint32_t d[kW + 1];
 #pragma unroll
-      for (int k = 0; k < 4; ++k) {
+      for (int k = 0; k < kW / 4; ++k) {
         const u32x4a4 x = ld16_a4(q + 16 * k);
         d[4 * k] = x.x;
         d[4 * k + 1] = x.y;
         d[4 * k + 2] = x.z;
         d[4 * k + 3] = x.w;
       }
-      d[16] = ld4_a4(q + 64);
+      d[kW] = ld4_a4(q + kLStep);
       if (vec) {
-        uint32_t w[16];
+        uint32_t w[kW];
 #pragma unroll
-        for (int j = 0; j < 16; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], m);
+        for (int j = 0; j < kW; ++j) w[j] = __builtin_amdgcn_alignbyte(d[j + 1], d[j], m);
         if (X64) {
 #pragma unroll
-          for (int st = 0; st < 2; ++st) {
+          for (int st = 0; st < kW / 8; ++st) {
             const uint32_t* x = w + 8 * st;
             v0 = r64(v0, static_cast<uint64_t>(x[0]) | (static_cast<uint64_t>(x[1]) << 32));
             v1 = r64(v1, static_cast<uint64_t>(x[2]) | (static_cast<uint64_t>(x[3]) << 32));
@@ -372,14 +390,14 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
           }
         } else {
 #pragma unroll
-          for (int st = 0; st < 4; ++st) {
+          for (int st = 0; st < kW / 4; ++st) {
             v0 = r32(static_cast<uint32_t>(v0), w[4 * st]);
             v1 = r32(static_cast<uint32_t>(v1), w[4 * st + 1]);
             v2 = r32(static_cast<uint32_t>(v2), w[4 * st + 2]);
             v3 = r32(static_cast<uint32_t>(v3), w[4 * st + 3]);
           }
         }
-        pos += 64;
+        pos += kLStep;
       }
     }
     // ---- lanes whose steps are done: the rest from the LDS slot, then store
@@ -388,16 +406,17 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
     if (fin) {
       // bytes [vend, nmem) as the dword-aligned words from pa + vend (at slot
       // byte m + x for message byte vend + x); words past the message are 0
-      const uint32_t span = m + (nmem - vend);  // <= 70
+      const uint32_t span = m + (nmem - vend);  // < kLStep + 4
       const uint8_t* q = pa + vend;
-      uint32_t t[18];
+      constexpr int kT = kLStep / 4 + 1;
+      uint32_t t[kT];
 #pragma unroll
-      for (int k = 0; k < 18; ++k) t[k] = 4u * k < span ? ld4_a4(q + 4 * k + vzero()) : 0u;
+      for (int k = 0; k < kT; ++k) t[k] = 4u * k < span ? ld4_a4(q + 4 * k + vzero()) : 0u;
       uint32_t* sw = reinterpret_cast<uint32_t*>(sl);
 #pragma unroll
-      for (int k = 0; k < 18; ++k) sw[k] = t[k];
-      sw[18] = 0u;
-      sw[19] = 0u;
+      for (int k = 0; k < kT; ++k) sw[k] = t[k];
+#pragma unroll
+      for (int k = kT; k < static_cast<int>(kLSlot / 4); ++k) sw[k] = 0u;
       if (nv) sl[span] = static_cast<uint8_t>(vb);
     }
     if (fin) {
@@ -406,7 +425,7 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
       uint32_t o = vend;               // message offset; slot byte m + (o - vend)
       auto w32 = [&](uint32_t at) { return slot32(sl, m + (at - vend)); };
       auto w64 = [&](uint32_t at) { return slot64(sl, m + (at - vend)); };
-      for (; o + S <= nst * S; o += S) {  // the stripes after the 64-byte steps
+      for (; o + S <= nst * S; o += S) {  // the stripes after the steps
         if (X64) {
           v0 = r64(v0, w64(o));
           v1 = r64(v1, w64(o + 8));
@@ -542,8 +561,8 @@ hipError_t launch_lane(int mode, const BlockArgs& a, hipStream_t stream, const c
   const DeviceInfo& di = device_info();
   const uint64_t batches = (a.n + 63) / 64;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
-      1, std::min<uint64_t>((batches + kLWaves - 1) / kLWaves, uint64_t(di.num_cus) * 8)));
-  // (8 workgroups of 4 waves per CU: 160 KiB of slots)
+      1, std::min<uint64_t>((batches + kLWaves - 1) / kLWaves,
+                            uint64_t(di.num_cus) * FORST_LANE_WG_PER_CU)));
   BlockArgs b = a;
   void* t = nullptr;
   hipError_t e = scratch_alloc(&t, 256, stream);

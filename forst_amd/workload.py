@@ -149,20 +149,46 @@ def wal_layout(lengths, recyclable=False):
 
 
 def make_wal_batch(n_records, seed, lo=32, hi=32768, recyclable=False, log_number=0,
-                   device="cuda", lengths=None):
+                   device="cuda", lengths=None, block_range=None):
     """C5-shaped WAL image built on the device: logical record
     lengths log-uniform in [lo, hi], framed by log::Writer's rules
     (forst_wal_layout); payload bytes are the splitmix64 stream of `seed`,
     headers [crc:4 len:2 type:1 (lognum:4)] are written in place, block-tail
     pads zeroed and the CRCs filled by the writer-side kernel
-    (forst_wal_record_crc_batch)."""
+    (forst_wal_record_crc_batch).  block_range = (b0, b1): only the 32 KiB
+    log blocks [b0, b1) of that log, as their own buffer (physical records
+    never straddle a block, log_writer.cc:86-102): a rank's shard of one log;
+    offsets are then relative to block b0 and n_records counts the logical
+    records whose first fragment lies in the range."""
     if lengths is None:
         lengths = log_uniform_lengths(n_records, lo, hi, seed)
     offs, lens, types, poffs, plens, total = wal_layout(lengths, recyclable)
+    if block_range is not None:
+        b0, b1 = block_range
+        lo_b, hi_b = b0 * 32768, min(total, b1 * 32768)
+        keep = (offs >= lo_b) & (offs < hi_b)
+        offs, lens, types = offs[keep] - np.uint64(lo_b), lens[keep], types[keep]
+        pk = (poffs >= lo_b) & (poffs < hi_b)
+        poffs, plens = poffs[pk] - np.uint64(lo_b), plens[pk]
+        total = hi_b - lo_b
+        alloc = max(256, (total + 255) // 256 * 256)
+        log = torch.empty(alloc, dtype=torch.uint8, device=device)
+        engine.fill_stream(log, lo_b, seed)
+        log = log[:total]
+        n_rec = int(((types == 1) | (types == 2) | (types == 5) | (types == 6)).sum())
+        return _frame_wal(log, offs, lens, types, poffs, plens, total, seed, n_rec, recyclable,
+                          log_number, device)
     alloc = max(256, (total + 255) // 256 * 256)
     log = torch.empty(alloc, dtype=torch.uint8, device=device)
     engine.fill_stream(log, 0, seed)
     log = log[:total]
+    return _frame_wal(log, offs, lens, types, poffs, plens, total, seed, len(lengths), recyclable,
+                      log_number, device)
+
+
+def _frame_wal(log, offs, lens, types, poffs, plens, total, seed, n_rec, recyclable, log_number,
+               device):
+    """headers, zeroed block tails and writer CRCs into a payload image"""
     d_offs = torch.from_numpy(offs.view(np.int64)).to(device)
     hdr = [(4, (lens & 0xFF).astype(np.uint8)), (5, (lens >> 8).astype(np.uint8)), (6, types)]
     if recyclable:
@@ -176,5 +202,6 @@ def make_wal_batch(n_records, seed, lo=32, hi=32768, recyclable=False, log_numbe
         within = np.arange(int(plens64.sum()), dtype=np.int64) - np.repeat(
             np.cumsum(plens64) - plens64, plens64)
         log[torch.from_numpy(starts + within).to(device)] = 0
-    engine.wal_record_crc_batch(log, d_offs, write_in_place=True)
-    return WalBatch(log, offs, lens, types, len(lengths), total, seed)
+    if len(offs):
+        engine.wal_record_crc_batch(log, d_offs, write_in_place=True)
+    return WalBatch(log, offs, lens, types, n_rec, total, seed)

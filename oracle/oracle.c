@@ -1195,6 +1195,7 @@ typedef struct {
   uint32_t* nrec_out;
   uint32_t* fail_out;
   uint32_t log_number;
+  int check_log;  /* compare recyclable headers' log number (the per-block form) */
 } wal_job;
 
 static void* wal_worker(void* arg) {
@@ -1217,7 +1218,7 @@ static void* wal_worker(void* arg) {
       if (recyc) hs = LOG_RHDR;
       if (end - pos < hs) break;
       if (hs + length > end - pos) { bad++; st = 2; break; } /* kBadRecordLen */
-      if (recyc && ld32(h + 7) != j->log_number) { st = 4; break; } /* kOldRecord */
+      if (j->check_log && recyc && ld32(h + 7) != j->log_number) { st = 4; break; } /* kOldRecord */
       if (type == kZeroType && length == 0) { st = 3; break; } /* preallocated */
       uint32_t expected = oracle_crc32c_unmask(ld32(h));
       uint32_t actual = ~crc_raw_update_fast(~0u, h + 6, length + hs - 6);
@@ -1252,6 +1253,7 @@ void oracle_wal_verify_blocks(const uint8_t* buf, uint64_t nbytes, uint32_t log_
     jobs[t].nrec_out = nrec;
     jobs[t].fail_out = fail_off;
     jobs[t].log_number = log_number;
+    jobs[t].check_log = 1;
   }
   for (int t = 1; t < nthreads; t++)
     pthread_create(&th[t], NULL, wal_worker, &jobs[t]);

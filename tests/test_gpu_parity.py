@@ -783,3 +783,31 @@ def test_c4_full_volume_sharded_on_one_gpu():
     _, _, ok_all, bad_all = engine.block_verify_batch(CT.kCRC32c, b.base, b.offsets, b.sizes)
     assert int(host(bad_all)[0]) == len(victims)
     assert np.nonzero(host(ok_all) == 0)[0].tolist() == victims
+
+
+def test_wal_block_range_shards_tile_the_log():
+    """bench.py's C5 at N GPUs: make_wal_batch(block_range=...) builds a
+    rank's contiguous log blocks of one log; the 3 shards concatenated are the
+    whole log byte for byte, their records are the log's records, and each
+    shard's per-block verify equals the whole log's (log_writer.cc:86-102:
+    records never straddle a block)"""
+    lengths = workload.log_uniform_lengths(60000, 32, 32768, workload.SEEDS["C5"])
+    full = workload.make_wal_batch(0, workload.SEEDS["C5"], lengths=lengths)
+    st, nr, fo, bad = engine.wal_verify_batch(full.log)
+    assert int(host(bad)[0]) == 0
+    nb = full.n_log_blocks
+    parts, recs = [], 0
+    for r in range(3):
+        b0, b1 = nb * r // 3, nb * (r + 1) // 3
+        w = workload.make_wal_batch(0, workload.SEEDS["C5"], lengths=lengths, block_range=(b0, b1))
+        parts.append(host(w.log))
+        s2, n2, f2, bad2 = engine.wal_verify_batch(w.log)
+        assert int(host(bad2)[0]) == 0
+        assert np.array_equal(host(s2), host(st)[b0:b1]) and np.array_equal(host(n2), host(nr)[b0:b1])
+        assert np.array_equal(host(f2), host(fo)[b0:b1])
+        assert np.array_equal(w.rec_offsets + np.uint64(b0 * 32768),
+                              full.rec_offsets[(full.rec_offsets >= b0 * 32768) &
+                                               (full.rec_offsets < b1 * 32768)])
+        recs += w.n_records
+    assert np.array_equal(np.concatenate(parts), host(full.log))
+    assert recs == full.n_records

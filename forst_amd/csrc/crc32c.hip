@@ -1241,6 +1241,8 @@ struct CRowPos {
   __device__ __forceinline__ uint32_t d1() const { return (pk >> 16) & 12u; }  // bytes: 0, 4, 8
   __device__ __forceinline__ bool r0() const { return (pk >> 20) & 1u; }
   __device__ __forceinline__ uint32_t slow_size() const { return (pk >> 24) & 15u; }
+  // (length-split batches) no descriptor yet, more may come: ask again
+  __device__ __forceinline__ bool wait() const { return (pk >> 21) & 1u; }
   // fast rows: offset + size of the block (where a trailer goes), from the
   // window end: E - the type byte when it is in memory
   template <int MODE>
@@ -1390,8 +1392,27 @@ constexpr uint32_t kRowsD2Waves = 12;
 constexpr uint32_t kDiagWaves = 8192;
 __device__ unsigned long long g_wave_t0[kDiagWaves], g_wave_t1[kDiagWaves];
 #endif
-template <int MODE, int PROBE, int DEPTH, bool RAW_WG = false>
+// Raw batches split by message length (FILT): messages shorter than
+// kRawSplit bytes go to crc32c_raw_lane_kernel (one message per lane), the
+// rest to the rows kernel, which drops the short ones from each descriptor
+// batch as it loads it.  A short WAL record still costs a row a whole 1 KiB
+// round; on C5 the records <= 512 B (40 % of them, 1.5 % of the bytes) took
+// 0.69 ms of the 9.03 ms raw pass (profiles/ab_r04/c5_record_classes_raw_crc.json).
+#ifndef FORST_RAW_SPLIT
+#define FORST_RAW_SPLIT 256
+#endif
+constexpr uint32_t kRawSplit = FORST_RAW_SPLIT;
+
+// A message goes to the rows filter kernel when it has kRawSplit bytes or
+// more and its offset is below 2^58 (any larger one lies outside every
+// buffer: the lane kernel reports it; batch_compact, stream_common.h).
+__device__ __forceinline__ bool raw_long(uint64_t off, uint32_t size) {
+  return size >= kRawSplit && (off >> 58) == 0;
+}
+
+template <int MODE, int PROBE, int DEPTH, bool RAW_WG = false, bool FILT = false>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
+  static_assert(!FILT || (MODE == kModeRaw && !RAW_WG), "length split: raw global feed only");
   __shared__ uint32_t L[kLds3Bytes / 4];
   feed_init();
   fill_tables3<64 * (DEPTH == 2 ? kRowsD2Waves : kWaves)>(L);
@@ -1433,12 +1454,42 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   __shared__ uint8_t st_ok[kStage ? kStageW : 4];
   if (!kStage && cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
-  uint64_t ng = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
-  uint32_t nlen = feed.len;
+  uint64_t ng = 0;
+  uint32_t nlen = 0;
+  if constexpr (!FILT) {  // (FILT: claimed after cb, whose loading may claim further)
+    ng = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
+    nlen = feed.len;
+  }
   DescBatch cb, nb;
   uint64_t kbrel = 0;  // stream position of cb's first entry
-  load_batch<MODE>(a, cg, a.n, lane, cb);
-  load_batch<MODE>(a, ng, a.n, lane, nb);
+  // FILT: the batch's messages of kRawSplit bytes or more, moved to its
+  // first lanes; a batch with none is skipped (the next one claimed) so a
+  // batch is empty only once the feed is exhausted.  (The ballot waits for
+  // the batch's loads: one load latency per 64 descriptors.)
+  auto load_f = [&](uint64_t& g, uint32_t& len, DescBatch& d) {
+    load_batch<MODE>(a, g, a.n, lane, d);
+    if constexpr (FILT) {
+      for (;;) {
+        const bool keep =
+            lane < len && raw_long((static_cast<uint64_t>(d.off_hi) << 32) | d.off_lo, d.size);
+        const uint64_t km = __ballot(keep);
+        if (km != 0 || len == 0) {
+          batch_compact<false, false>(d, km, keep, lane);
+          len = static_cast<uint32_t>(__popcll(km));
+          break;
+        }
+        g = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
+        len = feed.len;
+        load_batch<MODE>(a, g, a.n, lane, d);
+      }
+    }
+  };
+  load_f(cg, clen, cb);
+  if constexpr (FILT) {
+    ng = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
+    nlen = feed.len;
+  }
+  load_f(ng, nlen, nb);
   const uint64_t kbeg = 0;
   auto fetch = [&](uint64_t rel, CRowPos& P) {
     const BatchSlot q = batch_slot(rel, kbrel, cg, clen, ng, nlen, a.n);
@@ -1446,18 +1497,33 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     const uint32_t sz_c = __shfl(cb.size, q.src);
     const uint32_t lo_n = __shfl(nb.off_lo, q.src), hi_n = __shfl(nb.off_hi, q.src);
     const uint32_t sz_n = __shfl(nb.size, q.src);
-    const uint64_t off =
-        (static_cast<uint64_t>(q.in_n ? hi_n : hi_c) << 32) | (q.in_n ? lo_n : lo_c);
+    uint32_t hi = q.in_n ? hi_n : hi_c;
+    uint64_t gi = q.gi;
+    if constexpr (FILT) {  // slot k of a compacted batch: descriptor base + its lane as loaded
+      gi = (q.in_n ? ng : cg) + (hi >> 26);
+      hi &= 0x03ffffffu;
+    }
+    const uint64_t off = (static_cast<uint64_t>(hi) << 32) | (q.in_n ? lo_n : lo_c);
     const uint32_t size = q.in_n ? sz_n : sz_c;
-    P.rel = q.valid ? static_cast<uint32_t>(q.gi) : kNoBlk;
+    P.rel = q.valid ? static_cast<uint32_t>(gi) : kNoBlk;
     crow_derive<MODE>(a, off, size, P);
   };
+  // A compacted batch may hold fewer descriptors than the wave has rows
+  // (FILT): positions are handed out only while cb and nb have some left, and
+  // a row that finds none WAITS (asks again in the next step) unless the feed
+  // is exhausted -- a position handed to no row would be a descriptor never
+  // computed.  (Full batches have 64: the original rule never runs short.)
   uint64_t next = 4;
   CRowPos C;
   fetch(lane >> 4, C);
+  if constexpr (FILT) {
+    const uint64_t avail = clen + nlen;
+    if ((lane >> 4) >= avail && nlen != 0) C.pk |= 1u << 21;
+    next = avail < 4 ? avail : 4;
+  }
   auto advance = [&](const CRowPos& P, CRowPos& I) {
     const bool more = P.rel != kNoBlk && !P.slow() && P.rl > 1;
-    const bool need = P.rel != kNoBlk && !more;
+    const bool need = (P.rel != kNoBlk || (FILT && P.wait())) && !more;
     const uint64_t rows = __ballot(need && t == 0);  // one bit per row leader
     I = P;
     if (more) {
@@ -1470,10 +1536,21 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     // rows in the middle of their blocks (every row, 3 steps in 4 of a batch
     // of 4 KiB blocks): no descriptor work
     if (rows) {
-      const uint32_t rank = static_cast<uint32_t>(__popcll(rows & ((1ull << (lane & ~15u)) - 1)));
+      // rows needing one ahead of this row: rows' bits below the lane, less
+      // the row's own leader bit (rows holds leader bits only) -- v_mbcnt, no
+      // per-lane 64-bit mask held across the loop
+      const uint32_t below = __builtin_amdgcn_mbcnt_hi(
+          static_cast<uint32_t>(rows >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(rows), 0u));
+      const uint32_t rank = below - (t != 0 && need ? 1u : 0u);
       CRowPos F;
       fetch(next + rank, F);
-      next += static_cast<uint64_t>(__popcll(rows));
+      uint64_t got = static_cast<uint64_t>(__popcll(rows));
+      if constexpr (FILT) {
+        const uint64_t avail = kbrel + clen + nlen - next;
+        if (got > avail) got = avail;
+        if (rank >= avail && nlen != 0) F.pk |= 1u << 21;
+      }
+      next += got;
       if (need) I = F;
       if (next >= kbrel + clen) {  // every block of cb is assigned: slide the batches
         kbrel += clen;
@@ -1488,7 +1565,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
         cg = ng;
         ng = feed_next<kWgFeed, kChunk>(a, nw, lane, feed);
         nlen = feed.len;
-        load_batch<MODE>(a, ng, a.n, lane, nb);
+        load_f(ng, nlen, nb);
       }
     }
   };
@@ -1509,7 +1586,7 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
     // and the next step's loads overlap this step's wait (C5 verify / writer
     // +1.5 %); the block modes keep the early exit, which measured better on
     // uniform blocks (A/B on one box: C2 0.600 vs 0.592)
-    const bool live = __ballot(C.rel != kNoBlk) != 0;
+    const bool live = __ballot(C.rel != kNoBlk || (FILT && C.wait())) != 0;
     if ((DEPTH == 2 || MODE != kModeRaw) && !live) return false;
     crow_issue<MODE, PROBE>(a, lane, DEPTH == 2 ? I2 : I, kbeg, nx);
     const bool fast = C.rel != kNoBlk && !C.slow();
@@ -1759,6 +1836,159 @@ __global__ void __launch_bounds__(kThreads) crc32c_rows_kernel(BlockArgs a) {
 __global__ void __launch_bounds__(kThreads) crc32c_rows_raw_small_kernel(BlockArgs a) {
   crc32c_rows_body<kModeRaw, 0, 1, true>(a);
 }
+// the long messages of a raw batch (kRawSplit bytes or more)
+__global__ void __launch_bounds__(kThreads) crc32c_rows_raw_filt_kernel(BlockArgs a) {
+  crc32c_rows_body<kModeRaw, 0, 1, false, true>(a);
+}
+
+// ---- the short messages of a raw batch: one message per lane --------------
+// crc32c::Value(init, p, n) of a message of n < kRawSplit bytes by lane-serial
+// slicing-by-4 on the G tables (the rows kernel's layout, rows of 256 bytes,
+// so each ds_read of a wave is bank-conflict free).  16-byte loads, one in
+// flight ahead of the dwords being folded.  The first dword starts the chain
+// at S0 (~init moved back over the m = p & 3 bytes in front of the message,
+// which are masked to zero), as the rows kernel's head lane does.
+constexpr uint32_t kLaneThreads = 512;
+// 16-byte loads of a short message: its bytes from the dword boundary in
+// front (m <= 3) plus the tail dword
+constexpr uint32_t kLaneChunks = (kRawSplit + 2 + 4 + 15) / 16;
+__device__ __forceinline__ uint32_t lane_raw_crc(const uint8_t* __restrict__ Lb, const Lanes2& K,
+                                                 const uint8_t* base, uint64_t base_len,
+                                                 uint64_t off, uint32_t n, uint32_t init,
+                                                 bool has_init) {
+  const uint32_t m = static_cast<uint32_t>(off & 3);
+  const uint32_t tot = n + m;  // bytes from the dword boundary in front
+  const uint32_t nd = tot >> 2, nt = tot & 3;
+  const uint32_t nc = (nd + (nt ? 1u : 0u) + 3) >> 2;  // 16-byte loads
+  // messages within their first dword, and the last bytes of the buffer:
+  // dword-serial with byte loads at either end (never a byte past it)
+  if (nd == 0 || (off - m) + 16ull * nc > base_len)
+    return small_crc2(Lb, K, base + off, n, init, 0, 0);
+  const uint8_t* q = base + (off - m);
+  const uint32_t S0 = has_init ? unstep_m(~init, m)
+                               : m == 0 ? 0xffffffffu : m == 1 ? 0xa942e6bcu
+                               : m == 2 ? 0x2804363bu : 0x96db52a8u;  // kCrcS0
+  const uint32_t bm = 0xffffffffu << (8 * m);
+  const uint32_t tm = (1u << (8 * nt)) - 1u;
+  uint32_t s = 0;
+  // every load of the message first (one memory latency per message; a
+  // chunk-by-chunk loop waited one per 16 bytes: C5's 3.4 M short records
+  // took 0.42 ms that way), then the chain over them
+  u32x4a4 v[kLaneChunks];
+#pragma unroll
+  for (uint32_t c = 0; c < kLaneChunks; ++c)
+    v[c] = c < nc ? ld16_a4(q + 16 * c) : u32x4a4{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t c = 0; c < kLaneChunks; ++c) {
+    if (c < nc) {
+      const uint32_t w[4] = {v[c].x, v[c].y, v[c].z, v[c].w};
+#pragma unroll
+      for (uint32_t j = 0; j < 4; ++j) {
+        const uint32_t i = 4 * c + j;
+        if (i < nd)
+          s = rep_map<false>(Lb, K, i == 0 ? ((w[j] & bm) ^ S0) : (s ^ w[j]));
+        else if (i == nd && nt)
+          s = step_k(Lb, K, s, w[j] & tm, nt);
+      }
+    }
+  }
+  return ~s;
+}
+
+// every descriptor of the batch that is not raw_long (the rows filter
+// kernel takes those); the same results and stores as the rows kernel's
+// raw mode (wal_hs masking, expect: only differing results stored, an
+// out-of-range descriptor reported as 0).  Each wave takes windows of
+// kRawLaneR x 64 descriptors on its own (no workgroup barrier): it loads
+// them all at once, lists the short ones' window positions in its LDS slots
+// (on C5 at a 256-byte split 3 records in 10 are short) and gives them out
+// one per lane, the descriptor fields moved between lanes by ds_bpermute.
+// Latency bound, so waves independent: workgroup-wide windows with
+// barriers, and one descriptor per thread, measured 0.36 / 0.42 ms on C5
+// against this layout's.
+constexpr uint32_t kRawLaneR = 4;
+constexpr uint32_t kRawLaneWaves = kLaneThreads / 64;
+__global__ void __launch_bounds__(kLaneThreads) crc32c_raw_lane_kernel(BlockArgs a) {
+  __shared__ uint32_t L[16384];
+  __shared__ uint16_t slot[kRawLaneWaves][kRawLaneR * 64];
+  for (uint32_t i = threadIdx.x; i < 16384; i += kLaneThreads) {
+    const uint32_t e = i >> 6, d = i & 63;
+    if (d < 32) L[i] = kCrcG[((d >> 3) & 3) * 256 + e];
+  }
+  __syncthreads();
+  const uint8_t* Lb = reinterpret_cast<const uint8_t*>(L);
+  const uint32_t lane = threadIdx.x & 63;
+  const uint32_t wave = uniform(threadIdx.x >> 6);
+  const Lanes2 K = lanes2(lane);
+  const uint64_t below = (1ull << lane) - 1;
+  const uint64_t nw = static_cast<uint64_t>(gridDim.x) * kRawLaneWaves;
+  constexpr uint64_t W = uint64_t(kRawLaneR) * 64;
+  uint16_t* sl = slot[wave];
+  for (uint64_t w0 = (static_cast<uint64_t>(blockIdx.x) * kRawLaneWaves + wave) * W; w0 < a.n;
+       w0 += nw * W) {
+    uint32_t olo[kRawLaneR], ohi[kRawLaneR], sz[kRawLaneR];
+#pragma unroll
+    for (uint32_t r = 0; r < kRawLaneR; ++r) {  // every load first
+      uint64_t i = w0 + 64 * r + lane;
+      i = i < a.n ? i : a.n - 1;
+      const uint64_t off = a.offsets[i];
+      olo[r] = static_cast<uint32_t>(off);
+      ohi[r] = static_cast<uint32_t>(off >> 32);
+      sz[r] = a.sizes[i];
+    }
+    uint32_t cnt = 0;
+#pragma unroll
+    for (uint32_t r = 0; r < kRawLaneR; ++r) {
+      uint64_t off = (static_cast<uint64_t>(ohi[r]) << 32) | olo[r];
+      uint32_t size = sz[r];
+      if (a.wal_hs) {  // (as load_batch: header offset + payload length)
+        const bool ok = off <= a.base_len && a.base_len - off >= uint64_t(a.wal_hs) + size;
+        off = ok ? off + 6 : ~0ull;
+        size = ok ? a.wal_hs + size - 6 : 0u;
+        olo[r] = static_cast<uint32_t>(off);
+        ohi[r] = static_cast<uint32_t>(off >> 32);
+        sz[r] = size;
+      }
+      const bool sh = w0 + 64 * r + lane < a.n && !raw_long(off, size);
+      const uint64_t m = __ballot(sh);
+      if (sh) sl[cnt + static_cast<uint32_t>(__popcll(m & below))] = static_cast<uint16_t>(64 * r + lane);
+      cnt += static_cast<uint32_t>(__popcll(m));
+    }
+    wave_lds_sync();
+    for (uint32_t j0 = 0; j0 < cnt; j0 += 64) {  // (wave-uniform: the bpermutes need every lane)
+      const uint32_t j = j0 + lane;
+      const uint32_t q = j < cnt ? sl[j] : 0u;
+      const int src = static_cast<int>(4 * (q & 63));
+      uint32_t lo = 0, hi = 0, size = 0;
+#pragma unroll
+      for (uint32_t r = 0; r < kRawLaneR; ++r) {
+        const uint32_t vlo = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(olo[r])));
+        const uint32_t vhi = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(ohi[r])));
+        const uint32_t vsz = static_cast<uint32_t>(__builtin_amdgcn_ds_bpermute(src, static_cast<int>(sz[r])));
+        if ((q >> 6) == r) {
+          lo = vlo;
+          hi = vhi;
+          size = vsz;
+        }
+      }
+      if (j < cnt) {
+        const uint64_t i = w0 + q;
+        const uint64_t off = (static_cast<uint64_t>(hi) << 32) | lo;
+        const bool valid = desc_in_range<kModeRaw>(a, Desc{off, size, 0, 0});
+        const uint32_t init = a.init_crcs ? a.init_crcs[i] : 0u;
+        uint32_t v = 0;
+        if (valid) {
+          const uint32_t crc = lane_raw_crc(Lb, K, a.base, a.base_len, off, size, init,
+                                            a.init_crcs != nullptr);
+          v = a.wal_hs ? crc_mask(crc) : crc;
+        }
+        const bool differs = !a.expect || !valid || v != a.expect[i];
+        if (differs && a.out32) a.out32[i] = v;
+      }
+    }
+    wave_lds_sync();  // (the slots are rewritten by the next window)
+  }
+}
 
 #ifdef FORST_DIAG
 template <int PROBE>
@@ -1978,6 +2208,13 @@ hipError_t launch_crc_mode(CrcKernel k, const BlockArgs& a, uint32_t grid, hipSt
       }
       if (a.n < uint64_t(64) * grid * kWaves)
         return launch_kernel(crc32c_rows_raw_small_kernel, grid, 64 * kWaves, a, s);
+      if constexpr (M == kModeRaw && kRawSplit > 0) {
+        // short messages one per lane, then the rows kernel over the rest
+        const hipError_t e = launch_kernel(crc32c_raw_lane_kernel, 2 * device_info().num_cus,
+                                           kLaneThreads, a, s);
+        if (e != hipSuccess) return e;
+        return launch_fed(crc32c_rows_raw_filt_kernel, grid, kWaves, a, s);
+      }
       return launch_fed(crc32c_rows_kernel<M>, grid, kWaves, a, s);
     case CrcKernel::kV2:
       return launch_kernel(crc32c_stream2_kernel<M>, grid, kThreads, a, s);
@@ -2089,8 +2326,10 @@ hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream
   // output) exists in the rows kernel only
   if (a.wal_hs && (mode != kModeRaw || k != CrcKernel::kRows)) return hipErrorInvalidValue;
   *name = crc_kernel_name(k, mode);
-  if (k == CrcKernel::kRows && mode == kModeRaw && a.n < uint64_t(64) * grid * kWaves)
-    *name = "crc32c_rows_raw_small_kernel";
+  if (k == CrcKernel::kRows && mode == kModeRaw)
+    *name = a.n < uint64_t(64) * grid * kWaves ? "crc32c_rows_raw_small_kernel"
+            : kRawSplit > 0                    ? "crc32c_rows_raw_filt_kernel"
+                                               : "crc32c_rows_kernel<raw>";
   switch (mode) {
     case kModeCompute:
       return launch_crc_mode<kModeCompute>(k, a, grid, stream);

@@ -69,6 +69,19 @@ __device__ __forceinline__ uint32_t fresh(uint32_t v) {
   return v;
 }
 
+// Orders a wave's LDS stores before its later LDS loads of other lanes'
+// words (a wave's LDS operations complete in order on the GPU; the fences
+// keep the compiler from moving them across; the emulator's threads meet).
+__device__ __forceinline__ void wave_lds_sync() {
+#ifdef FORST_HOST_EMULATION
+  (void)__ballot(1);
+#else
+  __builtin_amdgcn_fence(__ATOMIC_RELEASE, "wavefront");
+  __builtin_amdgcn_wave_barrier();
+  __builtin_amdgcn_fence(__ATOMIC_ACQUIRE, "wavefront");
+#endif
+}
+
 #ifdef FORST_DEBUG_BOUNDS
 // Diagnostics build only (make DEBUG_BOUNDS=1 -> lib/libforst_checksum_dbg.so):
 // every block-data load is checked against the launch's buffer bounds; the

@@ -266,6 +266,31 @@ __device__ __forceinline__ void load_batch(const BlockArgs& a, uint64_t kb, uint
   }
 }
 
+// Length-split batches (the raw CRC rows kernel, the fragment XXH3 kernel):
+// the descriptors a kernel keeps move to the batch's first lanes, in lane
+// order (the others after them), by one ds_permute per field; each kept
+// descriptor's lane in the batch as loaded rides in the top 6 bits of off_hi,
+// so only offsets below 2^58 may be kept (any larger one lies outside every
+// buffer).  EXTRA / MOD: the fields the kernel reads besides offset and size.
+__device__ __forceinline__ bool below_2p58(const DescBatch& d) { return (d.off_hi >> 26) == 0; }
+template <bool EXTRA, bool MOD>
+__device__ __forceinline__ void batch_compact(DescBatch& d, uint64_t km, bool keep,
+                                              uint32_t lane) {
+  const uint64_t below = (1ull << lane) - 1;
+  const uint32_t nk = static_cast<uint32_t>(__popcll(km));
+  const uint32_t dst = keep ? static_cast<uint32_t>(__popcll(km & below))
+                            : nk + static_cast<uint32_t>(__popcll(~km & below));
+  const int ad = static_cast<int>(4 * dst);
+  auto perm = [&](uint32_t v) {
+    return static_cast<uint32_t>(__builtin_amdgcn_ds_permute(ad, static_cast<int>(v)));
+  };
+  d.off_lo = perm(d.off_lo);
+  d.off_hi = perm((d.off_hi & 0x03ffffffu) | (lane << 26));
+  d.size = perm(d.size);
+  if (EXTRA) d.extra = perm(d.extra);
+  if (MOD) d.mod = perm(d.mod);
+}
+
 // descriptor k (kb <= k < kb + 128) from the current / next batch, uniform
 struct Desc {
   uint64_t off;

@@ -38,11 +38,22 @@ constexpr uint32_t kWhLanes = 256;
 // per logical record: in-place descriptor (p0, len, info = hs | j_last << 8)
 // for the frag kernel, or glen = len when it must be gathered (its frag
 // descriptor then has length 0)
+// Packed form (n < 2^24 records, a log under 2^40 bytes): glen[j] = bytes |
+// 1 << 40 for a gathered record, so ONE exclusive scan gives both its scratch
+// offset (low 40 bits) and its list position (the high bits) -- one scan and
+// the flag pass fewer than two scans.
+constexpr uint32_t kWhPackShift = 40;
+constexpr uint64_t kWhPackMask = (uint64_t(1) << kWhPackShift) - 1;
+__device__ __forceinline__ uint64_t wh_goff(const uint64_t* go, uint64_t j, bool packed) {
+  return packed ? go[j] & kWhPackMask : go[j];
+}
+
 template <class F>
 __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, uint64_t log_len,
                                                            F f, uint64_t n,
                                                            uint64_t* p0, uint32_t* len,
-                                                           uint32_t* info, uint64_t* glen) {
+                                                           uint32_t* info, uint64_t* glen,
+                                                           bool packed) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
   if (j >= n) return;
   const uint64_t b = f.begin(j), e = f.end(j);
@@ -77,7 +88,7 @@ __global__ void __launch_bounds__(kWhLanes) wh_prep_kernel(const uint8_t* log, u
   p0[j] = start;
   len[j] = regular ? static_cast<uint32_t>(total) : 0u;
   info[j] = multi ? (hs0 | ((nz - 1) << 8)) : 0u;
-  glen[j] = regular ? 0 : total;
+  glen[j] = regular ? 0 : packed ? total | (uint64_t(1) << kWhPackShift) : total;
 }
 
 __global__ void __launch_bounds__(kWhLanes) wh_flag_kernel(const uint64_t* glen, uint64_t n,
@@ -92,13 +103,13 @@ __global__ void __launch_bounds__(kWhLanes) wh_list_kernel(const uint64_t* glen,
                                                            const uint64_t* goff,
                                                            const uint64_t* gpos, uint64_t n,
                                                            uint64_t* list, uint64_t* boff,
-                                                           uint32_t* blen) {
+                                                           uint32_t* blen, bool packed) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
   if (j >= n || glen[j] == 0) return;
-  const uint64_t i = gpos[j];
+  const uint64_t i = packed ? goff[j] >> kWhPackShift : gpos[j];
   list[i] = j;
-  boff[i] = goff[j];
-  blen[i] = static_cast<uint32_t>(glen[j]);
+  boff[i] = wh_goff(goff, j, packed);
+  blen[i] = static_cast<uint32_t>(packed ? glen[j] & kWhPackMask : glen[j]);
 }
 
 // one workgroup per gathered record: its fragments back to back at dst + boff[i]
@@ -131,14 +142,13 @@ __global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log,
   }
 }
 
-__global__ void __launch_bounds__(kWhLanes) wh_select_kernel(const uint64_t* glen,
-                                                             const uint64_t* gpos,
-                                                             const uint64_t* ha,
-                                                             const uint64_t* hb, uint64_t n,
-                                                             uint64_t* out) {
-  const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
-  if (j >= n) return;
-  out[j] = glen[j] ? hb[gpos[j]] : ha[j];
+// the frag kernel wrote every record's slot of out (a gathered record's
+// descriptor has length 0): the gathered records' hashes over theirs
+__global__ void __launch_bounds__(kWhLanes) wh_patch_kernel(const uint64_t* list,
+                                                            const uint64_t* hb, uint64_t ng,
+                                                            uint64_t* out) {
+  const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kWhLanes + threadIdx.x;
+  if (i < ng) out[list[i]] = hb[i];
 }
 
 // The gathered records' branch (list, gather, their XXH3) does not depend on
@@ -176,53 +186,56 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
                                 uint64_t* out, hipStream_t st, const char** name,
                                 bool overlap = true) {
   if (n == 0) return hipSuccess;
+  const bool packed = n < (uint64_t(1) << 24) && log_len < (uint64_t(1) << kWhPackShift);
   const uint64_t nt = n / kScanTile + 2;
   const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * nt);
   void* scratch = nullptr;
-  hipError_t e = scratch_alloc(&scratch, 8 * s8 + 3 * s4 + 2 * st8, st);
+  hipError_t e = scratch_alloc(&scratch, 7 * s8 + 3 * s4 + 2 * st8, st);
   if (e != hipSuccess) return e;
   uint8_t* p = static_cast<uint8_t*>(scratch);
   uint64_t* p0 = reinterpret_cast<uint64_t*>(p);
   uint64_t* glen = reinterpret_cast<uint64_t*>(p + s8);
   uint64_t* goff = reinterpret_cast<uint64_t*>(p + 2 * s8);
-  uint64_t* gpos = reinterpret_cast<uint64_t*>(p + 3 * s8);
-  uint64_t* ha = reinterpret_cast<uint64_t*>(p + 4 * s8);
-  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 5 * s8);
-  uint64_t* list = reinterpret_cast<uint64_t*>(p + 6 * s8);
-  uint64_t* boff = reinterpret_cast<uint64_t*>(p + 7 * s8);  // (reused as the flags)
-  uint32_t* len = reinterpret_cast<uint32_t*>(p + 8 * s8);
-  uint32_t* info = reinterpret_cast<uint32_t*>(p + 8 * s8 + s4);
-  uint32_t* blen = reinterpret_cast<uint32_t*>(p + 8 * s8 + 2 * s4);
-  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4);
-  uint64_t* tiles2 = reinterpret_cast<uint64_t*>(p + 8 * s8 + 3 * s4 + st8);
+  uint64_t* gpos = reinterpret_cast<uint64_t*>(p + 3 * s8);  // (unpacked form only)
+  uint64_t* hb = reinterpret_cast<uint64_t*>(p + 4 * s8);
+  uint64_t* list = reinterpret_cast<uint64_t*>(p + 5 * s8);
+  uint64_t* boff = reinterpret_cast<uint64_t*>(p + 6 * s8);  // (reused as the flags)
+  uint32_t* len = reinterpret_cast<uint32_t*>(p + 7 * s8);
+  uint32_t* info = reinterpret_cast<uint32_t*>(p + 7 * s8 + s4);
+  uint32_t* blen = reinterpret_cast<uint32_t*>(p + 7 * s8 + 2 * s4);
+  uint64_t* tiles = reinterpret_cast<uint64_t*>(p + 7 * s8 + 3 * s4);
+  uint64_t* tiles2 = reinterpret_cast<uint64_t*>(p + 7 * s8 + 3 * s4 + st8);
   hipLaunchKernelGGL(wh_prep_kernel<F>, wh_grid(n), dim3(kWhLanes), 0, st, log, log_len, f, n,
-                     p0, len,
-                     info, glen);
+                     p0, len, info, glen, packed);
   scan_u64(glen, n, tiles, goff, st);
-  hipLaunchKernelGGL(wh_flag_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, n, boff);
-  scan_u64(boff, n, tiles2, gpos, st);
-  uint64_t tot[2] = {0, 0};  // gathered bytes, gathered records
+  if (!packed) {
+    hipLaunchKernelGGL(wh_flag_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, n, boff);
+    scan_u64(boff, n, tiles2, gpos, st);
+  }
+  uint64_t tot[2] = {0, 0};  // gathered bytes, gathered records (packed: both in tot[0])
   const uint64_t ntl = (n + kScanTile - 1) / kScanTile;
-  // in place across the fragments (every record; gathered ones have length 0)
+  // in place across the fragments, straight into out (every record; the
+  // gathered ones have length 0 and are patched below)
   BlockArgs fa{};
   fa.base = log;
   fa.base_len = log_len;
   fa.offsets = p0;
   fa.sizes = len;
   fa.init_crcs = info;
-  fa.out64 = ha;
+  fa.out64 = out;
   fa.n = n;
   auto frag = [&]() {
     return log_len >= 4096 ? launch_xxh3_frag(fa, st, name)
                            : launch_xxh3_blocks(kModeRaw, fa, st, name);
   };
   if ((e = hipMemcpyAsync(&tot[0], tiles + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess ||
-      (e = hipMemcpyAsync(&tot[1], tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess) {
+      (!packed &&
+       (e = hipMemcpyAsync(&tot[1], tiles2 + ntl, 8, hipMemcpyDeviceToHost, st)) != hipSuccess)) {
     (void)scratch_free(scratch, st);
     return e;
   }
   // With the second stream the frag kernel is queued before the host waits
-  // for the two totals (on an event behind their copies), so the GPU does not
+  // for the totals (on an event behind their copies), so the GPU does not
   // idle through the host's turnaround, and the gathered branch starts on the
   // second stream while the frag kernel runs.
   AuxHold hold;
@@ -244,7 +257,8 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
     (void)scratch_free(scratch, st);
     return e;
   }
-  const uint64_t gtotal = tot[0], ng = tot[1];
+  const uint64_t gtotal = packed ? tot[0] & kWhPackMask : tot[0];
+  const uint64_t ng = packed ? tot[0] >> kWhPackShift : tot[1];
   void* gbuf = nullptr;
   if (ng) {
     hipStream_t gs = st;
@@ -253,7 +267,7 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
     e = scratch_alloc(&gbuf, wh_up256(gtotal + 4096), gs);
     if (e == hipSuccess) {
       hipLaunchKernelGGL(wh_list_kernel, wh_grid(n), dim3(kWhLanes), 0, gs, glen, goff, gpos, n,
-                         list, boff, blen);
+                         list, boff, blen, packed);
       const uint32_t gg = static_cast<uint32_t>(ng < 65536 ? ng : 65536);
       hipLaunchKernelGGL(wh_gather_kernel<F>, dim3(gg), dim3(kWhLanes), 0, gs, log, f, list,
                          boff, ng, static_cast<uint8_t*>(gbuf));
@@ -275,14 +289,9 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
       if (e == hipSuccess) e = hipErrorUnknown;
       (void)hipStreamSynchronize(gs);
     }
-  }
-  if (e == hipSuccess) {
-    if (ng) {
-      hipLaunchKernelGGL(wh_select_kernel, wh_grid(n), dim3(kWhLanes), 0, st, glen, gpos, ha, hb,
-                         n, out);
+    if (e == hipSuccess) {  // behind the frag kernel (st) and the join
+      hipLaunchKernelGGL(wh_patch_kernel, wh_grid(ng), dim3(kWhLanes), 0, st, list, hb, ng, out);
       e = hipGetLastError();
-    } else {
-      e = hipMemcpyAsync(out, ha, 8 * n, hipMemcpyDeviceToDevice, st);
     }
   }
   const hipError_t f1 = scratch_free(gbuf, st), f2 = scratch_free(scratch, st);

@@ -35,6 +35,7 @@ def lib():
             "forst_xxh3_64_batch": (i, [vp, u64, vp, vp, vp, u64, vp]),
             "forst_wal_verify_batch": (i, [vp, u64, u64, u64, u32, vp, vp, vp, vp, vp]),
             "forst_wal_record_crc_batch": (i, [vp, u64, vp, u64, i, vp, vp]),
+            "forst_wal_record_crc_lengths": (i, [vp, u64, vp, vp, u64, i, i, vp, vp]),
             "forst_hash64_batch": (i, [vp, u64, vp, vp, vp, u64, vp, u64, vp]),
             "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
             "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp,
@@ -155,6 +156,17 @@ def wal_record_crc(log, header_offsets, write_in_place=True):
     out = np.zeros(len(offs), np.uint32)
     _chk(lib().forst_wal_record_crc_batch(_p(log), log.nbytes, _p(offs), len(offs),
                                           int(write_in_place), _p(out), None))
+    return out, log
+
+
+def wal_record_crc_lengths(log, header_offsets, payload_lengths, recyclable=False,
+                           write_in_place=True):
+    log = _aligned(log)
+    offs = np.ascontiguousarray(header_offsets, dtype=np.uint64)
+    lens = np.ascontiguousarray(payload_lengths, dtype=np.uint32)
+    out = np.zeros(len(offs), np.uint32)
+    _chk(lib().forst_wal_record_crc_lengths(_p(log), log.nbytes, _p(offs), _p(lens), len(offs),
+                                            int(recyclable), int(write_in_place), _p(out), None))
     return out, log
 
 

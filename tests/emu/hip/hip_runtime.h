@@ -161,6 +161,36 @@ inline unsigned long long __ballot(int pred) {
   return m;
 }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+// v_mbcnt_lo / hi: acc + the bits of mask below this lane (lo: lanes 0..31 of
+// the mask, hi: lanes 32..63)
+inline uint32_t __builtin_amdgcn_mbcnt_lo(uint32_t m, uint32_t acc) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  return acc + static_cast<uint32_t>(__builtin_popcount(lane >= 32 ? m : m & ((1u << lane) - 1u)));
+}
+inline uint32_t __builtin_amdgcn_mbcnt_hi(uint32_t m, uint32_t acc) {
+  const uint32_t lane = emu::tl_tid.x & 63;
+  return acc + (lane < 32 ? 0u : static_cast<uint32_t>(__builtin_popcount(m & ((1u << (lane - 32)) - 1u))));
+}
+// ds_bpermute_b32 (pull): this lane reads lane (addr / 4) % 64's data
+inline int __builtin_amdgcn_ds_bpermute(int addr, int data) {
+  return static_cast<int>(emu::exchange(static_cast<uint32_t>(data),
+                                        (static_cast<uint32_t>(addr) >> 2) & 63u));
+}
+// ds_permute_b32 (push): lane (addr / 4) % 64 receives this lane's data; a
+// lane nobody writes gets 0 (callers here always form a permutation)
+inline int __builtin_amdgcn_ds_permute(int addr, int data) {
+  emu::Wave& w = emu::tl_group->waves[emu::tl_tid.x >> 6];
+  const uint32_t lane = emu::tl_tid.x & 63;
+  const uint32_t n = std::min<uint32_t>(64, emu::g_block.x - 64 * (emu::tl_tid.x >> 6));
+  w.slot[lane] = (static_cast<uint32_t>(addr) >> 2) & 63u;
+  w.bar->arrive_and_wait();
+  uint32_t src = 64;
+  for (uint32_t l = 0; l < n; ++l)
+    if (w.slot[l] == lane) src = l;
+  w.bar->arrive_and_wait();
+  const uint32_t v = emu::exchange(static_cast<uint32_t>(data), src < 64 ? src : lane);
+  return static_cast<int>(src < 64 ? v : 0u);
+}
 // DPP: row_shr:n (0x111..0x11f; lane i <- lane i-n in its row, else `old`)
 // and row_ror:n (0x121..0x12f; lane i <- lane (i-n) mod 16 of its row)
 inline uint32_t __builtin_amdgcn_update_dpp(uint32_t old, uint32_t src, int ctrl, int, int, bool) {
@@ -232,7 +262,9 @@ constexpr hipError_t hipErrorInvalidDevice = 101;
 constexpr hipError_t hipErrorInvalidValue = 1;
 enum hipMemcpyKind { hipMemcpyHostToDevice = 1, hipMemcpyDeviceToHost = 2, hipMemcpyDeviceToDevice = 3 };
 enum { hipMemAllocationTypePinned = 1, hipMemLocationTypeDevice = 1,
-       hipMemPoolAttrReleaseThreshold = 4 };
+       hipMemPoolAttrReleaseThreshold = 4, hipMemPoolReuseAllowOpportunistic = 2,
+       hipMemPoolReuseAllowInternalDependencies = 3 };
+typedef int hipMemPoolAttr;
 struct hipMemPoolProps {
   int allocType;
   int handleTypes;

@@ -394,3 +394,90 @@ def test_emu_rows_extra_dword_windows():
         b2, out = emu.block_trailer(t, base, offs, sizes, types)
         comp, st, ok, bad = emu.block_verify(t, b2, offs, sizes)
         assert bad == 0 and ok.all()
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_emu_raw_split_short_and_long(recyclable):
+    """Raw batches big enough for the global feed (>= 64 descriptors per wave
+    of the grid) are split by length (crc32c.hip FORST_RAW_SPLIT, 512 B):
+    shorter messages one per lane (crc32c_raw_lane_kernel), the rest on the
+    rows kernel, which drops the short ones from each batch as it loads it
+    (crc32c_rows_raw_filt_kernel).  Every length around the split, every start
+    alignment, per-message init, messages ending at the buffer end, and
+    out-of-range descriptors on both sides (one at an offset >= 2^58, whose
+    top bits the filter kernel reuses); then the WAL writer's lengths mode
+    and the reader's verify (only mismatching CRCs stored) on > 2048
+    physical records with corruptions in short and long ones."""
+    rng = np.random.default_rng(52 + int(recyclable))
+    n = 3000
+    sizes = rng.integers(0, 1500, n).astype(np.uint32)
+    sizes[:64] = 480 + np.arange(64)
+    sizes[64:80] = np.arange(16)
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + rng.integers(0, 4, n - 1).astype(np.uint64))
+    total = int(offs[-1]) + int(sizes[-1])
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    init = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32)
+    got = emu.crc32c(base, offs, sizes, init=init)
+    for k in range(n):
+        o, s = int(offs[k]), int(sizes[k])
+        assert int(got[k]) == O.crc32c_extend(int(init[k]), base[o:o + s]), (k, s, o & 3)
+    o2, s2 = offs.copy(), sizes.copy()
+    o2[5], s2[5] = total - 3, 10                 # short, past the end
+    o2[6], s2[6] = total - 100, 600              # long, past the end
+    o2[7], s2[7] = 1 << 59, 600                  # long, offset >= 2^58
+    o2[8], s2[8] = (1 << 58) - 1, 700            # long, just below 2^58
+    o2[9], s2[9] = total - 509, 509              # short, ends at the buffer end
+    o2[10], s2[10] = total - 1300, 1300          # long, ends at the buffer end
+    got = emu.crc32c(base, o2, s2)
+    for k in range(n):
+        o, s = int(o2[k]), int(s2[k])
+        want = 0 if k in (5, 6, 7, 8) else O.crc32c_extend(0, base[o:o + s])
+        assert int(got[k]) == want, (k, o, s)
+    # the WAL on both sides of the split
+    lens = rng.integers(0, 1200, 2500).astype(np.uint32)
+    lens[:30] = 505 - np.arange(30) % 12
+    payload = rng.integers(0, 256, int(lens.astype(np.int64).sum()), dtype=np.uint8)
+    buf, poffs, plens = O.wal_frame(payload, lens, recyclable=recyclable, log_number=5)
+    assert len(poffs) > 2048
+    w = buf.copy()
+    for o in poffs:
+        w[int(o):int(o) + 4] = 0
+    crcs, img = emu.wal_record_crc_lengths(w, poffs, plens, recyclable=recyclable)
+    assert (img[:len(buf)] == buf).all()
+    assert (crcs == np.frombuffer(b"".join(buf[int(o):int(o) + 4].tobytes() for o in poffs),
+                                  np.uint32)).all()
+    b = buf.copy()
+    hs = 11 if recyclable else 7
+    short = [k for k in range(len(poffs)) if 0 < plens[k] < 400]
+    longr = [k for k in range(len(poffs)) if plens[k] > 900]
+    for k in (short[3], short[-2], longr[4], longr[-3]):
+        b[int(poffs[k]) + hs + int(plens[k]) // 2] ^= 0x08
+    got = emu.wal_verify(b, log_number=5)
+    ost = O.wal_verify_blocks(b, 5, nthreads=2)
+    for g, want in zip(got[:3], ost):
+        assert (np.asarray(g) == want).all()
+    assert got[3] == int(((ost[0] != 0) & (ost[0] != 3)).sum()) >= 2
+
+
+def test_emu_raw_split_sparse_long():
+    """A raw batch whose long messages are sparse -- one in ~150, as a WAL
+    recovery's raw list (short candidates plus a few irregular long records)
+    -- so the compacted descriptor batches hold fewer entries than a wave has
+    rows: rows wait for the next batch instead of skipping positions
+    (crc32c.hip FILT), every message computed once, results exact."""
+    rng = np.random.default_rng(77)
+    n = 9000
+    sizes = rng.integers(0, 200, n).astype(np.uint32)
+    longs = rng.choice(n, 60, replace=False)
+    sizes[longs] = rng.integers(256, 6000, len(longs))
+    sizes[:3] = [300, 0, 5000]
+    offs = np.zeros(n, np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 7)
+    total = int(offs[-1]) + int(sizes[-1]) + 7
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    got = emu.crc32c(base, offs, sizes)
+    want = np.array([O.crc32c_extend(0, base[int(o):int(o) + int(s)]) for o, s in zip(offs, sizes)],
+                    np.uint32)
+    bad = np.nonzero(got != want)[0]
+    assert len(bad) == 0, (len(bad), bad[:8].tolist(), sizes[bad[:8]].tolist())

@@ -688,6 +688,30 @@ def test_wal_record_xxh3_fragment_edges(recyclable):
 
 
 @pytest.mark.parametrize("recyclable", [False, True])
+def test_full_size_c5_writer_crc(recyclable):
+    """C5 at full size, the writer's CRC of EVERY physical record (11.4 M,
+    log_writer.cc:228-263), both entry points (header offsets; the writer's
+    payload lengths), not written in place, against the CRCs the oracle's
+    framing stored in the headers: no result store is skipped (the verify
+    path pre-fills its results with the stored CRCs, so only a pass that stores
+    every CRC shows a record the kernels never reached)"""
+    w = workload.make_wal_batch(10_000_000, workload.SEEDS["C5"], recyclable=recyclable,
+                                log_number=77)
+    o = torch.from_numpy(w.rec_offsets.view(np.int64)).to(DEV)
+    stored = (w.log[(o[:, None] + torch.arange(4, device=DEV)[None, :]).reshape(-1)]
+              .reshape(-1, 4).to(torch.int64))
+    stored = host(stored[:, 0] | (stored[:, 1] << 8) | (stored[:, 2] << 16) | (stored[:, 3] << 24))
+    lens = w.rec_lengths
+    for kw in ({}, {"payload_lengths": d(lens.astype(np.int32)), "recyclable": recyclable}):
+        out = torch.full((len(w.rec_offsets),), 0x5A5A5A5A, dtype=torch.int32, device=DEV)
+        got = host(engine.wal_record_crc_batch(w.log, o, write_in_place=False, out=out,
+                                               **kw)).view(np.uint32)
+        bad = np.nonzero(got.astype(np.int64) != stored)[0]
+        assert len(bad) == 0, (len(bad), bad[:8].tolist(), lens[bad[:8]].tolist(),
+                               (got[bad[:8]] == 0x5A5A5A5A).tolist())
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
 def test_full_size_c5_record_xxh3(recyclable):
     """10 M logical records of C5 (legacy 7-byte and recyclable 11-byte
     headers): count, first fragments against the writer's layout, and EVERY

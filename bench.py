@@ -629,6 +629,9 @@ def _norm_kernel(name):
     modes = {"0": "compute", "1": "trailer", "2": "verify", "3": "raw"}
     n = name.replace("forst::(anonymous namespace)::", "").replace("void ", "")
     n = n.split("(forst::")[0].split("(unsigned")[0].strip()
+    # xxhash_lane_kernel<MODE, X64> (rocprof) -> xxhash32/64_lane_kernel<mode> (engine)
+    n = re.sub(r"^xxhash_lane_kernel<(\d), (true|false)>$",
+               lambda m: f"xxhash{64 if m.group(2) == 'true' else 32}_lane_kernel<{m.group(1)}>", n)
     return re.sub(r"<(\d)>", lambda m: "<" + modes[m.group(1)] + ">", n)
 
 

@@ -2286,6 +2286,14 @@ CrcKernel diag_crc_kernel(CrcKernel k, int mode) {
 
 }  // namespace
 
+// raw CRCs of messages all under kRawSplit bytes: the lane kernel alone (a
+// longer one would be left out: the caller guarantees the lengths)
+hipError_t launch_crc32c_raw_lanes(const BlockArgs& a, hipStream_t stream) {
+  if (a.n == 0) return hipSuccess;
+  if (kRawSplit < 256) return hipErrorInvalidValue;
+  return launch_kernel(crc32c_raw_lane_kernel, 2 * device_info().num_cus, kLaneThreads, a, stream);
+}
+
 hipError_t launch_crc32c_blocks(int mode, const BlockArgs& a, hipStream_t stream,
                                 const char** name) {
   const DeviceInfo& di = device_info();

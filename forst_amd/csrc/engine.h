@@ -182,6 +182,22 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
 // the fragment kernel with every physical record's CRC32C checked from the
 // same loads (wal_recover.hip): long records (> 240 B) only
 hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const char** kernel_name);
+// WAL recovery's short candidates (one fragment, <= 240 B) off the fused
+// kernel: their CRC on the raw path's lane kernel, their XXH3 one per lane
+// (launch_xxh3_short_sel), both ahead of the fused kernel, which is then
+// built for records > 240 B only (1); or in the fused kernel's rows (0)
+#ifndef FORST_REC_SHORT
+#define FORST_REC_SHORT 1
+#endif
+// XXH3_64bits of inputs of at most 240 bytes, one per 16-lane row: for
+// k < n, out[idx ? idx[k] : k] = XXH3(base + off[k], len[k]); a longer or
+// out-of-range input gives 0
+hipError_t launch_xxh3_short_rows(const uint8_t* base, uint64_t base_len, const uint64_t* off,
+                                  const uint32_t* len, uint64_t n, const uint64_t* idx,
+                                  uint64_t* out, hipStream_t stream);
+// raw CRC32C (crc32c::Value) of messages all under 256 bytes, one per lane
+// (crc32c.hip crc32c_raw_lane_kernel): offsets / sizes / out32 as in raw mode
+hipError_t launch_crc32c_raw_lanes(const BlockArgs& a, hipStream_t stream);
 hipError_t launch_noop_blocks(int mode, const BlockArgs& a,
                               hipStream_t stream, const char** kernel_name);
 // kxxHash (x64 = false, XXH32) / kxxHash64 (x64 = true, Lower32 of XXH64)

@@ -393,14 +393,23 @@ __device__ __forceinline__ void cand_one(const RecoverArgs& a, uint64_t ni, uint
   // (the fused kernel loads whole 1 KiB windows, and 32 bytes from a short
   // record's chunk: engine.h kFragTail)
   if (prev_end + kFragTail > a.log_len) ok = false;
+  // with the short path the fused kernel takes records over 240 B only: a
+  // shorter run of several items (an empty First, then one fragment) is left
+  // to the raw path and hash_logical_records
+  if (FORST_REC_SHORT && total <= 240 && t0 != 1) ok = false;
   if (!ok) return;
   if (nz == 0) start = it_off[i] + hs;
-  c.head[i] = 1;
+  // a short candidate (head 2, a Full record): its CRC by the lane kernel,
+  // its hash by xxh3_short_rows_kernel into ez[i] (no E / Z: the fused kernel
+  // never sees it), both from the short list (rw_cand_flags_kernel)
+  const bool shrt = FORST_REC_SHORT && total <= 240;
+  c.head[i] = shrt ? 2 : 1;
   c.p0[i] = start;
   c.len[i] = static_cast<uint32_t>(total);
   c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
   c.first[i] = static_cast<uint32_t>(first);
   c.last[i] = static_cast<uint32_t>(q);
+  if (shrt) return;
   // E / Z of every non-empty fragment (xxh3.hip, the fused CRC): E = H moved
   // from the fragment start to the end of its first window, Z = ~stored moved
   // from the fragment end to the end of its last window (windows of kFragWinFused)
@@ -437,19 +446,36 @@ __global__ void __launch_bounds__(kCandThreads) rw_cand_kernel(RecoverArgs a, ui
     cand_one(a, ni, i, it_off, it_old, ipack, crc_stored, c, T);
 }
 
-// compact lists: candidates (item order) and the physical records the rows
-// kernel CRCs (not fused)
+// the short candidates' list (item order): the CRC'd bytes (header[6..hs) +
+// payload) for the lane CRC kernel, the payload for the one-per-lane XXH3
+struct ShortList {
+  uint64_t* item;
+  uint64_t* off;
+  uint32_t* len;
+  uint64_t* p0;
+  uint32_t* plen;
+  uint32_t* computed;
+};
+
+// compact lists: candidates (fused, item order), short candidates and the
+// physical records the rows kernel CRCs.  Packed (ni < 2^32): fc = candidate
+// | short << 32, one scan for both positions; else fc, fs apart
 __global__ void __launch_bounds__(kLanes) rw_cand_flags_kernel(const Cand c, uint64_t ni,
                                                                const uint8_t* it_old,
-                                                               uint64_t* fc, uint64_t* fr) {
+                                                               uint64_t* fc, uint64_t* fr,
+                                                               uint64_t* fs) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
-  const uint64_t r = c.fused[i] || it_old[i] ? 0u : 1u;  // (skipped old records need no CRC)
-  if (fr) {
-    fc[i] = c.head[i];
-    fr[i] = r;
+  const uint8_t hd = c.head[i];
+  const uint64_t sh = hd == 2 ? 1u : 0u;
+  // (skipped old records need no CRC; short candidates take the lane kernel's)
+  fr[i] = c.fused[i] || it_old[i] || sh ? 0u : 1u;
+  const uint64_t h = hd == 1 ? 1u : 0u;
+  if (fs) {
+    fc[i] = h;
+    fs[i] = sh;
   } else {
-    fc[i] = c.head[i] | (r << 32);  // both flags in one word: one scan (ni < 2^32)
+    fc[i] = h | (sh << 32);
   }
 }
 
@@ -457,23 +483,32 @@ __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint
                                                               const uint8_t* it_old,
                                                               const uint64_t* cpos,
                                                               const uint64_t* rpos,
+                                                              const uint64_t* spos,
                                                               const uint64_t* crc_off,
                                                               const uint32_t* crc_len,
                                                               uint64_t* l_p0, uint32_t* l_len,
                                                               uint32_t* l_info, uint32_t* l_first,
                                                               uint64_t* r_off, uint32_t* r_len,
-                                                              uint64_t* r_item) {
+                                                              uint64_t* r_item, ShortList sl) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
-  if (c.head[i]) {
-    const uint64_t k = rpos ? cpos[i] : cpos[i] & 0xffffffffu;
+  const uint8_t hd = c.head[i];
+  if (hd == 1) {
+    const uint64_t k = spos ? cpos[i] : cpos[i] & 0xffffffffu;
     l_p0[k] = c.p0[i];
     l_len[k] = c.len[i];
     l_info[k] = c.info[i];
     l_first[k] = c.first[i];
+  } else if (hd == 2) {
+    const uint64_t k = spos ? spos[i] : cpos[i] >> 32;
+    sl.item[k] = i;
+    sl.off[k] = crc_off[i];
+    sl.len[k] = crc_len[i];
+    sl.p0[k] = c.p0[i];
+    sl.plen[k] = c.len[i];
   }
-  if (!c.fused[i] && !it_old[i]) {
-    const uint64_t k = rpos ? rpos[i] : cpos[i] >> 32;
+  if (!c.fused[i] && !it_old[i] && hd != 2) {
+    const uint64_t k = rpos[i];
     r_off[k] = crc_off[i];
     r_len[k] = crc_len[i];
     r_item[k] = i;
@@ -1128,8 +1163,10 @@ __global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const
   bool m = c.head != nullptr && hb[j] == h && (t.kind[h] == kTkFull || t.kind[h] == kTkFirst);
   if (m) {
     const uint64_t ih = t.item[h];
-    m = c.head[ih] && c.last[ih] == t.item[i];
-    if (m) hash_out[j] = cand_hash[cpos[ih] & cmask];  // (cmask: cpos packed with rpos)
+    const uint8_t hd = c.head[ih];
+    m = hd && c.last[ih] == t.item[i];
+    // (cmask: cpos packed with rpos; a short candidate's hash is in its ez)
+    if (m) hash_out[j] = hd == 1 ? cand_hash[cpos[ih] & cmask] : c.ez[ih];
   }
   need[j] = m ? 0u : 1u;
 }
@@ -1202,6 +1239,7 @@ struct P1 {
 };
 
 constexpr uint64_t kCtlCap = 4096;
+constexpr uint64_t kRawFirst = 65536;  // raw list entries that go ahead of the fused kernel
 
 // phase-2 arrays (per item / token)
 struct P2 {
@@ -1213,6 +1251,8 @@ struct P2 {
   Cand c;
   uint64_t *fc, *fr, *cpos, *rpos, *l_p0, *cand_hash, *r_off, *r_item;
   uint32_t *l_len, *l_info, *l_first, *r_len;
+  ShortList sl;
+  uint64_t *fs, *spos;
   Tokens t;
   uint64_t *ntok, *tok_base, *head, *plen, *pl, *seg, *seg_head, *n_emit, *n_rep, *emit_at, *rep_at,
       *tiles2, *ctl_list;
@@ -1247,6 +1287,14 @@ struct P2 {
     l_info = A.take<uint32_t>(ni);
     l_first = A.take<uint32_t>(ni);
     r_len = A.take<uint32_t>(ni);
+    sl.item = A.take<uint64_t>(ni);
+    sl.off = A.take<uint64_t>(ni);
+    sl.len = A.take<uint32_t>(ni);
+    sl.p0 = A.take<uint64_t>(ni);
+    sl.plen = A.take<uint32_t>(ni);
+    sl.computed = A.take<uint32_t>(ni);
+    fs = A.take<uint64_t>(ni);
+    spos = A.take<uint64_t>(ni);
     t.kind = A.take<uint8_t>(nt);
     t.item = A.take<uint64_t>(nt);
     t.len = A.take<uint32_t>(nt);
@@ -1410,32 +1458,80 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       hipLaunchKernelGGL(rw_cand_kernel, dim3(static_cast<uint32_t>(cg < ncu ? cg : ncu)),
                          dim3(kCandThreads), 0, st, a, ni, q.it_off, q.it_old, q.ipack,
                          q.crc_stored, q.c);
-      // both flags packed in one word and scanned once when the counts fit
-      // 32 bits (one scan instead of two)
+      // the candidate and short-candidate flags packed in one word and
+      // scanned once when the counts fit 32 bits; the raw flags apart
       const bool packed = ni < (uint64_t(1) << 32);
       hipLaunchKernelGGL(rw_cand_flags_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni,
-                         q.it_old, q.fc, packed ? nullptr : q.fr);
+                         q.it_old, q.fc, q.fr, packed ? nullptr : q.fs);
       const uint64_t nti = (ni + kScanTile - 1) / kScanTile;
-      uint64_t cnt2[2] = {0, 0};
+      uint64_t cnt2[3] = {0, 0, 0};
       scan_u64(q.fc, ni, q.tiles2, q.cpos, st);
       e = hipMemcpyAsync(&cnt2[0], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
+      if (e == hipSuccess) e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
       if (!packed) {
-        scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
+        scan_u64(q.fs, ni, q.tiles2, q.spos, st);
         if (e == hipSuccess)
-          e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+          e = hipMemcpyAsync(&cnt2[2], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
       }
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (e != hipSuccess) return fail(e);
       if (packed) {
-        cnt2[1] = cnt2[0] >> 32;
+        cnt2[2] = cnt2[0] >> 32;
         cnt2[0] &= 0xffffffffu;
         cpos_mask = 0xffffffffu;
       }
+      const uint64_t n_short = cnt2[2];
       n_cand = cnt2[0];
       const uint64_t n_raw = cnt2[1];
       hipLaunchKernelGGL(rw_cand_list_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni, q.it_old,
-                         q.cpos, packed ? nullptr : q.rpos, q.crc_off, q.crc_len, q.l_p0, q.l_len, q.l_info,
-                         q.l_first, q.r_off, q.r_len, q.r_item);
+                         q.cpos, q.rpos, packed ? nullptr : q.spos, q.crc_off, q.crc_len, q.l_p0,
+                         q.l_len, q.l_info, q.l_first, q.r_off, q.r_len, q.r_item, q.sl);
+      // the raw path: the CRCs of the physical records the fused kernel does
+      // not check (the rows kernels' raw mode, then their verdicts), and the
+      // short candidates' XXH3 (their hash into ez[item])
+      auto raw_path = [&](hipStream_t rs) -> hipError_t {
+        BlockArgs cb{};
+        cb.base = log;
+        cb.base_len = log_len;
+        cb.offsets = q.r_off;
+        cb.sizes = q.r_len;
+        cb.out32 = q.computed;
+        cb.n = n_raw;
+        const char* crc_name = nullptr;
+        hipError_t r = launch_crc32c_blocks(kModeRaw, cb, rs, &crc_name);
+        if (r != hipSuccess) return r;
+        hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_raw), dim3(kLanes), 0, rs, q.r_item,
+                           q.computed, n_raw, q.crc_stored, q.crc_ok);
+        return hipGetLastError();
+      };
+      // crc_ok pre-filled with 0 (fail-closed): the fused kernel, the short
+      // list and the raw path store every verdict
+      if ((n_cand || n_raw || n_short) && (e = hipMemsetAsync(q.crc_ok, 0, ni, st)) != hipSuccess)
+        return fail(e);
+      // the short candidates (C5: 2.9 M Full records <= 240 B): CRC and XXH3
+      // one per lane, ahead of the fused kernel on its stream (on a second
+      // stream they would wait for the fused kernel's workgroups, which hold
+      // all of the CUs' LDS, and run in its tail)
+      if (n_short) {
+        BlockArgs sb{};
+        sb.base = log;
+        sb.base_len = log_len;
+        sb.offsets = q.sl.off;
+        sb.sizes = q.sl.len;
+        sb.out32 = q.sl.computed;
+        sb.n = n_short;
+        if ((e = launch_crc32c_raw_lanes(sb, st)) != hipSuccess) return fail(e);
+        hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_short), dim3(kLanes), 0, st, q.sl.item,
+                           q.sl.computed, n_short, q.crc_stored, q.crc_ok);
+        if ((e = launch_xxh3_short_rows(log, log_len, q.sl.p0, q.sl.plen, n_short, q.sl.item,
+                                         q.c.ez, st)) != hipSuccess)
+          return fail(e);
+      }
+      // a long raw list (corrupted or re-typed logs) goes ahead of the fused
+      // kernel too, for the same reason
+      const bool raw_first = n_raw >= kRawFirst;
+      if (raw_first && (e = raw_path(st)) != hipSuccess) return fail(e);
       if (n_cand) {
         BlockArgs fa{};
         fa.base = log;
@@ -1445,14 +1541,14 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         fa.init_crcs = q.l_info;
         fa.modifiers = q.l_first;
         fa.crc_ez = q.c.ez;
-        fa.crc_ok = q.crc_ok;  // pre-filled with 0 (fail-closed): the fused kernel stores every verdict
+        fa.crc_ok = q.crc_ok;
         fa.out64 = q.cand_hash;
         fa.n = n_cand;
-        if ((e = hipMemsetAsync(q.crc_ok, 0, ni, st)) != hipSuccess) return fail(e);
-        // the raw CRC of the other records does not depend on the fused
-        // kernel (disjoint items of crc_ok): on a second stream, forked after
-        // the memset, it runs in the fused kernel's launch tail
-        if (FORST_REC_OVERLAP && n_raw && (raw_aux = raw_hold.a = aux_acquire(st)) != nullptr &&
+        // a short raw list does not depend on the fused kernel (disjoint
+        // items of crc_ok and ez): on a second stream, forked after the
+        // memset, it runs in the fused kernel's launch tail
+        if (FORST_REC_OVERLAP && n_raw && !raw_first &&
+            (raw_aux = raw_hold.a = aux_acquire(st)) != nullptr &&
             (hipEventRecord(raw_aux->fork, st) != hipSuccess ||
              hipStreamWaitEvent(raw_aux->s, raw_aux->fork, 0) != hipSuccess)) {
           (void)hipGetLastError();
@@ -1461,20 +1557,9 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         const char* fname = nullptr;
         if ((e = launch_xxh3_frag_crc(fa, st, &fname)) != hipSuccess) return fail(e);
       }
-      if (n_raw) {
+      if (n_raw && !raw_first) {
         const hipStream_t rs = raw_aux ? raw_aux->s : st;
-        BlockArgs cb{};
-        cb.base = log;
-        cb.base_len = log_len;
-        cb.offsets = q.r_off;
-        cb.sizes = q.r_len;
-        cb.out32 = q.computed;
-        cb.n = n_raw;
-        const char* crc_name = nullptr;
-        e = launch_crc32c_blocks(kModeRaw, cb, rs, &crc_name);
-        if (e == hipSuccess)
-          hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_raw), dim3(kLanes), 0, rs, q.r_item,
-                             q.computed, n_raw, q.crc_stored, q.crc_ok);
+        e = raw_path(rs);
         // join (also on failure: the scratch is freed on st)
         if (raw_aux && (hipEventRecord(raw_aux->join, rs) != hipSuccess ||
                         hipStreamWaitEvent(st, raw_aux->join, 0) != hipSuccess)) {
@@ -1697,7 +1782,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     uint64_t* hsub = A5.take<uint64_t>(nr);
     uint64_t* tiles5 = A5.take<uint64_t>(nr / kScanTile + 2);
     Cand cm = q.c;
-    if (!n_cand) cm.head = nullptr;
+    if (!ni) cm.head = nullptr;
     uint64_t n_need = 0, over = 0;
     auto match = [&]() {
       hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,

@@ -47,9 +47,12 @@ constexpr uint32_t kXxStageW = 16384;
 // (profiles/ab_r05/c3s_block_cost_staging.log): C3 sorted by size (C3S)
 // verify 0.758 (0) -> 0.766 (512) / 0.760 (1536) / 0.748 (4096), shuffled
 // C3 0.7665 unchanged -- a range of 4 KiB blocks is slower per byte than one
-// of 64 KiB blocks
+// of 64 KiB blocks.  Round 5, after the staged results and the LDS keys
+// (profiles/ab_r05/c3s_block_cost.log, C3 and C3S on one box): C3S verify
+// 0.775 (128) / 0.787 (256) / 0.784 (512) / 0.782 (1024) / 0.780 (2048),
+// trailer 0.760 / 0.773 / 0.768 / 0.764 / 0.763; C3 0.789-0.790 at all three
 #ifndef FORST_XX_BLOCK_COST
-#define FORST_XX_BLOCK_COST 512
+#define FORST_XX_BLOCK_COST 256
 #endif
 // fused WAL recovery: one CRC chain per lane through its four chunks of a
 // window (1: a 240-byte hop between chunks, J244, so a fragment's finish
@@ -265,6 +268,86 @@ __device__ __forceinline__ uint64_t xxh3_short_row(uint64_t d0, uint64_t d1, uin
   // (an opaque zero: the folded constant, kept live across the callers'
   // loops, was a spilled register pair)
   return xxh64_avalanche(sec64(56) ^ sec64(64) ^ fresh(0u));
+}
+
+// ---- short inputs (<= 240 B), one per 16-lane row ---------------------------
+// Lane t of the row loads the 16-byte chunk of xxh3_short_row's layout
+// (short_phys: one dword-aligned 16-byte load and the dword after it), so a
+// row's loads are one contiguous stretch of the input, and the formula runs
+// from registers with DPP row sums.  (One input per lane, with every 16-byte
+// window of the input in that lane's registers, measured 0.23-0.56 ms for
+// C5's 2.9 M short records against this: its scattered per-lane loads were
+// address-bound.)  Bytes at or past base_len read as zero (byte loads, only
+// at the buffer end).  WAL recovery's short candidates (wal_recover.hip).
+__device__ __forceinline__ u32x4a4 ld16_lim(const uint8_t* base, uint64_t base_len, uint64_t a) {
+  u32x4a4 v{0u, 0u, 0u, 0u};
+#pragma unroll
+  for (uint32_t j = 0; j < 16; ++j)
+    if (a + j < base_len) v[j >> 2] |= ldu8(base + a + j) << (8 * (j & 3));
+  return v;
+}
+__device__ __forceinline__ uint32_t ld4_lim(const uint8_t* base, uint64_t base_len, uint64_t a) {
+  uint32_t v = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 4; ++j)
+    if (a + j < base_len) v |= ldu8(base + a + j) << (8 * j);
+  return v;
+}
+constexpr uint32_t kShortRowsThreads = 256;
+constexpr uint32_t kShortRowsU = 4;  // inputs per row in flight (loads issued together)
+__global__ void __launch_bounds__(kShortRowsThreads) xxh3_short_rows_kernel(
+    const uint8_t* base, uint64_t base_len, const uint64_t* off, const uint32_t* len, uint64_t n,
+    const uint64_t* idx, uint64_t* out) {
+  __shared__ uint64_t shsec[64];
+  short_secrets_fill(shsec, threadIdx.x);
+  __syncthreads();
+  const uint32_t lane = threadIdx.x & 63, t = lane & 15, row = lane >> 4;
+  const uint64_t wave = uniform(threadIdx.x >> 6);
+  constexpr uint64_t kPerWave = 4 * kShortRowsU;
+  const uint64_t step = kPerWave * gridDim.x * (kShortRowsThreads / 64);
+  for (uint64_t k0 = kPerWave * (static_cast<uint64_t>(blockIdx.x) * (kShortRowsThreads / 64) + wave);
+       k0 < n; k0 += step) {  // (wave-uniform: the row sums need every lane)
+    uint64_t P0[kShortRowsU];
+    uint32_t L[kShortRowsU];
+#pragma unroll
+    for (uint32_t u = 0; u < kShortRowsU; ++u) {
+      const uint64_t k = k0 + 4 * u + row;
+      P0[u] = k < n ? off[k] : 0ull;
+      L[u] = k < n ? len[k] : 0u;
+    }
+    u32x4a4 c[kShortRowsU];
+    uint32_t nx[kShortRowsU];
+    uint64_t ph[kShortRowsU];
+    bool ok[kShortRowsU];
+#pragma unroll
+    for (uint32_t u = 0; u < kShortRowsU; ++u) {
+      ok[u] = k0 + 4 * u + row < n && L[u] <= 240 && P0[u] <= base_len && L[u] <= base_len - P0[u];
+      ph[u] = ok[u] ? short_phys(P0[u], L[u], t) : 0ull;
+      const uint64_t q = ph[u] & ~3ull;
+      // (an address past the buffer end: bytes loaded one by one, taken
+      // after the other loads so the common path's loads stay together)
+      const uint64_t qf = q + 20 <= base_len ? q : 0ull;
+      c[u] = ld16_a4(base + qf);
+      nx[u] = ld4_a4(base + qf + 16);
+    }
+#pragma unroll
+    for (uint32_t u = 0; u < kShortRowsU; ++u) {
+      const uint64_t q = ph[u] & ~3ull;
+      if (q + 20 > base_len) {
+        c[u] = ld16_lim(base, base_len, q);
+        nx[u] = ld4_lim(base, base_len, q + 16);
+      }
+      const uint32_t m = static_cast<uint32_t>(ph[u] & 3);
+      const uint64_t d0 = mk64(__builtin_amdgcn_alignbyte(c[u].y, c[u].x, m),
+                               __builtin_amdgcn_alignbyte(c[u].z, c[u].y, m));
+      const uint64_t d1 = mk64(__builtin_amdgcn_alignbyte(c[u].w, c[u].z, m),
+                               __builtin_amdgcn_alignbyte(nx[u], c[u].w, m));
+      const uint32_t pb = ok[u] ? static_cast<uint32_t>(P0[u] - short_phys(P0[u], L[u], 0)) : 0u;
+      const uint64_t h = xxh3_short_row(d0, d1, L[u], t, pb, shsec);
+      const uint64_t k = k0 + 4 * u + row;
+      if (k < n && t == 0) out[idx ? idx[k] : k] = ok[u] ? h : 0ull;
+    }
+  }
 }
 
 struct LaneKeys {
@@ -1123,7 +1206,9 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const bool lng = valid && P.size > 240;
   const uint32_t nb = (P.size - 1) >> G::kShift;
   const uint32_t hs = P.hs();
-  const bool shrt = valid && !lng;  // one fragment (wal_hash.h gathers the others)
+  // one fragment (wal_hash.h gathers the others); the fused kernel's
+  // candidates are all longer (FORST_REC_SHORT: rw_cand_kernel)
+  const bool shrt = (!CRC || !FORST_REC_SHORT) && valid && !lng;
   // Chunk k of lane t sits at window offset 16 t + 256 k, logical offset
   // wpos + 16 t + 256 k.  All chunks of a lane share two physical frames: B
   // (before the window's fragment boundary) and B + hs (past it); their
@@ -1438,7 +1523,7 @@ xxh3_frag_kernel(BlockArgs a) {
       const uint32_t nn = __builtin_amdgcn_mov_dpp(cu.x[k + 1][0], 0x12F, 0xf, 0xf, true);
       cu.x[k][4] = t == 15 ? nn : nx;
     }
-    if (valid && !lng) cu.x[2][4] = cu.x[3][0];
+    if ((!CRC || !FORST_REC_SHORT) && valid && !lng) cu.x[2][4] = cu.x[3][0];
     // the chunk across the boundary (one lane per row, in ~1 step in 32):
     // its bytes before the boundary come from its own frame (aux), the rest
     // from the shifted frame (x), merged once, out of line, into that chunk's
@@ -1655,7 +1740,7 @@ xxh3_frag_kernel(BlockArgs a) {
         tm += quad_xor64<2>(tm);
         h = xxh3_avalanche(static_cast<uint64_t>(C.size) * P64_1 + tm);
       }
-      if (__ballot(fin && valid && !lng)) {  // short records: the row's chunks
+      if ((!CRC || !FORST_REC_SHORT) && __ballot(fin && valid && !lng)) {  // short records: the row's chunks
         uint64_t d0, d1;
         xx_words(cu.x[2], (fm >> 4) & 3u, d0, d1);
         const uint64_t P0 = C.off();
@@ -1959,6 +2044,19 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 #define FORST_FRAG_CRC_DEPTH 1
 #endif
   return launch_frag<FORST_FRAG_CRC_WPE, true, FORST_FRAG_CRC_DEPTH>(a, stream, name);
+}
+
+hipError_t launch_xxh3_short_rows(const uint8_t* base, uint64_t base_len, const uint64_t* off,
+                                  const uint32_t* len, uint64_t n, const uint64_t* idx,
+                                  uint64_t* out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (!base || !off || !len || !out) return hipErrorInvalidValue;
+  const uint64_t per_wg = 4 * kShortRowsU * (kShortRowsThreads / 64);
+  const uint32_t grid = static_cast<uint32_t>(
+      std::min<uint64_t>((n + per_wg - 1) / per_wg, uint64_t(device_info().num_cus) * 32));
+  hipLaunchKernelGGL(xxh3_short_rows_kernel, dim3(grid), dim3(kShortRowsThreads), 0, stream, base,
+                     base_len, off, len, n, idx, out);
+  return hipGetLastError();
 }
 
 hipError_t launch_xxh3_blocks(int mode, const BlockArgs& a, hipStream_t stream,

@@ -71,6 +71,47 @@ def test_recover_on_gpu(recyclable):
             compare(recs, reps, res, log, ln, mode, name)
 
 
+def _short_lengths_log(recyclable, reps, seed):
+    """Full records of every short length 0..240 (their XXH3 on the lane
+    kernel, xxh3_short_sel, their CRCs on the raw path), each length at
+    every payload alignment mod 4 over the repeats, between long records;
+    one record's type byte flipped (a CRC mismatch on the raw path)"""
+    rng = np.random.default_rng(seed)
+    lens = []
+    for r in range(reps):
+        sh = np.arange(241, dtype=np.uint32)
+        rng.shuffle(sh)
+        lens += list(sh[:120]) + [int(rng.integers(3000, 9000))] + list(sh[120:]) + [r % 7 + 1]
+    lens += [20000, 600]
+    log, po, pl = W.frame_lens(lens, seed, recyclable=recyclable)
+    short = [int(o) for o, l_ in zip(po, pl) if 0 < l_ <= 240 and (int(o) % 32768) < 32000]
+    log[short[len(short) // 2] + 6] ^= 0x01
+    return log
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_recover_short_lengths_on_emulator(recyclable):
+    E = _emu()
+    log = _short_lengths_log(recyclable, 2, 3)
+    recs, reps, res = E.wal_recover(log, 7, R.kPointInTimeRecovery)
+    compare(recs, reps, res, log, 7, R.kPointInTimeRecovery, "short")
+
+
+@pytest.mark.gpu
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_recover_short_lengths_on_gpu(recyclable):
+    """the same on the GPU, with enough short records (> 64 K raw-list
+    entries) that the raw path runs ahead of the fused kernel"""
+    import torch
+    from forst_amd import engine
+    log = _short_lengths_log(recyclable, 300, 4)
+    for mode in MODES:
+        rec, rep, res = engine.wal_recover_batch(torch.from_numpy(log).cuda(), 7, mode)
+        recs = [rec[k].cpu().numpy() for k in ("offset", "length", "hash", "n_fragments")]
+        reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
+        compare(recs, reps, res, log, 7, mode, "short")
+
+
 @pytest.mark.gpu
 def test_recover_c5_shape_with_corruption():
     """200 000 C5-shaped records (log-uniform 32 B-32 KiB) from the writer

@@ -189,6 +189,13 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 #ifndef FORST_REC_SHORT
 #define FORST_REC_SHORT 1
 #endif
+// ... and the Full records of one fused window (<= kFragWinFused bytes) in a
+// fused-kernel launch of their own, ahead of the long records (1): measured
+// and not kept (C5 recovery 17.38 -> 17.61 ms, the two launches' fused time
+// 13.74 -> 13.80 ms: profiles/ab_r05/recovery_short_candidates.log)
+#ifndef FORST_REC_MED
+#define FORST_REC_MED 0
+#endif
 // XXH3_64bits of inputs of at most 240 bytes, one per 16-lane row: for
 // k < n, out[idx ? idx[k] : k] = XXH3(base + off[k], len[k]); a longer or
 // out-of-range input gives 0

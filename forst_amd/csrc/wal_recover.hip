@@ -403,7 +403,8 @@ __device__ __forceinline__ void cand_one(const RecoverArgs& a, uint64_t ni, uint
   // its hash by xxh3_short_rows_kernel into ez[i] (no E / Z: the fused kernel
   // never sees it), both from the short list (rw_cand_flags_kernel)
   const bool shrt = FORST_REC_SHORT && total <= 240;
-  c.head[i] = shrt ? 2 : 1;
+  const bool one = FORST_REC_MED && t0 == 1 && total <= kFragWinFused;  // one window
+  c.head[i] = shrt ? 2 : one ? 3 : 1;
   c.p0[i] = start;
   c.len[i] = static_cast<uint32_t>(total);
   c.info[i] = multi ? (hs | ((nz - 1) << 8)) : 0u;
@@ -457,33 +458,34 @@ struct ShortList {
   uint32_t* computed;
 };
 
-// compact lists: candidates (fused, item order), short candidates and the
-// physical records the rows kernel CRCs.  Packed (ni < 2^32): fc = candidate
-// | short << 32, one scan for both positions; else fc, fs apart
+// compact lists, item order: the fused kernel's candidates -- long ones
+// (head 1) and one-window Full records (head 3, FORST_REC_MED), launched
+// apart -- the short candidates (head 2) and the physical records the rows
+// kernel CRCs.  Candidates exist only when ni < 2^32 (RecoverArgs::fuse), so
+// two packed scans give all four positions: fc = long | one-window << 32,
+// fr = short | raw << 32 (else fr = raw alone, 64-bit)
 __global__ void __launch_bounds__(kLanes) rw_cand_flags_kernel(const Cand c, uint64_t ni,
-                                                               const uint8_t* it_old,
-                                                               uint64_t* fc, uint64_t* fr,
-                                                               uint64_t* fs) {
+                                                               const uint8_t* it_old, int packed,
+                                                               uint64_t* fc, uint64_t* fr) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
   const uint8_t hd = c.head[i];
   const uint64_t sh = hd == 2 ? 1u : 0u;
   // (skipped old records need no CRC; short candidates take the lane kernel's)
-  fr[i] = c.fused[i] || it_old[i] || sh ? 0u : 1u;
-  const uint64_t h = hd == 1 ? 1u : 0u;
-  if (fs) {
-    fc[i] = h;
-    fs[i] = sh;
+  const uint64_t r = c.fused[i] || it_old[i] || sh ? 0u : 1u;
+  if (packed) {
+    fc[i] = (hd == 1 ? 1u : 0u) | (static_cast<uint64_t>(hd == 3 ? 1u : 0u) << 32);
+    fr[i] = sh | (r << 32);
   } else {
-    fc[i] = h | (sh << 32);
+    fr[i] = r;
   }
 }
 
 __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint64_t ni,
-                                                              const uint8_t* it_old,
+                                                              const uint8_t* it_old, int packed,
+                                                              uint64_t n_long,
                                                               const uint64_t* cpos,
                                                               const uint64_t* rpos,
-                                                              const uint64_t* spos,
                                                               const uint64_t* crc_off,
                                                               const uint32_t* crc_len,
                                                               uint64_t* l_p0, uint32_t* l_len,
@@ -492,15 +494,15 @@ __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint
                                                               uint64_t* r_item, ShortList sl) {
   const uint64_t i = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
   if (i >= ni) return;
-  const uint8_t hd = c.head[i];
-  if (hd == 1) {
-    const uint64_t k = spos ? cpos[i] : cpos[i] & 0xffffffffu;
+  const uint8_t hd = packed ? c.head[i] : 0;
+  if (hd == 1 || hd == 3) {  // the one-window records after the long ones
+    const uint64_t k = hd == 1 ? (cpos[i] & 0xffffffffu) : n_long + (cpos[i] >> 32);
     l_p0[k] = c.p0[i];
     l_len[k] = c.len[i];
     l_info[k] = c.info[i];
     l_first[k] = c.first[i];
   } else if (hd == 2) {
-    const uint64_t k = spos ? spos[i] : cpos[i] >> 32;
+    const uint64_t k = rpos[i] & 0xffffffffu;
     sl.item[k] = i;
     sl.off[k] = crc_off[i];
     sl.len[k] = crc_len[i];
@@ -508,7 +510,7 @@ __global__ void __launch_bounds__(kLanes) rw_cand_list_kernel(const Cand c, uint
     sl.plen[k] = c.len[i];
   }
   if (!c.fused[i] && !it_old[i] && hd != 2) {
-    const uint64_t k = rpos[i];
+    const uint64_t k = packed ? rpos[i] >> 32 : rpos[i];
     r_off[k] = crc_off[i];
     r_len[k] = crc_len[i];
     r_item[k] = i;
@@ -1153,7 +1155,7 @@ struct RecFrags {
 __global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const uint64_t* hb,
                                                           const uint64_t* lt, uint64_t nr,
                                                           const Cand c, const uint64_t* cpos,
-                                                          uint64_t cmask,
+                                                          uint64_t n_long,
                                                           const uint64_t* cand_hash,
                                                           uint64_t* hash_out, uint64_t* need) {
   const uint64_t j = static_cast<uint64_t>(blockIdx.x) * kLanes + threadIdx.x;
@@ -1165,8 +1167,11 @@ __global__ void __launch_bounds__(kLanes) rw_match_kernel(Tokens t, Fsm f, const
     const uint64_t ih = t.item[h];
     const uint8_t hd = c.head[ih];
     m = hd && c.last[ih] == t.item[i];
-    // (cmask: cpos packed with rpos; a short candidate's hash is in its ez)
-    if (m) hash_out[j] = hd == 1 ? cand_hash[cpos[ih] & cmask] : c.ez[ih];
+    // (cpos: long | one-window positions; a short candidate's hash is in its ez)
+    if (m)
+      hash_out[j] = hd == 1   ? cand_hash[cpos[ih] & 0xffffffffu]
+                    : hd == 3 ? cand_hash[n_long + (cpos[ih] >> 32)]
+                              : c.ez[ih];
   }
   need[j] = m ? 0u : 1u;
 }
@@ -1252,7 +1257,7 @@ struct P2 {
   uint64_t *fc, *fr, *cpos, *rpos, *l_p0, *cand_hash, *r_off, *r_item;
   uint32_t *l_len, *l_info, *l_first, *r_len;
   ShortList sl;
-  uint64_t *fs, *spos;
+
   Tokens t;
   uint64_t *ntok, *tok_base, *head, *plen, *pl, *seg, *seg_head, *n_emit, *n_rep, *emit_at, *rep_at,
       *tiles2, *ctl_list;
@@ -1293,8 +1298,6 @@ struct P2 {
     sl.p0 = A.take<uint64_t>(ni);
     sl.plen = A.take<uint32_t>(ni);
     sl.computed = A.take<uint32_t>(ni);
-    fs = A.take<uint64_t>(ni);
-    spos = A.take<uint64_t>(ni);
     t.kind = A.take<uint8_t>(nt);
     t.item = A.take<uint64_t>(nt);
     t.len = A.take<uint32_t>(nt);
@@ -1442,7 +1445,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint64_t n_cand = 0;
   AuxHold raw_hold;  // second stream of the raw CRC (beside the fused kernel)
   AuxStream* raw_aux = nullptr;
-  uint64_t cpos_mask = ~0ull;  // 0xffffffff when cpos holds the packed positions
+  uint64_t n_long = 0;  // candidates [0, n_long) long, then the one-window ones
   if (nb) {
     hipLaunchKernelGGL(rw_fill_kernel, grid_for(nb), dim3(kLanes), 0, st, a, q1.ibase, q1.cnt,
                        q.it_off,
@@ -1458,34 +1461,26 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       hipLaunchKernelGGL(rw_cand_kernel, dim3(static_cast<uint32_t>(cg < ncu ? cg : ncu)),
                          dim3(kCandThreads), 0, st, a, ni, q.it_off, q.it_old, q.ipack,
                          q.crc_stored, q.c);
-      // the candidate and short-candidate flags packed in one word and
-      // scanned once when the counts fit 32 bits; the raw flags apart
-      const bool packed = ni < (uint64_t(1) << 32);
+      const bool packed = ni < (uint64_t(1) << 32);  // (a.fuse implies it)
       hipLaunchKernelGGL(rw_cand_flags_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni,
-                         q.it_old, q.fc, q.fr, packed ? nullptr : q.fs);
+                         q.it_old, packed ? 1 : 0, q.fc, q.fr);
       const uint64_t nti = (ni + kScanTile - 1) / kScanTile;
-      uint64_t cnt2[3] = {0, 0, 0};
-      scan_u64(q.fc, ni, q.tiles2, q.cpos, st);
-      e = hipMemcpyAsync(&cnt2[0], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      uint64_t cnt2[2] = {0, 0};
+      if (packed) {
+        scan_u64(q.fc, ni, q.tiles2, q.cpos, st);
+        e = hipMemcpyAsync(&cnt2[0], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
+      }
       scan_u64(q.fr, ni, q.tiles2, q.rpos, st);
       if (e == hipSuccess) e = hipMemcpyAsync(&cnt2[1], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
-      if (!packed) {
-        scan_u64(q.fs, ni, q.tiles2, q.spos, st);
-        if (e == hipSuccess)
-          e = hipMemcpyAsync(&cnt2[2], q.tiles2 + nti, 8, hipMemcpyDeviceToHost, st);
-      }
       if (e == hipSuccess) e = hipStreamSynchronize(st);
       if (e != hipSuccess) return fail(e);
-      if (packed) {
-        cnt2[2] = cnt2[0] >> 32;
-        cnt2[0] &= 0xffffffffu;
-        cpos_mask = 0xffffffffu;
-      }
-      const uint64_t n_short = cnt2[2];
-      n_cand = cnt2[0];
-      const uint64_t n_raw = cnt2[1];
+      n_long = packed ? cnt2[0] & 0xffffffffu : 0;
+      const uint64_t n_one = packed ? cnt2[0] >> 32 : 0;
+      const uint64_t n_short = packed ? cnt2[1] & 0xffffffffu : 0;
+      const uint64_t n_raw = packed ? cnt2[1] >> 32 : cnt2[1];
+      n_cand = n_long + n_one;
       hipLaunchKernelGGL(rw_cand_list_kernel, grid_for(ni), dim3(kLanes), 0, st, q.c, ni, q.it_old,
-                         q.cpos, q.rpos, packed ? nullptr : q.spos, q.crc_off, q.crc_len, q.l_p0,
+                         packed ? 1 : 0, n_long, q.cpos, q.rpos, q.crc_off, q.crc_len, q.l_p0,
                          q.l_len, q.l_info, q.l_first, q.r_off, q.r_len, q.r_item, q.sl);
       // the raw path: the CRCs of the physical records the fused kernel does
       // not check (the rows kernels' raw mode, then their verdicts), and the
@@ -1543,7 +1538,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         fa.crc_ez = q.c.ez;
         fa.crc_ok = q.crc_ok;
         fa.out64 = q.cand_hash;
-        fa.n = n_cand;
+        fa.n = n_long;
         // a short raw list does not depend on the fused kernel (disjoint
         // items of crc_ok and ez): on a second stream, forked after the
         // memset, it runs in the fused kernel's launch tail
@@ -1555,6 +1550,19 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
           raw_aux = nullptr;
         }
         const char* fname = nullptr;
+        // the one-window records in a launch of their own: every row then
+        // finishes its record in every step, where among long records a
+        // finishing row costs the whole wave the finish code
+        if (n_one) {
+          BlockArgs fo = fa;
+          fo.offsets = q.l_p0 + n_long;
+          fo.sizes = q.l_len + n_long;
+          fo.init_crcs = q.l_info + n_long;
+          fo.modifiers = q.l_first + n_long;
+          fo.out64 = q.cand_hash + n_long;
+          fo.n = n_one;
+          if ((e = launch_xxh3_frag_crc(fo, st, &fname)) != hipSuccess) return fail(e);
+        }
         if ((e = launch_xxh3_frag_crc(fa, st, &fname)) != hipSuccess) return fail(e);
       }
       if (n_raw && !raw_first) {
@@ -1786,7 +1794,7 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
     uint64_t n_need = 0, over = 0;
     auto match = [&]() {
       hipLaunchKernelGGL(rw_match_kernel, grid_for(nr), dim3(kLanes), 0, st, t, f, hash_begin,
-                         last_tok, nr, cm, q.cpos, cpos_mask, q.cand_hash, full.hash, need);
+                         last_tok, nr, cm, q.cpos, n_long, q.cand_hash, full.hash, need);
       scan_u64(need, nr, tiles5, npos, st);
       hipError_t r = hipMemcpyAsync(&n_need, tiles5 + (nr + kScanTile - 1) / kScanTile, 8,
                                     hipMemcpyDeviceToHost, st);

@@ -193,6 +193,12 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 // fused-kernel launch of their own, ahead of the long records (1): measured
 // and not kept (C5 recovery 17.38 -> 17.61 ms, the two launches' fused time
 // 13.74 -> 13.80 ms: profiles/ab_r05/recovery_short_candidates.log)
+// ... their CRC and XXH3 in one pass over the short list, on 16-lane rows
+// (launch_wal_short_rows: 1), or the lane CRC kernel and the XXH3 rows
+// kernel apart (0)
+#ifndef FORST_REC_SHORT_ROWS
+#define FORST_REC_SHORT_ROWS 1
+#endif
 #ifndef FORST_REC_MED
 #define FORST_REC_MED 0
 #endif
@@ -202,6 +208,14 @@ hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const ch
 hipError_t launch_xxh3_short_rows(const uint8_t* base, uint64_t base_len, const uint64_t* off,
                                   const uint32_t* len, uint64_t n, const uint64_t* idx,
                                   uint64_t* out, hipStream_t stream);
+// WAL recovery's short candidates, one per 16-lane row: for k < n,
+// crc_ok[item[k]] = (crc32c::Value(base + coff[k], clen[k]) ==
+// stored[item[k]]) and hash_out[item[k]] = XXH3(base + p0[k], plen[k])
+// (clen <= 252, plen <= 240)
+hipError_t launch_wal_short_rows(const uint8_t* base, uint64_t base_len, const uint64_t* coff,
+                                 const uint32_t* clen, const uint64_t* p0, const uint32_t* plen,
+                                 const uint64_t* item, uint64_t n, const uint32_t* stored,
+                                 uint8_t* crc_ok, uint64_t* hash_out, hipStream_t stream);
 // raw CRC32C (crc32c::Value) of messages all under 256 bytes, one per lane
 // (crc32c.hip crc32c_raw_lane_kernel): offsets / sizes / out32 as in raw mode
 hipError_t launch_crc32c_raw_lanes(const BlockArgs& a, hipStream_t stream);

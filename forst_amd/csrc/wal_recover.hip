@@ -1509,6 +1509,13 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
       // stream they would wait for the fused kernel's workgroups, which hold
       // all of the CUs' LDS, and run in its tail)
       if (n_short) {
+#if FORST_REC_SHORT_ROWS
+        // both on 16-lane rows, one pass over the list (xxh3.hip)
+        if ((e = launch_wal_short_rows(log, log_len, q.sl.off, q.sl.len, q.sl.p0, q.sl.plen,
+                                       q.sl.item, n_short, q.crc_stored, q.crc_ok, q.c.ez, st)) !=
+            hipSuccess)
+          return fail(e);
+#else
         BlockArgs sb{};
         sb.base = log;
         sb.base_len = log_len;
@@ -1520,8 +1527,9 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
         hipLaunchKernelGGL(rw_raw_ok_kernel, grid_for(n_short), dim3(kLanes), 0, st, q.sl.item,
                            q.sl.computed, n_short, q.crc_stored, q.crc_ok);
         if ((e = launch_xxh3_short_rows(log, log_len, q.sl.p0, q.sl.plen, n_short, q.sl.item,
-                                         q.c.ez, st)) != hipSuccess)
+                                        q.c.ez, st)) != hipSuccess)
           return fail(e);
+#endif
       }
       // a long raw list (corrupted or re-typed logs) goes ahead of the fused
       // kernel too, for the same reason

@@ -1352,6 +1352,160 @@ __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
     if (tid + k * NT < 18 * 1024) L[kFcOffA16 / 4 + tid + k * NT] = v2[k];
 }
 
+// ---- WAL recovery's short candidates: CRC32C and XXH3 on one 16-lane row --
+// One record per row (wal_recover.hip's short list: CRC'd bytes under 253,
+// payload <= 240).  CRC: the message right-aligned in a 256-byte window
+// behind the 4 bytes P with raw_0(P) = ~0 (so the window's raw CRC from 0 is
+// crc32c's value with its init) and zeros; lane t holds window bytes
+// [16 t, 16 t + 16): its raw chunk CRC (16 G lookups) moved to the window
+// end (A16[14 - t], the fused kernel's tables), then a DPP XOR over the row.
+// XXH3: the chunk of xxh3_short_row's layout, as xxh3_short_rows_kernel.
+// A record within 32 bytes of the log start (whose window would begin before
+// the buffer) or near its end is CRC'd byte by byte by lane 0 of its row.
+constexpr uint32_t kShortCrcThreads = 1024;  // one workgroup per CU: 136 KiB of tables
+constexpr uint32_t kShortCrcU = 2;           // records per row in flight
+constexpr uint32_t kCrcInitPrefix = 0x641f6454u;  // P, little-endian: raw CRC from 0 = 0xffffffff
+__device__ __forceinline__ uint32_t fcrc_chunk_raw(const uint8_t* __restrict__ Lb,
+                                                   const fcrc::Lanes& K, uint32_t w0, uint32_t w1,
+                                                   uint32_t w2, uint32_t w3) {
+  uint32_t l[4];
+  fcrc::look<false>(Lb, K, w0, l);
+  uint32_t x = fcrc::xor3(l[0], l[1], fcrc::xor3(l[2], l[3], w1));
+  x = fcrc::g_then(Lb, K, x, w2);
+  x = fcrc::g_then(Lb, K, x, w3);
+  return fcrc::g_then(Lb, K, x, 0u);
+}
+__global__ void __launch_bounds__(kShortCrcThreads) wal_short_rows_kernel(
+    const uint8_t* base, uint64_t base_len, const uint64_t* coff, const uint32_t* clen,
+    const uint64_t* p0, const uint32_t* plen, const uint64_t* item, uint64_t n,
+    const uint32_t* stored, uint8_t* crc_ok, uint64_t* hash_out) {
+  __shared__ uint32_t crcL[kFcLds / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t kmask[17 * 4];
+  __shared__ uint64_t shsec[64];
+  fill_frag_crc_tables<kShortCrcThreads>(crcL);
+  if (threadIdx.x < 17 * 4) kmask[threadIdx.x] = fcrc::keep_word(threadIdx.x >> 2, threadIdx.x & 3);
+  short_secrets_fill(shsec, threadIdx.x);
+  __syncthreads();
+  const uint8_t* Lb = reinterpret_cast<const uint8_t*>(crcL);
+  const uint32_t lane = threadIdx.x & 63, t = lane & 15, row = lane >> 4;
+  const uint64_t wave = uniform(threadIdx.x >> 6);
+  const fcrc::Lanes FK = fcrc::lanes(lane);
+  constexpr uint64_t kPerWave = 4 * kShortCrcU;
+  const uint64_t step = kPerWave * gridDim.x * (kShortCrcThreads / 64);
+  // the list entries of the next round are loaded while this round's data
+  // loads are in flight (one memory round trip per round, not two)
+  uint64_t co[kShortCrcU], pp[kShortCrcU], it[kShortCrcU];
+  uint32_t cl[kShortCrcU], pl[kShortCrcU];
+  auto load_list = [&](uint64_t kb) {
+#pragma unroll
+    for (uint32_t u = 0; u < kShortCrcU; ++u) {
+      const uint64_t k = kb + 4 * u + row;
+      const bool v = k < n;
+      co[u] = v ? coff[k] : 0ull;
+      cl[u] = v ? clen[k] : 0u;
+      pp[u] = v ? p0[k] : 0ull;
+      pl[u] = v ? plen[k] : 0u;
+      it[u] = v ? item[k] : 0ull;
+    }
+  };
+  uint64_t k0 = kPerWave * (static_cast<uint64_t>(blockIdx.x) * (kShortCrcThreads / 64) + wave);
+  load_list(k0);
+  for (; k0 < n; k0 += step) {  // (wave-uniform: the row sums need every lane)
+    u32x4a4 cc[kShortCrcU], xc[kShortCrcU];
+    uint32_t cn[kShortCrcU], xn[kShortCrcU], stv[kShortCrcU];
+    uint64_t ca[kShortCrcU], xp[kShortCrcU];
+    bool fast[kShortCrcU], ok[kShortCrcU];
+#pragma unroll
+    for (uint32_t u = 0; u < kShortCrcU; ++u) {
+      const uint64_t k = k0 + 4 * u + row;
+      ok[u] = k < n && pl[u] <= 240 && pp[u] <= base_len && pl[u] <= base_len - pp[u];
+      // CRC: window byte 16 t is message byte 16 t - s, s = 256 - clen
+      fast[u] = k < n && cl[u] <= 252 && co[u] >= 32 && co[u] <= base_len &&
+                base_len - co[u] >= uint64_t(cl[u]) + 4;
+      ca[u] = fast[u] ? co[u] + 16 * t - (256 - cl[u]) : 0ull;  // (>= co - 260 + 16 t)
+      const uint64_t cq = (fast[u] && 16 * t + 16 > 256 - cl[u] - 4) ? (ca[u] & ~3ull) : 0ull;
+      cc[u] = ld16_a4(base + cq);
+      cn[u] = ld4_a4(base + cq + 16);
+      // XXH3: the chunk of xxh3_short_row's layout
+      xp[u] = ok[u] ? short_phys(pp[u], pl[u], t) : 0ull;
+      const uint64_t xq = (xp[u] & ~3ull) + 20 <= base_len ? (xp[u] & ~3ull) : 0ull;
+      xc[u] = ld16_a4(base + xq);
+      xn[u] = ld4_a4(base + xq + 16);
+      stv[u] = k < n ? stored[it[u]] : 0u;
+    }
+    // this round's list values, then the next round's list loads
+    uint64_t co_[kShortCrcU], pp_[kShortCrcU], it_[kShortCrcU];
+    uint32_t cl_[kShortCrcU], pl_[kShortCrcU];
+#pragma unroll
+    for (uint32_t u = 0; u < kShortCrcU; ++u) {
+      co_[u] = co[u];
+      pp_[u] = pp[u];
+      it_[u] = it[u];
+      cl_[u] = cl[u];
+      pl_[u] = pl[u];
+    }
+    load_list(k0 + step);
+#pragma unroll
+    for (uint32_t u = 0; u < kShortCrcU; ++u) {
+      const uint64_t k = k0 + 4 * u + row;
+      // ---- CRC
+      const uint32_t sw = 256 - cl_[u];  // the message's window start
+      const bool live = fast[u] && 16 * t + 16 > sw - 4;
+      const uint32_t m = static_cast<uint32_t>(ca[u] & 3);
+      uint32_t w[4] = {__builtin_amdgcn_alignbyte(cc[u].y, cc[u].x, m),
+                       __builtin_amdgcn_alignbyte(cc[u].z, cc[u].y, m),
+                       __builtin_amdgcn_alignbyte(cc[u].w, cc[u].z, m),
+                       __builtin_amdgcn_alignbyte(cn[u], cc[u].w, m)};
+      const int32_t b0 = static_cast<int32_t>(sw) - static_cast<int32_t>(16 * t);
+      const uint32_t bk = live ? (b0 <= 0 ? 0u : (b0 >= 16 ? 16u : static_cast<uint32_t>(b0))) : 16u;
+      const u32x4 km = *reinterpret_cast<const u32x4*>(kmask + 4 * bk);
+      const int32_t o = b0 - 4;  // P's first byte in the lane's chunk
+      uint32_t pd[4];
+#pragma unroll
+      for (uint32_t i = 0; i < 4; ++i) {
+        const int32_t x = o - static_cast<int32_t>(4 * i) + 4;
+        pd[i] = live && x >= 0 && x < 8
+                    ? static_cast<uint32_t>((static_cast<uint64_t>(kCrcInitPrefix) << (8 * x)) >> 32)
+                    : 0u;
+      }
+      w[0] = (w[0] & ~km.x) | pd[0];
+      w[1] = (w[1] & ~km.y) | pd[1];
+      w[2] = (w[2] & ~km.z) | pd[2];
+      w[3] = (w[3] & ~km.w) | pd[3];
+      uint32_t v = fcrc_chunk_raw(Lb, FK, w[0], w[1], w[2], w[3]);
+      v = t == 15 ? v : fcrc::shift_at(Lb, kFcOffA16 + 4096 * (14 - t), v);
+      v = fcrc::row_ror_xor<1>(v);
+      v = fcrc::row_ror_xor<2>(v);
+      v = fcrc::row_ror_xor<4>(v);
+      v = fcrc::row_ror_xor<8>(v);
+      uint32_t crc = ~v;
+      if (k < n && !fast[u] && t == 0) {  // byte by byte (G3: table 3, copy 0)
+        uint32_t r = 0xffffffffu;
+        const uint64_t e = co_[u] + cl_[u];
+        for (uint64_t q = co_[u]; q < e && q < base_len; ++q)
+          r = (r >> 8) ^ fcrc::lds32(Lb, 256 * ((r ^ ldu8(base + q)) & 0xffu) + 96);
+        crc = co_[u] <= base_len && base_len - co_[u] >= cl_[u] ? ~r : ~stv[u];
+      }
+      // ---- XXH3
+      if ((xp[u] & ~3ull) + 20 > base_len) {
+        xc[u] = ld16_lim(base, base_len, xp[u] & ~3ull);
+        xn[u] = ld4_lim(base, base_len, (xp[u] & ~3ull) + 16);
+      }
+      const uint32_t xm = static_cast<uint32_t>(xp[u] & 3);
+      const uint64_t d0 = mk64(__builtin_amdgcn_alignbyte(xc[u].y, xc[u].x, xm),
+                               __builtin_amdgcn_alignbyte(xc[u].z, xc[u].y, xm));
+      const uint64_t d1 = mk64(__builtin_amdgcn_alignbyte(xc[u].w, xc[u].z, xm),
+                               __builtin_amdgcn_alignbyte(xn[u], xc[u].w, xm));
+      const uint32_t pb = ok[u] ? static_cast<uint32_t>(pp_[u] - short_phys(pp_[u], pl_[u], 0)) : 0u;
+      const uint64_t h = xxh3_short_row(d0, d1, pl_[u], t, pb, shsec);
+      if (k < n && t == 0) {
+        crc_ok[it_[u]] = crc == stv[u] ? 1 : 0;
+        hash_out[it_[u]] = ok[u] ? h : 0ull;
+      }
+    }
+  }
+}
+
 // CRC = true (fused WAL recovery, wal_recover.hip): besides the XXH3 of every
 // logical record, the CRC32C of each of its physical records (fragments) is
 // checked from the same loads.  CRC32C is linear: a fragment's CRC over
@@ -2056,6 +2210,21 @@ hipError_t launch_xxh3_short_rows(const uint8_t* base, uint64_t base_len, const 
       std::min<uint64_t>((n + per_wg - 1) / per_wg, uint64_t(device_info().num_cus) * 32));
   hipLaunchKernelGGL(xxh3_short_rows_kernel, dim3(grid), dim3(kShortRowsThreads), 0, stream, base,
                      base_len, off, len, n, idx, out);
+  return hipGetLastError();
+}
+
+hipError_t launch_wal_short_rows(const uint8_t* base, uint64_t base_len, const uint64_t* coff,
+                                 const uint32_t* clen, const uint64_t* p0, const uint32_t* plen,
+                                 const uint64_t* item, uint64_t n, const uint32_t* stored,
+                                 uint8_t* crc_ok, uint64_t* hash_out, hipStream_t stream) {
+  if (n == 0) return hipSuccess;
+  if (!base || !coff || !clen || !p0 || !plen || !item || !stored || !crc_ok || !hash_out)
+    return hipErrorInvalidValue;
+  const uint64_t per_wg = 4 * kShortCrcU * (kShortCrcThreads / 64);
+  const uint32_t grid = static_cast<uint32_t>(
+      std::min<uint64_t>((n + per_wg - 1) / per_wg, uint64_t(device_info().num_cus)));
+  hipLaunchKernelGGL(wal_short_rows_kernel, dim3(grid), dim3(kShortCrcThreads), 0, stream, base,
+                     base_len, coff, clen, p0, plen, item, n, stored, crc_ok, hash_out);
   return hipGetLastError();
 }
 

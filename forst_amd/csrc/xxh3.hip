@@ -1321,11 +1321,12 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   }
 }
 
-// WPE: waves per SIMD the register allocation targets (3, the default: 168
-// VGPRs with a few spilled dwords, C5 a14 21.5 vs 24.8 ms at 2: 181 VGPRs)
-// the fused CRC's tables: [0, 64K) G and J1012 replicated (crc_lds.h),
-// [64K, 124K) A16[1..15], [124K, 136K) C256[1..3]; constant trip counts (see
-// fill_tables3)
+// WPE: waves per SIMD the register allocation targets (3, the default: round
+// 5 builds, the a14 kernel 167 VGPRs and the fused one 164, no VGPR spills;
+// C5 a14 21.5 vs 24.8 ms at 2 in round 2)
+// the fused CRC's tables: [0, 64K) G and J244 (one chain per lane; J1012 for
+// the column chains) replicated (crc_lds.h), [64K, 124K) A16[1..15], [124K,
+// 136K) C256[1..3]; constant trip counts (see fill_tables3)
 template <uint32_t NT>
 __device__ __forceinline__ void fill_frag_crc_tables(uint32_t* L) {
   const uint32_t tid = threadIdx.x;

@@ -1162,6 +1162,10 @@ struct FragGeo {
 };
 template <bool CRC>
 constexpr uint32_t frag_k() { return CRC ? kFragKFused : kFragKA14; }
+// the fused kernel's candidates are all over 240 bytes with the short path
+// (FORST_REC_SHORT, rw_cand_kernel): its rows need no length test
+template <bool CRC>
+constexpr bool kFusedLong() { return CRC && FORST_REC_SHORT; }
 
 template <uint32_t K>
 struct FStep {
@@ -1203,7 +1207,7 @@ __device__ __forceinline__ void frag_issue(const BlockArgs& a, uint32_t lane, co
   const uint32_t t = lane & 15, s4 = t >> 2;
   const uint64_t P0 = P.off();
   const bool valid = P.rel != kNoMsg && P0 <= a.base_len;
-  const bool lng = valid && P.size > 240;
+  const bool lng = valid && (kFusedLong<CRC>() || P.size > 240);
   const uint32_t nb = (P.size - 1) >> G::kShift;
   const uint32_t hs = P.hs();
   // one fragment (wal_hash.h gathers the others); the fused kernel's
@@ -1599,7 +1603,7 @@ xxh3_frag_kernel(BlockArgs a) {
   FRow C;
   fetch(row, C);
   auto advance = [&](const FRow& P, FRow& I) {
-    const bool lng = P.rel != kNoMsg && P.size > 240;
+    const bool lng = P.rel != kNoMsg && (kFusedLong<CRC>() || P.size > 240);
     const uint32_t nbP = (P.size - 1) >> G::kShift;
     const bool more = lng && P.g < nbP;
     const bool need = P.rel != kNoMsg && !more;
@@ -1659,7 +1663,7 @@ xxh3_frag_kernel(BlockArgs a) {
     __builtin_amdgcn_sched_barrier(0);
 #endif
     const bool valid = C.rel != kNoMsg && C.off() <= a.base_len;
-    const bool lng = valid && C.size > 240;
+    const bool lng = valid && (kFusedLong<CRC>() || C.size > 240);
     // XXH3-blocks: nbC full ones (scrambled), then nbSC stripes of the last
     const uint32_t nbC = (C.size - 1) >> 10, nbSC = ((C.size - 1) & 1023) >> 6;
     if (C.g == 0) {  // XXH3_INIT_ACC (xxhash.h:5188)

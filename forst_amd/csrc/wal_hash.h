@@ -136,7 +136,36 @@ __global__ void __launch_bounds__(kWhLanes) wh_gather_kernel(const uint8_t* log,
       if (threadIdx.x < hb) d[threadIdx.x] = src[threadIdx.x];
       if (threadIdx.x < l - tb) d[tb + threadIdx.x] = src[tb + threadIdx.x];
       uint32_t* dw = reinterpret_cast<uint32_t*>(d + hb);
-      for (uint32_t x = threadIdx.x; x < nw; x += kWhLanes) dw[x] = ldu32(src + hb + 4 * x);
+      // 16 destination bytes per thread from a dword-aligned 16-byte load and
+      // the dword after it (realigned), four groups per thread in flight; a
+      // group's fifth source dword stays inside the fragment (n16), the
+      // dwords after the last group one by one
+      const uint8_t* s0 = src + hb;
+      const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uintptr_t>(s0) & 3);
+      const uint8_t* sa = s0 - m;
+      const uint32_t n16 = nw >= 5 ? (nw - 1) >> 2 : 0u;
+      for (uint32_t g0 = threadIdx.x; g0 < n16; g0 += 4 * kWhLanes) {
+        u32x4a4 v[4];
+        uint32_t nx[4];
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {  // (unconditional loads: a group past n16 reads g0's)
+          const uint32_t g = g0 + k * kWhLanes < n16 ? g0 + k * kWhLanes : g0;
+          v[k] = ld16_a4(sa + 16 * g);
+          nx[k] = ld4_a4(sa + 16 * g + 16);
+        }
+#pragma unroll
+        for (uint32_t k = 0; k < 4; ++k) {
+          const uint32_t g = g0 + k * kWhLanes;
+          if (g < n16) {
+            const u32x4a4 o{__builtin_amdgcn_alignbyte(v[k].y, v[k].x, m),
+                            __builtin_amdgcn_alignbyte(v[k].z, v[k].y, m),
+                            __builtin_amdgcn_alignbyte(v[k].w, v[k].z, m),
+                            __builtin_amdgcn_alignbyte(nx[k], v[k].w, m)};
+            *reinterpret_cast<u32x4a4*>(dw + 4 * g) = o;
+          }
+        }
+      }
+      for (uint32_t x = 4 * n16 + threadIdx.x; x < nw; x += kWhLanes) dw[x] = ldu32(src + hb + 4 * x);
       d += l;
     }
   }

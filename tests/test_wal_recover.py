@@ -92,7 +92,7 @@ def _short_lengths_log(recyclable, reps, seed):
 @pytest.mark.parametrize("recyclable", [False, True])
 def test_recover_short_lengths_on_emulator(recyclable):
     E = _emu()
-    log = _short_lengths_log(recyclable, 2, 3)
+    log = _short_lengths_log(recyclable, 1, 3)
     recs, reps, res = E.wal_recover(log, 7, R.kPointInTimeRecovery)
     compare(recs, reps, res, log, 7, R.kPointInTimeRecovery, "short")
 

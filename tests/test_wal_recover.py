@@ -114,6 +114,28 @@ def test_recover_short_lengths_on_gpu(recyclable):
 
 
 @pytest.mark.gpu
+def test_recover_many_raw_records_on_gpu():
+    """a raw list over 64 K entries (records no candidate covers: here
+    re-typed to an unknown type with a valid CRC), so the raw path runs
+    ahead of the fused kernel on its stream; a few of them with a wrong CRC;
+    every record and report against the serial reader, every mode"""
+    import torch
+    from forst_amd import engine
+    rng = np.random.default_rng(29)
+    lens = rng.integers(20, 300, 150_000).astype(np.uint32)
+    log, po, pl = W.frame_lens(lens, 6)
+    for off in po[1::2]:
+        W.set_type(log, int(off), 30)
+    for off in rng.choice(po[1::2], 5, replace=False):
+        log[int(off) + 7] ^= 0x04  # a payload byte of a re-typed record: a CRC mismatch
+    for mode in MODES:
+        rec, rep, res = engine.wal_recover_batch(torch.from_numpy(log).cuda(), 7, mode)
+        recs = [rec[k].cpu().numpy() for k in ("offset", "length", "hash", "n_fragments")]
+        reps = [rep[k].cpu().numpy() for k in ("offset", "bytes", "reason", "type")]
+        compare(recs, reps, res, log, 7, mode, "raw")
+
+
+@pytest.mark.gpu
 def test_recover_c5_shape_with_corruption():
     """200 000 C5-shaped records (log-uniform 32 B-32 KiB) from the writer
     kernels, 40 payload flips: every record before / after the dropped blocks

@@ -264,7 +264,7 @@ def run_wal(steps, warmup, n_records=10_000_000):
            "recover_GiBps": round(w.total / t_r / GIB, 1),
            "recover_desc": "forst_wal_recover_batch: header walk + every physical CRC + "
                            "fragment state machine + XXH3 of every logical record, "
-                           "kPointInTimeRecovery, incl. its 4 stream synchronisations"}
+                           "kPointInTimeRecovery, incl. its 5-6 stream synchronisations"}
     del w
     return out
 

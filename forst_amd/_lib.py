@@ -82,6 +82,12 @@ def lib():
         "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
         "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp, vp,
                                       u64, vp]),
+        "forst_memtable_verify_batch": (i, [vp, u64, vp, u64, u32, vp, vp, vp, vp]),
+        "forst_memtable_protect_batch": (i, [vp, u64, vp, u64, u32, i, vp, vp, vp]),
+        "forst_write_batch_protect_batch": (i, [vp, u64, vp, vp, u64, vp, vp, u64, vp, vp, vp,
+                                                vp]),
+        "forst_block_kv_checksum_batch": (i, [vp, u64, vp, vp, vp, u64, u32, vp, vp, vp, u64, vp,
+                                              vp, vp]),
         "forst_wal_layout": (i, [vp, u64, i, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp]),
         "forst_wal_layout_at": (i, [vp, u64, i, u32, vp, vp, vp, u64, vp, vp, u64, vp, vp, vp,
                                     vp]),

@@ -671,6 +671,133 @@ FORST_API int forst_kv_verify_batch(const uint8_t* base, uint64_t base_len,
   return dispatch_kv(kKvVerify, a, stream);
 }
 
+namespace {
+int mem_args(KvArgs& a, const uint8_t* base, uint64_t base_len, const uint64_t* entry_offsets,
+             uint32_t protection_bytes, uint64_t n) {
+  if (n && !entry_offsets) return set_error(FORST_EINVAL, "entry_offsets must be non-null");
+  if (protection_bytes != 1 && protection_bytes != 2 && protection_bytes != 4 &&
+      protection_bytes != 8)
+    return set_error(FORST_EINVAL, "protection_bytes must be 1, 2, 4 or 8");
+  a.base = base;
+  a.base_len = base_len;
+  a.key_off = entry_offsets;
+  a.prot_bytes = protection_bytes;
+  a.n = n;
+  return FORST_OK;
+}
+int dispatch_mem(int mode, const KvArgs& a, void* stream) {
+  if (a.n == 0) return FORST_OK;
+  if (!a.base) return set_error(FORST_EINVAL, "base must be non-null");
+  int rc = check_device();
+  if (rc) return rc;
+  return hip_status(launch_kv(mode, a, static_cast<hipStream_t>(stream), &g_last_kernel),
+                    "memtable kv launch");
+}
+}  // namespace
+
+FORST_API int forst_memtable_verify_batch(const uint8_t* base, uint64_t base_len,
+                                          const uint64_t* entry_offsets, uint64_t n,
+                                          uint32_t protection_bytes, uint64_t* computed,
+                                          uint8_t* status, unsigned long long* mismatches,
+                                          void* stream) {
+  KvArgs a{};
+  int rc = mem_args(a, base, base_len, entry_offsets, protection_bytes, n);
+  if (rc) return rc;
+  a.out = computed;
+  a.status = status;
+  a.mismatches = mismatches;
+  return dispatch_mem(kKvMemVerify, a, stream);
+}
+
+FORST_API int forst_memtable_protect_batch(uint8_t* base, uint64_t base_len,
+                                           const uint64_t* entry_offsets, uint64_t n,
+                                           uint32_t protection_bytes, int write_in_place,
+                                           uint64_t* out, uint8_t* status, void* stream) {
+  KvArgs a{};
+  int rc = mem_args(a, base, base_len, entry_offsets, protection_bytes, n);
+  if (rc) return rc;
+  a.out = out;
+  a.status = status;
+  a.write_in_place = write_in_place ? 1 : 0;
+  return dispatch_mem(kKvMemProtect, a, stream);
+}
+
+FORST_API int forst_write_batch_protect_batch(const uint8_t* base, uint64_t base_len,
+                                              const uint64_t* rep_offsets,
+                                              const uint32_t* rep_sizes, uint64_t n_reps,
+                                              uint64_t* first_entry, uint64_t* prot,
+                                              uint64_t capacity, uint8_t* status,
+                                              uint32_t* n_protected, uint64_t* n_total,
+                                              void* stream) {
+  if (n_total) *n_total = 0;
+  if (!first_entry) return set_error(FORST_EINVAL, "first_entry must be non-null");
+  if (n_reps && (!base || !rep_offsets || !rep_sizes))
+    return set_error(FORST_EINVAL, "base/rep_offsets/rep_sizes must be non-null");
+  if (capacity && !prot) return set_error(FORST_EINVAL, "prot must be non-null");
+  int rc = check_device();
+  if (rc) return rc;
+  WbArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = rep_offsets;
+  a.sizes = rep_sizes;
+  a.n = n_reps;
+  a.first_entry = first_entry;
+  a.prot = prot;
+  a.capacity = capacity;
+  a.status = status;
+  a.n_protected = n_protected;
+  uint64_t total = 0;
+  const hipError_t e = launch_write_batch_protect(a, static_cast<hipStream_t>(stream), &total,
+                                                  &g_last_kernel);
+  if (n_total) *n_total = total;
+  if (e == hipErrorInvalidValue && total > capacity)
+    return set_error(FORST_EINVAL, "capacity " + std::to_string(capacity) + " < " +
+                                       std::to_string(total) + " protection slots");
+  return hip_status(e, "write_batch_protect");
+}
+
+FORST_API int forst_block_kv_checksum_batch(const uint8_t* base, uint64_t base_len,
+                                            const uint64_t* block_offsets,
+                                            const uint32_t* block_sizes, const uint8_t* kinds,
+                                            uint64_t n_blocks, uint32_t protection_bytes,
+                                            uint64_t* first_key, uint8_t* kv_checksums,
+                                            uint64_t* prot, uint64_t capacity, uint8_t* status,
+                                            uint64_t* n_total, void* stream) {
+  if (n_total) *n_total = 0;
+  if (!first_key) return set_error(FORST_EINVAL, "first_key must be non-null");
+  if (n_blocks && (!base || !block_offsets || !block_sizes || !kinds))
+    return set_error(FORST_EINVAL, "base/block_offsets/block_sizes/kinds must be non-null");
+  if (protection_bytes != 1 && protection_bytes != 2 && protection_bytes != 4 &&
+      protection_bytes != 8)
+    return set_error(FORST_EINVAL, "protection_bytes must be 1, 2, 4 or 8");
+  if (capacity && !kv_checksums)
+    return set_error(FORST_EINVAL, "kv_checksums must be non-null");
+  int rc = check_device();
+  if (rc) return rc;
+  BlkArgs a{};
+  a.base = base;
+  a.base_len = base_len;
+  a.offsets = block_offsets;
+  a.sizes = block_sizes;
+  a.kinds = kinds;
+  a.n = n_blocks;
+  a.prot_bytes = protection_bytes;
+  a.first_key = first_key;
+  a.kv_checksums = kv_checksums;
+  a.prot = prot;
+  a.capacity = capacity;
+  a.status = status;
+  uint64_t total = 0;
+  const hipError_t e =
+      launch_block_kv_checksum(a, static_cast<hipStream_t>(stream), &total, &g_last_kernel);
+  if (n_total) *n_total = total;
+  if (e == hipErrorInvalidValue && total > capacity)
+    return set_error(FORST_EINVAL, "capacity " + std::to_string(capacity) + " < " +
+                                       std::to_string(total) + " keys");
+  return hip_status(e, "block_kv_checksum");
+}
+
 FORST_API int forst_fill_stream(uint8_t* dev, uint64_t start, uint64_t n, uint64_t seed,
                                 void* stream) {
   if (n == 0) return FORST_OK;

@@ -109,6 +109,21 @@ enum KvMode : int {
   kKvHash = 0,     // out[i] = Hash64(key_i, seeds ? seeds[i] : seed)
   kKvProtect = 1,  // out[i] = ProtectionInfo64 of (key, value[, op][, seq][, cf])
   kKvVerify = 2,   // ... compared with prot_bytes LE bytes at chk_off[i]
+  // encoded memtable entries (db/memtable.cc:273-307, :696-732): key_off[i] =
+  // the entry; klen / tag / vlen decoded on the device
+  kKvMemVerify = 3,   // MemTable::VerifyEntryChecksum -> status[i]
+  kKvMemProtect = 4,  // MemTable::UpdateEntryChecksum (written in place if asked)
+};
+
+// per-entry status of the memtable modes (MemTable::VerifyEntryChecksum's
+// Corruption reasons, memtable.cc:280-306)
+enum KvMemStatus : uint8_t {
+  kMemOk = 0,
+  kMemBadKeyLength = 1,  // "Unable to parse internal key length"
+  kMemKeyTooShort = 2,   // "Memtable entry internal key length too short."
+  kMemBadValue = 3,      // "Unable to parse internal key value"
+  kMemMismatch = 4,      // "Corrupted memtable entry, per key-value checksum ..."
+  kMemOutOfRange = 5,    // the entry reaches past the buffer (no reference twin)
 };
 
 struct KvArgs {
@@ -129,7 +144,82 @@ struct KvArgs {
   uint8_t* ok;               // verify, nullable
   unsigned long long* mismatches;  // verify, nullable
   uint64_t n;
+  uint8_t* status;           // memtable modes: KvMemStatus per entry, nullable
+  int write_in_place;        // kKvMemProtect: Encode(prot_bytes) at the checksum
+  const uint8_t* key_base;   // nullable: keys live in this buffer instead of base
+  uint64_t key_base_len;
+  uint8_t* enc_out;          // kKvProtect, nullable: Encode(prot_bytes) of entry i
+                             // at enc_out + i * prot_bytes (a block's kv_checksum_)
 };
+
+// Block protection (kv_sites.hip): block kinds and per-block status
+enum BlkKind : uint8_t {
+  kBlkData = 0,            // InitializeDataBlockProtectionInfo (block.cc:1113)
+  kBlkIndex = 1,           // InitializeIndexBlockProtectionInfo (block.cc:1162)
+  kBlkMeta = 2,            // InitializeMetaIndexBlockProtectionInfo (block.cc:1205)
+  kBlkValueIsFull = 4,     // index: values not delta-encoded
+  kBlkHasFirstKey = 8,     // index: kBinarySearchWithFirstKey values
+};
+enum BlkStatus : uint8_t {
+  kBlkOk = 0,
+  kBlkBadContents = 1,  // Block's size_ = 0 error marker / "bad block contents"
+  kBlkBadEntry = 2,     // "bad entry in block" (the iterator's CorruptionError)
+  kBlkOutOfRange = 3,   // the block reaches past the buffer
+};
+struct BlkArgs {
+  const uint8_t* base;
+  uint64_t base_len;
+  const uint64_t* offsets;  // block b = base[offsets[b] .. + sizes[b]) (no trailer)
+  const uint32_t* sizes;
+  const uint8_t* kinds;     // BlkKind | flags per block
+  uint64_t n;
+  uint32_t prot_bytes;
+  uint64_t* first_key;      // out, n + 1
+  uint8_t* kv_checksums;    // out, capacity * prot_bytes bytes
+  uint64_t* prot;           // out, nullable: the full values, capacity
+  uint64_t capacity;
+  uint8_t* status;          // out, nullable
+};
+hipError_t launch_block_kv_checksum(const BlkArgs& a, hipStream_t st, uint64_t* total,
+                                    const char** kernel_name);
+
+// WriteBatch reps (kv_sites.hip): per-rep status, the Corruption texts of
+// ReadRecordFromWriteBatch / WriteBatch::Iterate (db/write_batch.cc:361-716)
+enum WbStatus : uint8_t {
+  kWbOk = 0,
+  kWbTooSmall = 1,          // "malformed WriteBatch (too small)"
+  kWbBadPut = 2,            // "bad WriteBatch Put"
+  kWbBadDelete = 3,         // "bad WriteBatch Delete"
+  kWbBadDeleteRange = 4,    // "bad WriteBatch DeleteRange"
+  kWbBadMerge = 5,          // "bad WriteBatch Merge"
+  kWbBadBlobIndex = 6,      // "bad WriteBatch BlobIndex"
+  kWbBadBlob = 7,           // "bad WriteBatch Blob"
+  kWbBadEndPrepareXid = 8,  // "bad EndPrepare XID"
+  kWbBadCommitTs = 9,       // "bad commit timestamp"
+  kWbBadCommitXid = 10,     // "bad Commit XID"
+  kWbBadRollbackXid = 11,   // "bad Rollback XID"
+  kWbBadPutEntity = 12,     // "bad WriteBatch PutEntity"
+  kWbUnknownTag = 13,       // "unknown WriteBatch tag"
+  kWbWrongCount = 14,       // "WriteBatch has wrong count"
+  kWbOutOfRange = 15,       // the rep reaches past the buffer (no reference twin)
+};
+
+struct WbArgs {
+  const uint8_t* base;
+  uint64_t base_len;
+  const uint64_t* offsets;  // rep b = base[offsets[b] .. + sizes[b])
+  const uint32_t* sizes;
+  uint64_t n;
+  uint64_t* first_entry;    // out, n + 1: rep b's protections at [first[b], first[b+1])
+  uint64_t* prot;           // out, capacity
+  uint64_t capacity;
+  uint8_t* status;          // out, nullable: WbStatus per rep
+  uint32_t* n_protected;    // out, nullable: slots filled per rep
+};
+// synchronous (reads the protection total back into *total); fails with
+// hipErrorInvalidValue when *total > a.capacity
+hipError_t launch_write_batch_protect(const WbArgs& a, hipStream_t st, uint64_t* total,
+                                      const char** kernel_name);
 
 struct DeviceInfo {
   int device;

@@ -14,12 +14,25 @@
 // its own seed (:84-88); op type (1 byte), sequence number (8) and column
 // family id (4) are hashed as their native little-endian bytes (:27-29).
 //
-// Layout: one wave per 64 entries, one LANE per entry for fields <= 240 bytes
-// (keys, small values, op/seq/cf: the length-class formulas need no cross-lane
-// work); every field > 240 bytes is hashed by the WHOLE wave in turn (ballot
-// of the long fields, the XXH3-style lane split: lane L takes 16 bytes --
-// stripe L/4, accumulator pair L%4 -- of each 1 KiB block, 16-lane stripe sum,
-// serial scramble), and the owner lane XORs the result in.
+// Layout (round 6): ONE 16-LANE ROW PER ENTRY.  A wave takes a tile of 64
+// entries: lane i loads entry i's descriptors (coalesced) and hashes its
+// op/seq/cf fields; then 16 rounds, in round r row R hashes the key and value
+// of entry 16R + r.  Every byte an entry's hashes read is loaded by the lanes
+// of that row at once -- adjacent 16-byte pieces of one key / value, so a
+// row's loads hit the same few cache lines -- and every formula is split over
+// the row's lanes:
+//   * 17..240 bytes: the XXPH3 sum of mix16B terms (xxph3.h:1651-1707) is a
+//     sum of independent terms: lane t computes term t, two segmented row sums
+//     (lanes 0-7, 8-15) give both accumulation phases;
+//   * > 240 bytes: lane t takes the 16-byte chunks 16t + 256k of each 1 KiB
+//     block (stripe t/4 + 4k, accumulator pair t%4), the first block and the
+//     last stripe loaded together with the short terms;
+//   * <= 16 bytes: one lane (7: key, 6: value).
+// Row r's hash lands in an LDS slot of its owner lane; the owner XORs it with
+// the op/seq/cf hashes and writes / verifies.  (Round 5 hashed short fields
+// one LANE per entry with scattered 8-byte loads -- 64 entries, 64 cache
+// lines per load -- and long values in a second pass that fetched the same
+// lines again: 0.18 of peak, 1.4x traffic.)
 #include <cstdlib>
 
 #include "device_common.h"
@@ -32,6 +45,7 @@ namespace {
 
 constexpr uint32_t kWaves = 4;
 constexpr uint32_t kThreads = kWaves * 64;
+constexpr uint32_t kSecWords = 26;  // kSecret as 24 LE u64 words + 2 zero words
 
 // db/kv_checksum.h:84-88
 constexpr uint64_t kSeedK = 0;
@@ -48,14 +62,15 @@ __device__ __forceinline__ uint64_t xxph3_avalanche(uint64_t h) {
   return h;
 }
 
-// 8 bytes at byte offset `off` of the seeded custom secret (xxph3.h:1609-1620:
-// word 2i gets +seed, word 2i+1 gets -seed)
-__device__ __forceinline__ uint64_t psec64(uint32_t off, uint64_t seed) {
+// 8 bytes at byte offset `off` of the secret for `seed` (xxph3.h:1609-1620:
+// word 2i gets +seed, word 2i+1 gets -seed; seed 0 = the default secret),
+// from the LDS copy of kSecret's words
+__device__ __forceinline__ uint64_t psec(const uint64_t* S, uint32_t off, uint64_t seed) {
   const uint32_t w = off >> 3, sh = off & 7;
-  const uint64_t a = sec64(8 * w) + ((w & 1) ? (0 - seed) : seed);
-  if (sh == 0) return a;
-  const uint64_t b = sec64(8 * w + 8) + ((w & 1) ? seed : (0 - seed));
-  return (a >> (8 * sh)) | (b << (64 - 8 * sh));
+  const uint64_t x = S[w] + ((w & 1) ? (0 - seed) : seed);
+  if (sh == 0) return x;
+  const uint64_t y = S[w + 1] + ((w & 1) ? seed : (0 - seed));
+  return (x >> (8 * sh)) | (y << (64 - 8 * sh));
 }
 
 // xxph3.h:1098 XXPH3_len_4to8_64b on the input already folded to 64 bits
@@ -72,52 +87,71 @@ __device__ __forceinline__ uint64_t xxph3_1to3(uint32_t c1, uint32_t c2, uint32_
                          (static_cast<uint64_t>(static_cast<uint32_t>(sec64(0))) + seed);
   return xxph3_avalanche(keyed * P64_1);
 }
-// xxph3.h:1640 XXPH3_mix16B (default secret, explicit seed)
-__device__ __forceinline__ uint64_t xxph3_mix16B(const uint8_t* in, uint32_t s, uint64_t seed) {
-  return mul128_fold64(ldu64(in) ^ (sec64(s) + seed), ldu64(in + 8) ^ (sec64(s + 8) - seed));
+
+// The bytes a 0..16-byte field's formula reads (xxph3.h:1082-1140), loaded
+// exactly: 9..16 -> d0 = first 8, d1 = last 8; 4..8 -> d0 = first 4 | last 4
+// << 32; 1..3 -> d0 = in[0] | in[len/2] << 8 | in[len-1] << 16.
+__device__ __forceinline__ void tiny_load(const uint8_t* in, uint32_t len, uint64_t& d0,
+                                          uint64_t& d1) {
+  if (len > 8) {
+    d0 = ldu64(in);
+    d1 = ldu64(in + len - 8);
+  } else if (len >= 4) {
+    d0 = ldu32(in) | (static_cast<uint64_t>(ldu32(in + len - 4)) << 32);
+  } else if (len) {
+    d0 = ldu8(in) | (ldu8(in + (len >> 1)) << 8) | (ldu8(in + len - 1) << 16);
+  }
+}
+__device__ __forceinline__ uint64_t tiny_hash(uint64_t d0, uint64_t d1, uint32_t len, uint64_t seed) {
+  if (len > 8) {
+    const uint64_t lo = d0 ^ (sec64(0) + seed);
+    const uint64_t hi = d1 ^ (sec64(8) - seed);
+    return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
+  }
+  if (len >= 4) return xxph3_4to8(d0, len, seed);
+  if (len) {
+    const uint32_t w = static_cast<uint32_t>(d0);
+    return xxph3_1to3(w & 0xff, (w >> 8) & 0xff, (w >> 16) & 0xff, len, seed);
+  }
+  return mul128_fold64(seed + sec64(0), P64_2);  // xxph3.h:1133-1138 (RocksDB)
 }
 
-// XXPH3_64bits_withSeed for len <= 240 (per lane, xxph3.h:1126-1140,
-// 1651-1707)
-__device__ uint64_t xxph3_short(const uint8_t* in, uint32_t len, uint64_t seed) {
-  if (len <= 16) {
-    if (len > 8) {
-      const uint64_t lo = ldu64(in) ^ (sec64(0) + seed);
-      const uint64_t hi = ldu64(in + len - 8) ^ (sec64(8) - seed);
-      return xxph3_avalanche(len + (lo + hi) + mul128_fold64(lo, hi));
-    }
-    if (len >= 4) {
-      const uint64_t in64 = ldu32(in) | (static_cast<uint64_t>(ldu32(in + len - 4)) << 32);
-      return xxph3_4to8(in64, len, seed);
-    }
-    if (len) return xxph3_1to3(ldu8(in), ldu8(in + (len >> 1)), ldu8(in + len - 1), len, seed);
-    return mul128_fold64(seed + sec64(0), P64_2);  // xxph3.h:1133-1138 (RocksDB)
-  }
+// Which 16 bytes of a 17..240-byte field lane t mixes (xxph3.h:1651-1707):
+//   17..128:  term t < nt (nt = 2/4/6/8 for len > 0/32/64/96): even t at
+//             in + 8t, odd t at in + len - 8(t+1); secret 16t
+//   129..240: t < 8 at in + 16t, secret 16t; 8 <= t < len/16 (t < 15) at
+//             in + 16t, secret 16(t-8) + 3; t = 15 at in + len - 16, secret 119
+// Returns false for a lane without a term.
+__device__ __forceinline__ bool term_at(uint32_t t, uint32_t len, uint32_t& d) {
   if (len <= 128) {
-    uint64_t acc = len * P64_1;
-    if (len > 32) {
-      if (len > 64) {
-        if (len > 96) {
-          acc += xxph3_mix16B(in + 48, 96, seed);
-          acc += xxph3_mix16B(in + len - 64, 112, seed);
-        }
-        acc += xxph3_mix16B(in + 32, 64, seed);
-        acc += xxph3_mix16B(in + len - 48, 80, seed);
-      }
-      acc += xxph3_mix16B(in + 16, 32, seed);
-      acc += xxph3_mix16B(in + len - 32, 48, seed);
-    }
-    acc += xxph3_mix16B(in, 0, seed);
-    acc += xxph3_mix16B(in + len - 16, 16, seed);
-    return xxph3_avalanche(acc);
+    const uint32_t nt = len > 96 ? 8 : len > 64 ? 6 : len > 32 ? 4 : 2;
+    d = (t & 1) ? len - 8 * (t + 1) : 8 * t;
+    return t < nt;
   }
-  uint64_t acc = len * P64_1;
-  for (uint32_t i = 0; i < 8; ++i) acc += xxph3_mix16B(in + 16 * i, 16 * i, seed);
-  acc = xxph3_avalanche(acc);
-  const uint32_t nb_rounds = len / 16;
-  for (uint32_t i = 8; i < nb_rounds; ++i) acc += xxph3_mix16B(in + 16 * i, 16 * (i - 8) + 3, seed);
-  acc += xxph3_mix16B(in + len - 16, 136 - 17, seed);
-  return xxph3_avalanche(acc);
+  d = t == 15 ? len - 16 : 16 * t;
+  return t < 8 || t == 15 || t < (len >> 4);
+}
+__device__ __forceinline__ uint32_t term_secret(uint32_t t) {
+  return t < 8 ? 16 * t : t < 15 ? 16 * (t - 8) + 3 : 119;
+}
+
+// DPP row_shr:n with bound_ctrl (lanes without a source get 0)
+template <int N>
+__device__ __forceinline__ uint64_t row_shr64(uint64_t v) {
+  return dpp64<0x110 + N>(v);
+}
+
+// lane 7 of each row: the XXPH3 hash of a 17..240-byte field from the row's
+// mix16B terms (0 in lanes without one): the segmented sums over lanes 0-7
+// and 8-15 are the two accumulation phases
+__device__ __forceinline__ uint64_t short_finish(uint64_t term, uint32_t len) {
+  term += row_shr64<1>(term);
+  term += row_shr64<2>(term);
+  term += row_shr64<4>(term);  // lane 7: sum of 0..7, lane 15: sum of 8..15
+  const uint64_t s2 = row_ror64<8>(term);
+  uint64_t x = static_cast<uint64_t>(len) * P64_1 + term;
+  if (len > 128) x = xxph3_avalanche(x) + s2;
+  return xxph3_avalanche(x);
 }
 
 __device__ __forceinline__ uint64_t scramble_acc(uint64_t a, uint64_t key) {
@@ -126,266 +160,362 @@ __device__ __forceinline__ uint64_t scramble_acc(uint64_t a, uint64_t key) {
   return a * P32_1;
 }
 
-// XXPH3_64bits_withSeed for len > 240, whole wave (all arguments uniform);
-// every lane returns the hash.  xxph3.h:1514-1583, 1630-1637.
-__device__ uint64_t wave_xxph3_long(const uint8_t* p, uint32_t len, uint64_t seed, uint32_t lane) {
-  const uint32_t s = lane >> 2, pp = lane & 3;
-  const uint64_t k0 = psec64(8 * s + 16 * pp, seed), k1 = psec64(8 * s + 16 * pp + 8, seed);
-  const uint64_t ks0 = psec64(128 + 16 * pp, seed), ks1 = psec64(136 + 16 * pp, seed);
-  // XXPH3_INIT_ACC (xxph3.h:1567)
-  uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;
-  uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
-  const uint32_t nb = len / 1024;
-  const uint32_t nbS = (len - 1024 * nb) / 64;
+// The chunks lane t mixes in 1 KiB block g of a > 240-byte field: bytes
+// 1024g + 16t + 256k (stripe t/4 + 4k, accumulator pair t%4), k = 0..3;
+// bit k of the mask = the chunk exists (whole blocks, then the nbS stripes of
+// the last partial block).
+struct Block {
+  uint64_t d0[4], d1[4];
+  uint32_t mask;
+};
+__device__ __forceinline__ void long_block_load(const uint8_t* p, uint32_t len, uint32_t g,
+                                                uint32_t t, bool act, Block& b) {
+  const uint32_t nb = len >> 10, nbS = (len & 1023) >> 6;
   const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3);
-  const uint8_t* q = p - m + 16 * lane;
-  uint32_t g = 0;
-  for (; g + 4 <= nb; g += 4) {  // 4 loads in flight per lane
-    uint64_t c0[4], c1[4];
+  const uint8_t* q = p - m + 1024 * g + 16 * t;
+  b.mask = 0;
 #pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      uint64_t d0, d1;
-      ld16u(q + 1024 * (g + j), m, d0, d1);
-      c0[j] = d0 + mul32to64(d0 ^ k0);  // acc_64bits: acc[i] += data + lo*hi(data ^ key)
-      c1[j] = d1 + mul32to64(d1 ^ k1);
-    }
-#pragma unroll
-    for (int j = 0; j < 4; ++j) {
-      acc0 = scramble_acc(acc0 + stripe_sum(c0[j]), ks0);
-      acc1 = scramble_acc(acc1 + stripe_sum(c1[j]), ks1);
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t st = (t >> 2) + 4 * k;
+    b.d0[k] = b.d1[k] = 0;
+    if (act && (g < nb || (g == nb && st < nbS))) {
+      ld16u(q + 256 * k, m, b.d0[k], b.d1[k]);
+      b.mask |= 1u << k;
     }
   }
-  for (; g < nb; ++g) {
-    uint64_t d0, d1;
-    ld16u(q + 1024 * g, m, d0, d1);
-    acc0 = scramble_acc(acc0 + stripe_sum(d0 + mul32to64(d0 ^ k0)), ks0);
-    acc1 = scramble_acc(acc1 + stripe_sum(d1 + mul32to64(d1 ^ k1)), ks1);
-  }
-  {  // last partial block: stripes [0, nbS), no scramble
-    uint64_t c0 = 0, c1 = 0;
-    if (s < nbS) {
-      uint64_t d0, d1;
-      ld16u(q + 1024 * nb, m, d0, d1);
-      c0 = d0 + mul32to64(d0 ^ k0);
-      c1 = d1 + mul32to64(d1 ^ k1);
-    }
-    acc0 += stripe_sum(c0);
-    acc1 += stripe_sum(c1);
-  }
-  if (len & 63) {  // last stripe at len - 64, secret + 192 - 64 - 7 (xxph3.h:1539-1542)
-    const uint8_t* lp = p + len - 64 + 16 * pp;
-    const uint32_t ml = static_cast<uint32_t>(reinterpret_cast<uint64_t>(lp) & 3);
-    uint64_t d0, d1;
-    ld16u(lp - ml, ml, d0, d1);
-    acc0 += d0 + mul32to64(d0 ^ psec64(121 + 16 * pp, seed));
-    acc1 += d1 + mul32to64(d1 ^ psec64(129 + 16 * pp, seed));
-  }
-  // XXPH3_mergeAccs from secret + 11 (xxph3.h:1554-1582)
-  uint64_t t = mul128_fold64(acc0 ^ psec64(11 + 16 * pp, seed), acc1 ^ psec64(19 + 16 * pp, seed));
-  t += quad_xor64<1>(t);
-  t += quad_xor64<2>(t);
-  return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + t);
 }
-
-// The same on one 16-lane row (t = lane & 15), four fields per wave at once
-// (round 5): lane t takes the 16-byte chunks at 16 t + 256 k of each 1 KiB
-// block (stripe t/4 + 4k, accumulator pair t%4), and the last stripe's load
-// is issued with them, so a field under 1 KiB (a value of 240..1000 bytes,
-// the memtable shape) costs one round trip to memory instead of two, and
-// four of them overlap.  Every lane of the row returns the hash.
-__device__ uint64_t row_xxph3_long(const uint8_t* p, uint32_t len, uint64_t seed, uint32_t t) {
-  const uint32_t s4 = t >> 2, pp = t & 3;
-  uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;
-  uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
-  const uint32_t nb = len / 1024;
-  const uint32_t nbS = (len - 1024 * nb) / 64;
-  const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3);
-  const uint8_t* q = p - m + 16 * t;
-  const uint64_t ks0 = psec64(128 + 16 * pp, seed), ks1 = psec64(136 + 16 * pp, seed);
-  // the last stripe (xxph3.h:1539-1542), loaded up front
-  uint64_t l0 = 0, l1 = 0;
-  {
-    const uint8_t* lp = p + len - 64 + 16 * pp;
+// the last stripe (len - 64 + 16 (t%4), xxph3.h:1539-1542), when len % 64
+__device__ __forceinline__ void long_last_load(const uint8_t* p, uint32_t len, uint32_t t, bool act,
+                                               uint64_t& l0, uint64_t& l1) {
+  l0 = l1 = 0;
+  if (act && (len & 63)) {
+    const uint8_t* lp = p + len - 64 + 16 * (t & 3);
     const uint32_t ml = static_cast<uint32_t>(reinterpret_cast<uint64_t>(lp) & 3);
     ld16u(lp - ml, ml, l0, l1);
   }
-  // (rows of one wave may have different block counts: the loop runs to the
-  // wave's largest, wave-uniform around the row sums)
-  for (uint32_t g = 0; __ballot(g <= nb); ++g) {
+}
+
+// Row-wide XXPH3 of a > 240-byte field (xxph3.h:1514-1583, 1630-1637) whose
+// first block `b` and last stripe (l0, l1) are already loaded; every lane of
+// a row with act gets the hash.  Rows may differ in length: the block loop
+// runs to the wave's largest, uniform around the DPP row sums.
+__device__ uint64_t row_long(const uint64_t* S, const uint8_t* p, uint32_t len, uint64_t seed,
+                             bool act, uint32_t t, Block& b, uint64_t l0, uint64_t l1) {
+  const uint32_t pp = t & 3;
+  uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;  // INIT_ACC
+  uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
+  const uint32_t nb = act ? len >> 10 : 0;
+  // the chunk secrets: stripe st's at 8 st + 16 pp (aligned words)
+  uint64_t k0[4], k1[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t off = 8 * ((t >> 2) + 4 * k) + 16 * pp;
+    k0[k] = psec(S, off, seed);
+    k1[k] = psec(S, off + 8, seed);
+  }
+  const uint64_t ks0 = psec(S, 128 + 16 * pp, seed), ks1 = psec(S, 136 + 16 * pp, seed);
+  for (uint32_t g = 0;; ++g) {
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
-    for (uint32_t k = 0; k < 4; ++k) {
-      const uint32_t st = s4 + 4 * k;
-      if (g < nb || (g == nb && st < nbS)) {
-        uint64_t d0, d1;
-        ld16u(q + 1024 * g + 256 * k, m, d0, d1);
-        c0 += d0 + mul32to64(d0 ^ psec64(8 * st + 16 * pp, seed));  // acc_64bits
-        c1 += d1 + mul32to64(d1 ^ psec64(8 * st + 16 * pp + 8, seed));
+    for (uint32_t k = 0; k < 4; ++k)
+      if (b.mask & (1u << k)) {  // acc_64bits: acc[i] += data + lo*hi(data ^ key)
+        c0 += b.d0[k] + mul32to64(b.d0[k] ^ k0[k]);
+        c1 += b.d1[k] + mul32to64(b.d1[k] ^ k1[k]);
       }
-    }
     c0 += row_ror64<4>(c0);
     c1 += row_ror64<4>(c1);
     c0 += row_ror64<8>(c0);
     c1 += row_ror64<8>(c1);
-    if (g <= nb) {
-      acc0 += c0;
-      acc1 += c1;
-    }
+    acc0 += c0;
+    acc1 += c1;
     if (g < nb) {
       acc0 = scramble_acc(acc0, ks0);
       acc1 = scramble_acc(acc1, ks1);
     }
+    if (!__ballot(g < nb)) break;
+    long_block_load(p, len, g + 1, t, act && g < nb, b);
   }
   if (len & 63) {
-    acc0 += l0 + mul32to64(l0 ^ psec64(121 + 16 * pp, seed));
-    acc1 += l1 + mul32to64(l1 ^ psec64(129 + 16 * pp, seed));
+    acc0 += l0 + mul32to64(l0 ^ psec(S, 121 + 16 * pp, seed));
+    acc1 += l1 + mul32to64(l1 ^ psec(S, 129 + 16 * pp, seed));
   }
-  uint64_t h = mul128_fold64(acc0 ^ psec64(11 + 16 * pp, seed), acc1 ^ psec64(19 + 16 * pp, seed));
+  // XXPH3_mergeAccs from secret + 11 (xxph3.h:1554-1582)
+  uint64_t h = mul128_fold64(acc0 ^ psec(S, 11 + 16 * pp, seed), acc1 ^ psec(S, 19 + 16 * pp, seed));
   h += quad_xor64<1>(h);
   h += quad_xor64<2>(h);
   return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + h);
 }
 
-#ifndef FORST_KV_ROWS
-#define FORST_KV_ROWS 1
-#endif
-
 __device__ __forceinline__ bool in_range(uint64_t off, uint64_t len, uint64_t base_len) {
   return off <= base_len && len <= base_len - off;
+}
+
+__device__ __forceinline__ uint64_t shfl64(uint64_t v, uint32_t src) {
+  return mk64(__shfl(static_cast<uint32_t>(v), src), __shfl(static_cast<uint32_t>(v >> 32), src));
+}
+
+// 16 bytes at byte position pos as 4 LE dwords; bytes at or past base_len
+// read as 0 and *avail = how many of the 16 lie inside the buffer
+struct W16 {
+  uint32_t w[4];
+};
+__device__ __forceinline__ W16 load16_bounded(const uint8_t* base, uint64_t base_len, uint64_t pos,
+                                              uint32_t& avail) {
+  W16 r;
+  avail = pos >= base_len ? 0u : base_len - pos >= 16 ? 16u : static_cast<uint32_t>(base_len - pos);
+  const uint64_t q = pos & ~3ull;
+  if (q + 20 <= base_len) {
+    const uint32_t m = static_cast<uint32_t>(pos & 3);
+    const u32x4a4 v = ld16_a4(base + q + vzero());
+    const uint32_t x4 = m ? ld4_a4(base + q + 16 + vzero()) : 0u;
+    r.w[0] = __builtin_amdgcn_alignbyte(v.y, v.x, m);
+    r.w[1] = __builtin_amdgcn_alignbyte(v.z, v.y, m);
+    r.w[2] = __builtin_amdgcn_alignbyte(v.w, v.z, m);
+    r.w[3] = __builtin_amdgcn_alignbyte(x4, v.w, m);
+  } else {
+#pragma unroll
+    for (uint32_t k = 0; k < 4; ++k) r.w[k] = 0;
+    for (uint32_t k = 0; k < avail; ++k) r.w[k >> 2] |= ldu8(base + pos + k) << (8 * (k & 3));
+  }
+  return r;
+}
+__device__ __forceinline__ uint32_t byte_of(const W16& v, uint32_t k) {
+  return (v.w[k >> 2] >> (8 * (k & 3))) & 0xffu;
+}
+// GetVarint32Ptr(p, p + 5, &val) (util/coding.h:109, coding.cc
+// GetVarint32PtrFallback) on window byte k0: the bytes consumed, 0 when five
+// bytes all carry the continuation bit, kVarOut when the varint runs past the
+// buffer (the reference reads on; the engine reports it)
+constexpr uint32_t kVarOut = 0xff;
+__device__ __forceinline__ uint32_t varint32_at(const W16& v, uint32_t k0, uint32_t avail,
+                                                uint32_t& val) {
+  uint32_t r = 0;
+#pragma unroll
+  for (uint32_t j = 0; j < 5; ++j) {
+    if (k0 + j >= avail) return kVarOut;
+    const uint32_t b = byte_of(v, k0 + j);
+    r |= (b & 127u) << (7 * j);  // (shift 28: the bits past 32 drop, as in the reference)
+    if (!(b & 128u)) {
+      val = r;
+      return j + 1;
+    }
+  }
+  return 0;
+}
+
+// MemTable entry (memtable.cc:696-732 layout, :273-307 decode):
+//   varint32 internal_key_len | user_key | tag = seq << 8 | type (LE64) |
+//   varint32 value_len | value | protection_bytes checksum
+// -> key / value / checksum positions, type and seq; returns a KvMemStatus.
+__device__ __forceinline__ uint32_t decode_mem_entry(const KvArgs& a, uint64_t pos, uint64_t& ko,
+                                                     uint32_t& kl, uint64_t& vo, uint32_t& vl,
+                                                     uint64_t& co, uint64_t& tag) {
+  uint32_t av;
+  const W16 e = load16_bounded(a.base, a.base_len, pos, av);
+  uint32_t ikl = 0;
+  const uint32_t n1 = varint32_at(e, 0, av, ikl);
+  if (n1 == kVarOut) return kMemOutOfRange;
+  if (n1 == 0) return kMemBadKeyLength;
+  if (ikl < 8) return kMemKeyTooShort;
+  ko = pos + n1;
+  kl = ikl - 8;
+  const uint64_t tp = ko + kl;
+  uint32_t av2;
+  const W16 t = load16_bounded(a.base, a.base_len, tp, av2);
+  if (av2 < 8) return kMemOutOfRange;
+  tag = mk64(t.w[0], t.w[1]);
+  const uint32_t n2 = varint32_at(t, 8, av2, vl);
+  if (n2 == kVarOut) return kMemOutOfRange;
+  if (n2 == 0) return kMemBadValue;
+  vo = tp + 8 + n2;
+  co = vo + vl;
+  return in_range(co, a.prot_bytes, a.base_len) ? kMemOk : kMemOutOfRange;
+}
+
+// field classes
+constexpr uint32_t kTiny = 0, kShort = 1, kLong = 2, kNone = 3;
+__device__ __forceinline__ uint32_t field_class(bool valid, uint32_t len) {
+  return !valid ? kNone : len <= 16 ? kTiny : len <= 240 ? kShort : kLong;
 }
 
 // MODE: kKvHash (Hash64 per buffer), kKvProtect, kKvVerify
 template <int MODE>
 __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
+  __shared__ uint64_t s_sec[kSecWords];
+  __shared__ uint64_t s_slot[kWaves][64];
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
+  const uint32_t t = lane & 15;
+  if (threadIdx.x < kSecWords) s_sec[threadIdx.x] = threadIdx.x < 24 ? sec64(8 * threadIdx.x) : 0;
+  __syncthreads();
+  const uint64_t* S = s_sec;
+  // this lane's mix16B secret pair (seed applied per field)
+  const uint64_t SA = psec(S, term_secret(t), 0), SB = psec(S, term_secret(t) + 8, 0);
+  uint64_t* slot = s_slot[wave];
+
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves * 64;
   for (uint64_t b0 = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * 64; b0 < a.n;
        b0 += stride) {
+    // ---- lane = entry: descriptors and the op / seq / cf hashes
     const uint64_t i = b0 + lane;
     const bool act = i < a.n;
-    uint64_t ko = 0, vo = 0, co = 0, kseed = kSeedK;
-    uint32_t kl = 0, vl = 0;
+    uint64_t ko = 0, vo = 0, co = 0, kseed = kSeedK, hs = 0;
+    uint32_t kl = 0, vl = 0, mst = kMemOk;
     bool valid = false;
-    if (act) {
+    if (MODE == kKvMemVerify || MODE == kKvMemProtect) {
+      if (act) {
+        uint64_t tag = 0;
+        mst = decode_mem_entry(a, a.key_off[i], ko, kl, vo, vl, co, tag);
+        valid = mst == kMemOk;
+        // ProtectKVO(user_key, value, type).ProtectS(seq) (memtable.cc:298-302)
+        const uint32_t op = static_cast<uint32_t>(tag & 0xff);
+        hs = xxph3_1to3(op, op, op, 1, kSeedO) ^ xxph3_4to8(tag >> 8, 8, kSeedS);
+      }
+    } else if (act) {
       ko = a.key_off[i];
       kl = a.key_len[i];
-      valid = in_range(ko, kl, a.base_len);
+      valid = in_range(ko, kl, a.key_base ? a.key_base_len : a.base_len);
       if (MODE == kKvHash) {
         kseed = a.seeds ? a.seeds[i] : a.seed;
       } else {
         vo = a.val_off[i];
         vl = a.val_len[i];
         valid = valid && in_range(vo, vl, a.base_len);
+        if (a.ops) {  // NPHash64(&op_type, 1, kSeedO)
+          const uint32_t op = a.ops[i];
+          hs ^= xxph3_1to3(op, op, op, 1, kSeedO);
+        }
+        if (a.seqs) hs ^= xxph3_4to8(a.seqs[i], 8, kSeedS);  // native LE bytes
+        if (a.cfs) {
+          const uint64_t cf = a.cfs[i];
+          hs ^= xxph3_4to8(cf | (cf << 32), 4, kSeedC);
+        }
       }
       if (MODE == kKvVerify) {
         co = a.chk_off[i];
         valid = valid && in_range(co, a.prot_bytes, a.base_len);
       }
     }
-    uint64_t h = 0;
-    if (valid && kl <= 240) h ^= xxph3_short(a.base + ko, kl, kseed);
-    if (MODE != kKvHash) {
-      if (valid && vl <= 240) h ^= xxph3_short(a.base + vo, vl, kSeedV);
-      if (valid && a.ops) {  // NPHash64(&op_type, 1, kSeedO)
-        const uint32_t op = a.ops[i];
-        h ^= xxph3_1to3(op, op, op, 1, kSeedO);
+    const uint64_t vmask = __ballot(valid);
+
+    // ---- 16 rounds: row R hashes the key and value of entry 16R + r
+    for (uint32_t r = 0; r < 16; ++r) {
+      const uint32_t src = (lane & 48) | r;
+      if (!(vmask & (0x0001000100010001ull << r))) continue;  // (wave-uniform)
+      const bool rv = (vmask >> src) & 1;
+      const uint64_t rko = shfl64(ko, src);
+      const uint32_t rkl = __shfl(kl, src);
+      const uint64_t rks = MODE == kKvHash ? shfl64(kseed, src) : kSeedK;
+      uint64_t rvo = 0;
+      uint32_t rvl = 0;
+      if (MODE != kKvHash) {
+        rvo = shfl64(vo, src);
+        rvl = __shfl(vl, src);
       }
-      if (valid && a.seqs) h ^= xxph3_4to8(a.seqs[i], 8, kSeedS);  // native LE bytes
-      if (valid && a.cfs) {
-        const uint64_t cf = a.cfs[i];
-        h ^= xxph3_4to8(cf | (cf << 32), 4, kSeedC);
+      const uint32_t kc = field_class(rv, rkl);
+      const uint32_t vc = MODE == kKvHash ? kNone : field_class(rv, rvl);
+      const uint8_t* kp = (a.key_base ? a.key_base : a.base) + rko;
+      const uint8_t* vp = a.base + rvo;
+
+      // -- every load of the round, issued before any of it is used
+      uint64_t kd0 = 0, kd1 = 0, vd0 = 0, vd1 = 0;
+      uint32_t dk = 0, dv = 0;
+      const bool kterm = kc == kShort && term_at(t, rkl, dk);
+      const bool vterm = vc == kShort && term_at(t, rvl, dv);
+      if (kterm) {
+        const uint8_t* e = kp + dk;
+        const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(e) & 3);
+        ld16u(e - m, m, kd0, kd1);
+      } else if (kc == kTiny && t == 7) {
+        tiny_load(kp, rkl, kd0, kd1);
       }
-    }
-    if (FORST_KV_ROWS) {
-      // fields > 240 bytes: four at a time, one per 16-lane row (keys first)
-      uint64_t lk = __ballot(valid && kl > 240);
-      uint64_t lv = MODE != kKvHash ? __ballot(valid && vl > 240) : 0ull;
-      const uint32_t row = lane >> 4, t = lane & 15;
-      while (lk | lv) {
-        uint32_t src = 64, isv = 0;
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-          uint32_t sr = 64, vr = 0;
-          if (lk) {
-            sr = static_cast<uint32_t>(__builtin_ctzll(lk));
-            lk &= lk - 1;
-          } else if (lv) {
-            sr = static_cast<uint32_t>(__builtin_ctzll(lv));
-            lv &= lv - 1;
-            vr = 1;
-          }
-          if (row == r) {
-            src = sr;
-            isv = vr;
-          }
-        }
-        const uint32_t sl = src < 64 ? src : 0;
-        // (the source lane's key and value fields, the row picks one)
-        const uint32_t klo = __shfl(static_cast<uint32_t>(ko), sl);
-        const uint32_t khi = __shfl(static_cast<uint32_t>(ko >> 32), sl);
-        const uint32_t kln = __shfl(kl, sl);
-        uint32_t vlo = 0, vhi = 0, vln = 0;
-        if (MODE != kKvHash) {
-          vlo = __shfl(static_cast<uint32_t>(vo), sl);
-          vhi = __shfl(static_cast<uint32_t>(vo >> 32), sl);
-          vln = __shfl(vl, sl);
-        }
-        const uint32_t flo = isv ? vlo : klo, fhi = isv ? vhi : khi, fl = isv ? vln : kln;
-        const uint32_t slo = __shfl(static_cast<uint32_t>(kseed), sl);
-        const uint32_t shi = __shfl(static_cast<uint32_t>(kseed >> 32), sl);
-        const uint64_t o = src < 64 ? (static_cast<uint64_t>(fhi) << 32) | flo : 0ull;
-        const uint64_t sd = isv ? kSeedV : (static_cast<uint64_t>(shi) << 32) | slo;
-        // (a row without a field hashes the buffer's first 241 bytes, discarded: a
-        // long field exists, so base_len > 240)
-        const uint64_t hv = row_xxph3_long(a.base + o, src < 64 ? fl : 241u, sd, t);
-#pragma unroll
-        for (uint32_t r = 0; r < 4; ++r) {
-          const uint32_t sr = readlane32(src, 16 * r);
-          const uint64_t vr = readlane64(static_cast<uint32_t>(hv), static_cast<uint32_t>(hv >> 32),
-                                         16 * r);
-          if (lane == sr) h ^= vr;
-        }
+      if (vterm) {
+        const uint8_t* e = vp + dv;
+        const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(e) & 3);
+        ld16u(e - m, m, vd0, vd1);
+      } else if (vc == kTiny && t == 6) {
+        tiny_load(vp, rvl, vd0, vd1);
       }
-    }
-    // fields > 240 bytes: the whole wave hashes them one after the other
-    uint64_t lk = FORST_KV_ROWS ? 0ull : __ballot(valid && kl > 240);
-    while (lk) {
-      const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lk));
-      lk &= lk - 1;
-      const uint64_t o = readlane64(static_cast<uint32_t>(ko), static_cast<uint32_t>(ko >> 32), l);
-      const uint32_t n = readlane32(kl, l);
-      const uint64_t sd = readlane64(static_cast<uint32_t>(kseed), static_cast<uint32_t>(kseed >> 32), l);
-      const uint64_t hv = wave_xxph3_long(a.base + o, n, sd, lane);
-      h ^= lane == l ? hv : 0ull;
-    }
-    if (MODE != kKvHash && !FORST_KV_ROWS) {
-      uint64_t lv = __ballot(valid && vl > 240);
-      while (lv) {
-        const uint32_t l = static_cast<uint32_t>(__builtin_ctzll(lv));
-        lv &= lv - 1;
-        const uint64_t o = readlane64(static_cast<uint32_t>(vo), static_cast<uint32_t>(vo >> 32), l);
-        const uint32_t n = readlane32(vl, l);
-        const uint64_t hv = wave_xxph3_long(a.base + o, n, kSeedV, lane);
-        h ^= lane == l ? hv : 0ull;
+      Block vb;
+      uint64_t vl0, vl1;
+      long_block_load(vp, rvl, 0, t, vc == kLong, vb);
+      long_last_load(vp, rvl, t, vc == kLong, vl0, vl1);
+
+      // -- 17..240-byte fields: the row's terms
+      uint64_t h = 0;
+      {
+        const uint64_t tk = kterm ? mul128_fold64(kd0 ^ (SA + rks), kd1 ^ (SB - rks)) : 0;
+        const uint64_t fk = short_finish(tk, rkl);
+        if (kc == kShort) h ^= fk;
       }
+      if (MODE != kKvHash) {
+        const uint64_t tv = vterm ? mul128_fold64(vd0 ^ (SA + kSeedV), vd1 ^ (SB - kSeedV)) : 0;
+        const uint64_t fv = short_finish(tv, rvl);
+        if (vc == kShort) h ^= fv;
+      }
+      // -- 0..16-byte fields: lane 7 the key's, lane 6 the value's
+      {
+        const bool k7 = t == 7 && kc == kTiny, v6 = t == 6 && vc == kTiny;
+        const uint64_t x = tiny_hash(k7 ? kd0 : vd0, k7 ? kd1 : vd1, k7 ? rkl : rvl,
+                                     k7 ? rks : kSeedV);
+        const uint64_t y = (k7 || v6) ? x : 0;
+        h ^= y ^ dpp64<0x121>(y);  // row_ror:1 -> lane 7 also gets lane 6's
+      }
+      // -- > 240-byte fields
+      if (__ballot(vc == kLong)) {
+        const uint64_t hl = row_long(S, vp, rvl, kSeedV, vc == kLong, t, vb, vl0, vl1);
+        if (vc == kLong) h ^= hl;
+      }
+      if (__ballot(kc == kLong)) {  // (keys over 240 bytes: rare, loaded here)
+        Block kb;
+        uint64_t kl0, kl1;
+        long_block_load(kp, rkl, 0, t, kc == kLong, kb);
+        long_last_load(kp, rkl, t, kc == kLong, kl0, kl1);
+        const uint64_t hl = row_long(S, kp, rkl, rks, kc == kLong, t, kb, kl0, kl1);
+        if (kc == kLong) h ^= hl;
+      }
+      if (t == 7) slot[src] = h;
     }
-    if (!valid) h = 0;
-    if (MODE == kKvVerify) {
+    wave_lds_sync();
+    uint64_t h = valid ? hs ^ slot[lane] : 0;
+    wave_lds_sync();  // (the next tile's rounds overwrite the slots)
+
+    if (MODE == kKvMemProtect) {
+      // MemTable::UpdateEntryChecksum (memtable.cc:676-693): Encode(prot_bytes)
+      if (valid && a.write_in_place) {
+        uint8_t* c = const_cast<uint8_t*>(a.base) + co;
+        for (uint32_t b = 0; b < a.prot_bytes; ++b) c[b] = static_cast<uint8_t>(h >> (8 * b));
+      }
+      if (act && a.out) a.out[i] = h;
+      if (act && a.status) a.status[i] = static_cast<uint8_t>(mst);
+    } else if (MODE == kKvVerify || MODE == kKvMemVerify) {
       // ProtectionInfo<T>::Verify (kv_checksum.h:117-133): low prot_bytes bytes, LE
       uint64_t stored = 0;
-      if (valid)
-        for (uint32_t b = 0; b < a.prot_bytes; ++b)
-          stored |= static_cast<uint64_t>(ldu8(a.base + co + b)) << (8 * b);
+      if (valid) {
+        const uint8_t* c = a.base + co;
+        if (a.prot_bytes == 8) {
+          stored = ldu64(c);
+        } else if (a.prot_bytes == 4) {
+          stored = ldu32(c);
+        } else {
+          for (uint32_t b = 0; b < a.prot_bytes; ++b)
+            stored |= static_cast<uint64_t>(ldu8(c + b)) << (8 * b);
+        }
+      }
       const uint64_t mask = a.prot_bytes >= 8 ? ~0ull : ((1ull << (8 * a.prot_bytes)) - 1);
       const bool ok = valid && ((stored ^ h) & mask) == 0;
       if (act && a.out) a.out[i] = h;
       if (act && a.ok) a.ok[i] = ok ? 1 : 0;
+      if (MODE == kKvMemVerify && act && a.status)
+        a.status[i] = static_cast<uint8_t>(mst != kMemOk ? mst : ok ? kMemOk : kMemMismatch);
       const uint64_t badm = __ballot(act && !ok);
       if (a.mismatches && badm && lane == 0)
         atomicAdd(a.mismatches, static_cast<unsigned long long>(__popcll(badm)));
     } else if (act) {
-      a.out[i] = h;
+      if (a.out) a.out[i] = h;
+      if (a.enc_out)  // Encode(prot_bytes) (kv_checksum.h:97-115)
+        for (uint32_t b = 0; b < a.prot_bytes; ++b)
+          a.enc_out[i * a.prot_bytes + b] = static_cast<uint8_t>(h >> (8 * b));
     }
   }
 }
@@ -396,8 +526,12 @@ hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char**
   const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
   const uint64_t per_wg = uint64_t(kWaves) * 64;
+  static const uint32_t wg_per_cu = [] {
+    const char* e = std::getenv("FORST_KV_WG_PER_CU");
+    return e ? static_cast<uint32_t>(std::max(1, atoi(e))) : 8u;
+  }();
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
-      1, std::min<uint64_t>((a.n + per_wg - 1) / per_wg, uint64_t(di.num_cus) * 8)));
+      1, std::min<uint64_t>((a.n + per_wg - 1) / per_wg, uint64_t(di.num_cus) * wg_per_cu)));
   switch (mode) {
     case kKvHash:
       *name = "kv_kernel<hash64>";
@@ -406,6 +540,14 @@ hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char**
     case kKvProtect:
       *name = "kv_kernel<protect>";
       hipLaunchKernelGGL(kv_kernel<kKvProtect>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case kKvMemVerify:
+      *name = "kv_kernel<mem_verify>";
+      hipLaunchKernelGGL(kv_kernel<kKvMemVerify>, dim3(grid), dim3(kThreads), 0, stream, a);
+      break;
+    case kKvMemProtect:
+      *name = "kv_kernel<mem_protect>";
+      hipLaunchKernelGGL(kv_kernel<kKvMemProtect>, dim3(grid), dim3(kThreads), 0, stream, a);
       break;
     default:
       *name = "kv_kernel<verify>";

@@ -349,6 +349,108 @@ def kv_verify_batch(base, key_offsets, key_sizes, value_offsets, value_sizes, pr
     return c, o, mismatches
 
 
+def memtable_verify_batch(base, entry_offsets, protection_bytes, computed=True, status=True,
+                          mismatches=None, stream=None):
+    """MemTable::VerifyEntryChecksum per encoded entry (db/memtable.cc:273-307),
+    decoded on the device.  Returns (computed, status, mismatches); status
+    codes as in include/forst_checksum.h."""
+    _dev_u8(base)
+    n = entry_offsets.numel()
+    dev = base.device
+    c = torch.empty(n, dtype=torch.uint64, device=dev) if computed is True else computed
+    s = torch.empty(n, dtype=torch.uint8, device=dev) if status is True else status
+    if mismatches is None:
+        mismatches = torch.zeros(1, dtype=torch.int64, device=dev)
+    check(lib().forst_memtable_verify_batch(base.data_ptr(), base.numel(), entry_offsets.data_ptr(),
+                                            n, protection_bytes, _p(c), _p(s), _p(mismatches),
+                                            _stream(stream)))
+    return c, s, mismatches
+
+
+def memtable_protect_batch(base, entry_offsets, protection_bytes, write_in_place=True, out=True,
+                           status=True, stream=None):
+    """MemTable::UpdateEntryChecksum per encoded entry (db/memtable.cc:676-693):
+    the protection value, written in place as Encode(protection_bytes).
+    Returns (out, status)."""
+    _dev_u8(base)
+    n = entry_offsets.numel()
+    dev = base.device
+    o = torch.empty(n, dtype=torch.uint64, device=dev) if out is True else out
+    s = torch.empty(n, dtype=torch.uint8, device=dev) if status is True else status
+    check(lib().forst_memtable_protect_batch(base.data_ptr(), base.numel(),
+                                             entry_offsets.data_ptr(), n, protection_bytes,
+                                             1 if write_in_place else 0, _p(o), _p(s),
+                                             _stream(stream)))
+    return o, s
+
+
+def write_batch_protect_batch(base, rep_offsets, rep_sizes, capacity=None, stream=None):
+    """WriteBatchInternal::UpdateProtectionInfo per WriteBatch rep
+    (db/write_batch.cc:3164-3181), parsed on the device.  Returns
+    (prot, first_entry, status, n_protected): rep b's protection values are
+    prot[first_entry[b]:first_entry[b+1]].  Synchronous (one count read-back)."""
+    _dev_u8(base)
+    n = _desc(rep_offsets, rep_sizes)
+    dev = base.device
+    first = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    nprot = torch.empty(n, dtype=torch.int32, device=dev)
+    total = ctypes.c_uint64()
+    if capacity is None:  # size from the header counts: a first call with capacity 0
+        rc = lib().forst_write_batch_protect_batch(base.data_ptr(), base.numel(),
+                                                   rep_offsets.data_ptr(), rep_sizes.data_ptr(),
+                                                   n, first.data_ptr(), None, 0, None, None,
+                                                   ctypes.byref(total), _stream(stream))
+        if rc != 0 and total.value == 0:
+            check(rc)
+        capacity = total.value
+    prot = torch.empty(max(1, capacity), dtype=torch.uint64, device=dev)
+    check(lib().forst_write_batch_protect_batch(base.data_ptr(), base.numel(),
+                                                rep_offsets.data_ptr(), rep_sizes.data_ptr(), n,
+                                                first.data_ptr(), prot.data_ptr(), capacity,
+                                                status.data_ptr(), nprot.data_ptr(),
+                                                ctypes.byref(total), _stream(stream)))
+    return prot[:total.value], first, status, nprot
+
+
+class BlockKind(enum.IntFlag):
+    """kinds[] of block_kv_checksum_batch (include/forst_checksum.h)"""
+    DATA = 0
+    INDEX = 1
+    META = 2
+    VALUE_IS_FULL = 4
+    HAS_FIRST_KEY = 8
+
+
+def block_kv_checksum_batch(base, block_offsets, block_sizes, kinds, protection_bytes,
+                            capacity=None, stream=None):
+    """Block::Initialize{Data,Index,MetaIndex}BlockProtectionInfo per block
+    (table/block_based/block.cc:1113-1235), decoded on the device.  Returns
+    (kv_checksums u8, prot u64, first_key, status): block b's kv_checksum_ is
+    kv_checksums[first_key[b] * pb : first_key[b+1] * pb].  Synchronous."""
+    _dev_u8(base)
+    n = _desc(block_offsets, block_sizes)
+    dev = base.device
+    first = torch.empty(n + 1, dtype=torch.int64, device=dev)
+    status = torch.empty(n, dtype=torch.uint8, device=dev)
+    total = ctypes.c_uint64()
+    args = (base.data_ptr(), base.numel(), block_offsets.data_ptr(), block_sizes.data_ptr(),
+            kinds.data_ptr(), n, protection_bytes, first.data_ptr())
+    if capacity is None:
+        rc = lib().forst_block_kv_checksum_batch(*args, None, None, 0, None, ctypes.byref(total),
+                                                 _stream(stream))
+        if rc != 0 and total.value == 0:
+            check(rc)
+        capacity = total.value
+    enc = torch.empty(max(1, capacity) * protection_bytes, dtype=torch.uint8, device=dev)
+    prot = torch.empty(max(1, capacity), dtype=torch.uint64, device=dev)
+    check(lib().forst_block_kv_checksum_batch(*args, enc.data_ptr(), prot.data_ptr(), capacity,
+                                              status.data_ptr(), ctypes.byref(total),
+                                              _stream(stream)))
+    m = total.value
+    return enc[:m * protection_bytes], prot[:m], first, status
+
+
 def fill_stream(dev_u8, start, seed, stream=None):
     """Synthetic splitmix64 byte stream written on the device."""
     _dev_u8(dev_u8)

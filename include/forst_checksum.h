@@ -44,6 +44,10 @@
  *                                  (db/kv_checksum.h:296-460)
  *   forst_kv_verify_batch       <- ProtectionInfo<T>::Verify
  *                                  (db/kv_checksum.h:117-133)
+ *   forst_memtable_verify_batch <- MemTable::VerifyEntryChecksum
+ *                                  (db/memtable.cc:273-307)
+ *   forst_memtable_protect_batch<- MemTable::UpdateEntryChecksum
+ *                                  (db/memtable.cc:676-693)
  *
  * Conventions
  *  - All array/buffer pointers are DEVICE pointers (hipMalloc'd, or host
@@ -374,6 +378,87 @@ int forst_kv_verify_batch(const uint8_t* base, uint64_t base_len,
                           const uint32_t* cf_ids, uint32_t protection_bytes,
                           const uint64_t* checksum_offsets, uint64_t* computed, uint8_t* ok,
                           unsigned long long* mismatches, uint64_t n, void* stream);
+
+/* Encoded MemTable entries (a15 at its memtable call site).  Entry i starts at
+ * base + entry_offsets[i] in MemTable::Add's layout (db/memtable.cc:696-732):
+ *   varint32 internal_key_len | user_key | LE64 (seq << 8 | type) |
+ *   varint32 value_len | value | protection_bytes checksum
+ * and is decoded on the device (klen, tag split into seq and type, vlen).
+ *
+ * forst_memtable_verify_batch <- MemTable::VerifyEntryChecksum
+ *   (db/memtable.cc:273-307): ProtectKVO(user_key, value, type).ProtectS(seq)
+ *   .Verify(protection_bytes, checksum).  status[i] (nullable) =
+ *     0 OK
+ *     1 "Unable to parse internal key length"
+ *     2 "Memtable entry internal key length too short."
+ *     3 "Unable to parse internal key value"
+ *     4 "Corrupted memtable entry, per key-value checksum verification failed."
+ *     5 the entry reaches past base_len (the reference would read on)
+ *   computed[i] (nullable) = the 64-bit protection value (0 unless parsed);
+ *   *mismatches (device counter, nullable) += entries with status != 0.
+ * forst_memtable_protect_batch <- MemTable::UpdateEntryChecksum
+ *   (db/memtable.cc:676-693, kv_prot_info == nullptr): the same value, written
+ *   as Encode(protection_bytes) at the entry's checksum bytes when
+ *   write_in_place; out / status nullable (status 0, 1, 2, 3 or 5). */
+int forst_memtable_verify_batch(const uint8_t* base, uint64_t base_len,
+                                const uint64_t* entry_offsets, uint64_t n,
+                                uint32_t protection_bytes, uint64_t* computed, uint8_t* status,
+                                unsigned long long* mismatches, void* stream);
+int forst_memtable_protect_batch(uint8_t* base, uint64_t base_len, const uint64_t* entry_offsets,
+                                 uint64_t n, uint32_t protection_bytes, int write_in_place,
+                                 uint64_t* out, uint8_t* status, void* stream);
+
+/* WriteBatch reps (a15 at its WriteBatch call site) <-
+ * WriteBatchInternal::UpdateProtectionInfo(wb, 8) (db/write_batch.cc:3164-3181):
+ * for every rep b = base[rep_offsets[b] .. + rep_sizes[b]) (e.g. the logical
+ * records forst_wal_recover_batch emits), WriteBatch::Iterate's parse
+ * (write_batch.cc:361-716) on the device and, per data record in order,
+ * ProtectionInfoUpdater's ProtectKVO(key, value, op).ProtectC(cf)
+ * (write_batch.cc:3016-3080; CF variants hash as their base op; Delete /
+ * SingleDelete with an empty value).  Rep b's values land at
+ * prot[first_entry[b] .. first_entry[b+1]) (first_entry: n_reps + 1 device
+ * u64, from the reps' header counts); slots no record filled hold 0.
+ * status[b] (nullable): 0 OK, 1 "malformed WriteBatch (too small)",
+ * 2 "bad WriteBatch Put", 3 "bad WriteBatch Delete", 4 "bad WriteBatch
+ * DeleteRange", 5 "bad WriteBatch Merge", 6 "bad WriteBatch BlobIndex",
+ * 7 "bad WriteBatch Blob", 8 "bad EndPrepare XID", 9 "bad commit timestamp",
+ * 10 "bad Commit XID", 11 "bad Rollback XID", 12 "bad WriteBatch PutEntity",
+ * 13 "unknown WriteBatch tag", 14 "WriteBatch has wrong count", 15 the rep
+ * reaches past base_len.  n_protected[b] (nullable) = slots filled.
+ * Synchronous: *n_total (host) = first_entry[n_reps]; FORST_EINVAL when it
+ * exceeds capacity (call again with capacity >= *n_total). */
+int forst_write_batch_protect_batch(const uint8_t* base, uint64_t base_len,
+                                    const uint64_t* rep_offsets, const uint32_t* rep_sizes,
+                                    uint64_t n_reps, uint64_t* first_entry, uint64_t* prot,
+                                    uint64_t capacity, uint8_t* status, uint32_t* n_protected,
+                                    uint64_t* n_total, void* stream);
+
+/* Block protection (a15 at its block-load call site) <-
+ * Block::InitializeDataBlockProtectionInfo / InitializeIndexBlockProtectionInfo
+ * / InitializeMetaIndexBlockProtectionInfo (table/block_based/block.cc:1113-1235,
+ * option block_protection_bytes_per_key, include/rocksdb/advanced_options.h:1227):
+ * for every uncompressed block b = base[block_offsets[b] .. + block_sizes[b])
+ * (no trailer), its entries are decoded on the device as the block iterators
+ * decode them -- restart array / data-block hash index geometry, shared /
+ * non-shared key prefixes (each full key rebuilt in scratch), index values
+ * delta-encoded or full -- and per entry, in order,
+ * ProtectionInfo64().ProtectKV(key, value).Encode(protection_bytes) (block.h:
+ * 271-274 GenerateKVChecksum) is written: block b's kv_checksum_ is
+ * kv_checksums[first_key[b] * protection_bytes .. first_key[b+1] * protection_bytes)
+ * (first_key: n_blocks + 1 device u64); prot (nullable, capacity u64) gets the
+ * full 64-bit values.  kinds[b]: 0 data, 1 index, 2 metaindex, | 4 index values
+ * not delta-encoded (value_is_full), | 8 index values carry the first key
+ * (kBinarySearchWithFirstKey).  status[b] (nullable): 0 OK, 1 bad block
+ * contents (the reference's size_ = 0 error marker), 2 "bad entry in block",
+ * 3 the block reaches past base_len; a failing block gets no keys.
+ * Synchronous: *n_total (host) = the key total; FORST_EINVAL when it exceeds
+ * capacity (call again with capacity >= *n_total). */
+int forst_block_kv_checksum_batch(const uint8_t* base, uint64_t base_len,
+                                  const uint64_t* block_offsets, const uint32_t* block_sizes,
+                                  const uint8_t* kinds, uint64_t n_blocks,
+                                  uint32_t protection_bytes, uint64_t* first_key,
+                                  uint8_t* kv_checksums, uint64_t* prot, uint64_t capacity,
+                                  uint8_t* status, uint64_t* n_total, void* stream);
 
 /* Bench/test utility: fill dev[0 .. n) with bytes [start, start+n) of the
  * splitmix64 stream `seed` (SURVEY.md §8d synthetic inputs). */

@@ -763,6 +763,64 @@ int oracle_kv_verify(uint64_t prot, uint32_t len, const void* stored) {
   return ((s ^ prot) & mask) == 0;
 }
 
+/* util/coding.h:109 GetVarint32Ptr(p, limit) (+ coding.cc
+ * GetVarint32PtrFallback): bytes consumed, 0 on failure.  `avail` bounds the
+ * read (the reference reads up to limit regardless); -1 when it cuts in. */
+static int varint32_ptr(const uint8_t* p, size_t avail, size_t limit, uint32_t* v) {
+  uint32_t r = 0;
+  for (size_t j = 0; j < 5 && j < limit; j++) {
+    if (j >= avail) return -1;
+    const uint32_t b = p[j];
+    r |= (b & 127u) << (7 * j);
+    if (!(b & 128u)) {
+      *v = r;
+      return (int)j + 1;
+    }
+  }
+  return 0;
+}
+
+/* MemTable::VerifyEntryChecksum (db/memtable.cc:273-307) on the entry at p
+ * with `avail` readable bytes: 0 OK, 1 "Unable to parse internal key length",
+ * 2 "... internal key length too short.", 3 "Unable to parse internal key
+ * value", 4 checksum mismatch, 5 the entry runs past avail (the engine's
+ * report; the reference would read on).  *computed = the protection value
+ * ProtectKVO(user_key, value, type).ProtectS(seq) (0 unless parsed). */
+int oracle_memtable_verify(const uint8_t* p, size_t avail, uint32_t prot_bytes,
+                           uint64_t* computed) {
+  *computed = 0;
+  uint32_t ikl = 0, vl = 0;
+  const int n1 = varint32_ptr(p, avail, 5, &ikl);
+  if (n1 < 0) return 5;
+  if (n1 == 0) return 1;
+  if (ikl < 8) return 2;
+  const size_t ko = (size_t)n1, kl = ikl - 8;
+  if (ko + kl + 8 > avail) return 5;
+  uint64_t tag;
+  memcpy(&tag, p + ko + kl, 8);
+  const size_t vp = ko + kl + 8;
+  const int n2 = varint32_ptr(p + vp, avail - vp, 5, &vl);
+  if (n2 < 0) return 5;
+  if (n2 == 0) return 3;
+  const size_t vo = vp + (size_t)n2;
+  if (vo + vl + prot_bytes > avail) return 5;
+  /* UnPackSequenceAndType (dbformat.h): seq = tag >> 8, type = tag & 0xff */
+  *computed = oracle_kv_protect(p + ko, kl, p + vo, vl, (int)(tag & 0xff), 1, tag >> 8, 0, 0);
+  return oracle_kv_verify(*computed, prot_bytes, p + vo + vl) ? 0 : 4;
+}
+
+void oracle_memtable_verify_batch(const uint8_t* base, size_t base_len, const uint64_t* offsets,
+                                  size_t n, uint32_t prot_bytes, uint64_t* computed,
+                                  uint8_t* status) {
+  for (size_t i = 0; i < n; i++) {
+    const size_t o = offsets[i];
+    status[i] = (uint8_t)(o > base_len ? 5
+                                       : oracle_memtable_verify(base + o, base_len - o, prot_bytes,
+                                                                &computed[i]));
+    if (o > base_len) computed[i] = 0;
+  }
+}
+
 /* ======================================================================== */
 /* Block checksum dispatcher (table/format.cc, table/format.h)               */
 /* ======================================================================== */

@@ -45,6 +45,11 @@ uint64_t oracle_kv_protect(const void* key, size_t klen, const void* value, size
                            int op_type, int has_seq, uint64_t seq, int has_cf, uint32_t cf);
 /* ProtectionInfo<T>::Verify (kv_checksum.h:117-133); 1 if the low len bytes match */
 int oracle_kv_verify(uint64_t prot, uint32_t len, const void* stored);
+int oracle_memtable_verify(const uint8_t* p, size_t avail, uint32_t prot_bytes,
+                           uint64_t* computed);
+void oracle_memtable_verify_batch(const uint8_t* base, size_t base_len, const uint64_t* offsets,
+                                  size_t n, uint32_t prot_bytes, uint64_t* computed,
+                                  uint8_t* status);
 /* batch forms matching forst_hash64_batch / forst_kv_{protect,verify}_batch */
 void oracle_hash64_batch(const uint8_t* base, const uint64_t* offsets, const uint32_t* lengths,
                          const uint64_t* seeds, uint64_t seed, uint64_t* out, size_t n);

@@ -6,6 +6,7 @@ product package (forst_amd/), which has no CPU fallback.
 """
 import ctypes
 import os
+import struct
 import subprocess
 
 import numpy as np
@@ -61,6 +62,7 @@ def lib():
             "oracle_kv_verify": (i, [u64, u32, vp]),
             "oracle_hash64_batch": (None, [vp, vp, vp, vp, u64, vp, sz]),
             "oracle_kv_protect_batch": (None, [vp, vp, vp, vp, vp, vp, vp, vp, vp, sz]),
+            "oracle_memtable_verify_batch": (None, [vp, sz, vp, sz, u32, vp, vp]),
             "oracle_splitmix64": (u64, [u64]),
             "oracle_fill_stream": (None, [vp, u64, u64, u64]),
         }
@@ -295,6 +297,92 @@ def kv_protect_batch(base, key_offsets, key_sizes, value_offsets, value_sizes, o
     lib().oracle_kv_protect_batch(_ptr(base), *[_ptr(a) for a in arrs], *[_ptr(a) for a in opt],
                                   _ptr(out), n)
     return out
+
+
+def memtable_verify_batch(base, base_len, offsets, prot_bytes):
+    """MemTable::VerifyEntryChecksum per encoded entry (db/memtable.cc:273-307):
+    (computed, status) -- status codes as include/forst_checksum.h"""
+    offsets = np.ascontiguousarray(offsets, np.uint64)
+    n = len(offsets)
+    comp = np.zeros(n, np.uint64)
+    st = np.zeros(n, np.uint8)
+    lib().oracle_memtable_verify_batch(_ptr(base), base_len, _ptr(offsets), n, prot_bytes,
+                                       _ptr(comp), _ptr(st))
+    return comp, st
+
+
+MEM_STATUS = {0: "OK",
+              1: "Corruption: Unable to parse internal key length",
+              2: "Corruption: Memtable entry internal key length too short.",
+              3: "Corruption: Unable to parse internal key value",
+              4: "Corruption: Corrupted memtable entry, per key-value checksum verification "
+                 "failed."}  # db/memtable.cc:280-306
+
+WB_STATUS = {0: "OK", 1: "Corruption: malformed WriteBatch (too small)",
+             2: "Corruption: bad WriteBatch Put", 3: "Corruption: bad WriteBatch Delete",
+             4: "Corruption: bad WriteBatch DeleteRange", 5: "Corruption: bad WriteBatch Merge",
+             6: "Corruption: bad WriteBatch BlobIndex", 7: "Corruption: bad WriteBatch Blob",
+             8: "Corruption: bad EndPrepare XID", 9: "Corruption: bad commit timestamp",
+             10: "Corruption: bad Commit XID", 11: "Corruption: bad Rollback XID",
+             12: "Corruption: bad WriteBatch PutEntity", 13: "Corruption: unknown WriteBatch tag",
+             14: "Corruption: WriteBatch has wrong count"}  # db/write_batch.cc:361-716
+
+# ReadRecordFromWriteBatch (write_batch.cc:361-475): tag -> (has cf, parts, error,
+# ProtectionInfoUpdater op type (write_batch.cc:3023-3052) or None)
+_WB_TAGS = {0x05: (1, "kv", 2, 0x01), 0x01: (0, "kv", 2, 0x01),
+            0x04: (1, "k", 3, 0x00), 0x08: (1, "k", 3, 0x07), 0x00: (0, "k", 3, 0x00),
+            0x07: (0, "k", 3, 0x07), 0x0E: (1, "kv", 4, 0x0F), 0x0F: (0, "kv", 4, 0x0F),
+            0x06: (1, "kv", 5, 0x02), 0x02: (0, "kv", 5, 0x02), 0x10: (1, "kv", 6, 0x11),
+            0x11: (0, "kv", 6, 0x11), 0x17: (1, "kv", 12, 0x16), 0x16: (0, "kv", 12, 0x16),
+            0x03: (0, "x", 7, None), 0x0D: (0, "", 0, None), 0x09: (0, "", 0, None),
+            0x12: (0, "", 0, None), 0x13: (0, "", 0, None), 0x0A: (0, "x", 8, None),
+            0x0B: (0, "x", 10, None), 0x15: (0, "kx", 9, None), 0x0C: (0, "x", 11, None)}
+
+
+def _wb_varint(b, p, end):
+    """GetVarint32 over input [p, end): (value, next p) or None"""
+    r = 0
+    for j in range(5):
+        if p + j >= end:
+            return None
+        x = b[p + j]
+        r |= (x & 127) << (7 * j)
+        if not x & 128:
+            return r & 0xFFFFFFFF, p + j + 1
+    return None
+
+
+def write_batch_protect(rep):
+    """WriteBatchInternal::UpdateProtectionInfo(wb, 8) restated
+    (write_batch.cc:3164-3181, Iterate :477-716, ReadRecordFromWriteBatch
+    :361-475): (status code as WB_STATUS, [protection values of the data
+    records in order])"""
+    b = bytes(rep)
+    if len(b) < 12:
+        return 1, []
+    count = struct.unpack_from("<I", b, 8)[0]
+    p, end, out = 12, len(b), []
+    while p < end:
+        tag = b[p]
+        p += 1
+        if tag not in _WB_TAGS:
+            return 13, out
+        has_cf, parts, err, op = _WB_TAGS[tag]
+        cf, sl = 0, []
+        if has_cf:
+            v = _wb_varint(b, p, end)
+            if v is None:
+                return err, out
+            cf, p = v
+        for i, part in enumerate(parts):
+            v = _wb_varint(b, p, end)
+            if v is None or end - v[1] < v[0]:
+                return (10 if tag == 0x15 and i == 1 else err), out
+            sl.append(b[v[1]:v[1] + v[0]])
+            p = v[1] + v[0]
+        if op is not None:
+            out.append(kv_protect(sl[0], sl[1] if len(sl) > 1 else b"", op, cf=cf))
+    return (14 if len(out) != count else 0), out
 
 
 def splitmix64(x):

@@ -33,3 +33,16 @@ def kats():
 
     with open(os.path.join(GOLDEN, "kat_reference_tests.json")) as f:
         return json.load(f)
+
+
+@pytest.fixture(scope="session")
+def kv_sites():
+    """reference-made a15 call-site fixtures (tests/golden/gen_kv_golden.py)"""
+    import json
+
+    import numpy as np
+
+    with open(os.path.join(GOLDEN, "kv_sites.json")) as f:
+        meta = json.load(f)
+    z = np.load(os.path.join(GOLDEN, "kv_sites.npz"), allow_pickle=False)
+    return meta, {k: z[k] for k in z.files}

@@ -40,6 +40,12 @@ def lib():
             "forst_kv_protect_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, vp, u64, vp]),
             "forst_kv_verify_batch": (i, [vp, u64, vp, vp, vp, vp, vp, vp, vp, u32, vp, vp, vp,
                                           vp, u64, vp]),
+            "forst_memtable_verify_batch": (i, [vp, u64, vp, u64, u32, vp, vp, vp, vp]),
+            "forst_memtable_protect_batch": (i, [vp, u64, vp, u64, u32, i, vp, vp, vp]),
+            "forst_write_batch_protect_batch": (i, [vp, u64, vp, vp, u64, vp, vp, u64, vp, vp,
+                                                    vp, vp]),
+            "forst_block_kv_checksum_batch": (i, [vp, u64, vp, vp, vp, u64, u32, vp, vp, vp, u64,
+                                                  vp, vp, vp]),
         }
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
@@ -210,6 +216,71 @@ def kv_verify(base, ko, ks, vo, vs, prot_bytes, chk, ops=None, seqs=None, cfs=No
                                      *[_p(a) for a in opt], prot_bytes, _p(chk), _p(comp),
                                      _p(ok), _p(bad), n, None))
     return comp, ok, int(bad[0])
+
+
+def memtable_verify(base, offs, prot_bytes):
+    """-> (computed, status, mismatches)"""
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    comp = np.zeros(len(offs), np.uint64)
+    st = np.zeros(len(offs), np.uint8)
+    bad = np.zeros(1, np.uint64)
+    _chk(lib().forst_memtable_verify_batch(_p(base), base.nbytes, _p(offs), len(offs), prot_bytes,
+                                           _p(comp), _p(st), _p(bad), None))
+    return comp, st, int(bad[0])
+
+
+def memtable_protect(base, offs, prot_bytes):
+    """-> (buffer with the checksums written in place, values, status)"""
+    b = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    out = np.zeros(len(offs), np.uint64)
+    st = np.zeros(len(offs), np.uint8)
+    _chk(lib().forst_memtable_protect_batch(_p(b), b.nbytes, _p(offs), len(offs), prot_bytes, 1,
+                                            _p(out), _p(st), None))
+    return b.copy(), out, st
+
+
+def write_batch_protect(base, offs, lens):
+    """-> (prot, first_entry, status, n_protected)"""
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    lens = np.ascontiguousarray(lens, np.uint32)
+    n = len(offs)
+    first = np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.uint8)
+    nprot = np.zeros(n, np.uint32)
+    total = ctypes.c_uint64()
+    lib().forst_write_batch_protect_batch(_p(base), base.nbytes, _p(offs), _p(lens), n,
+                                          _p(first), None, 0, None, None, ctypes.byref(total),
+                                          None)
+    prot = np.zeros(max(1, total.value), np.uint64)
+    _chk(lib().forst_write_batch_protect_batch(_p(base), base.nbytes, _p(offs), _p(lens), n,
+                                               _p(first), _p(prot), total.value, _p(st),
+                                               _p(nprot), ctypes.byref(total), None))
+    return prot[:total.value], first, st, nprot
+
+
+def block_kv_checksum(base, offs, sizes, kinds, pb):
+    """-> (kv_checksums u8, prot u64, first_key, status)"""
+    base = _aligned(base)
+    offs = np.ascontiguousarray(offs, np.uint64)
+    sizes = np.ascontiguousarray(sizes, np.uint32)
+    kinds = np.ascontiguousarray(kinds, np.uint8)
+    n = len(offs)
+    first = np.zeros(n + 1, np.uint64)
+    st = np.zeros(n, np.uint8)
+    total = ctypes.c_uint64()
+    lib().forst_block_kv_checksum_batch(_p(base), base.nbytes, _p(offs), _p(sizes), _p(kinds), n,
+                                        pb, _p(first), None, None, 0, None, ctypes.byref(total),
+                                        None)
+    m = total.value
+    enc = np.zeros(max(1, m) * pb, np.uint8)
+    prot = np.zeros(max(1, m), np.uint64)
+    _chk(lib().forst_block_kv_checksum_batch(_p(base), base.nbytes, _p(offs), _p(sizes),
+                                             _p(kinds), n, pb, _p(first), _p(enc), _p(prot), m,
+                                             _p(st), ctypes.byref(total), None))
+    return enc[:m * pb], prot[:m], first, st
 
 
 def wal_recover(log, log_number=0, mode=2, cap=None):

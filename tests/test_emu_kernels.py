@@ -481,3 +481,55 @@ def test_emu_raw_split_sparse_long():
                     np.uint32)
     bad = np.nonzero(got != want)[0]
     assert len(bad) == 0, (len(bad), bad[:8].tolist(), sizes[bad[:8]].tolist())
+
+
+# ---- a15 at the reference's call sites (kv_sites fixtures, gen_kv_golden.py) --
+def test_emu_memtable_entries_vs_reference(kv_sites):
+    import kvsites
+
+    for name, base, offs, pb, want in kvsites.memtable_cases(*kv_sites):
+        comp, st, bad = emu.memtable_verify(base, offs, pb)
+        assert [O.MEM_STATUS[int(s)] for s in st] == want, name
+        ocomp, ost = O.memtable_verify_batch(base, len(base), offs, pb)
+        assert (comp == ocomp).all() and bad == int((st != 0).sum()), name
+        if not name.endswith("_corrupt") and name != "crafted":
+            # MemTable::UpdateEntryChecksum in place over zeroed checksum bytes
+            z = base.copy()
+            for o in offs:
+                c = kvsites.mem_checksum_pos(base, int(o))
+                z[c:c + pb] = 0
+            b2, out, pst = emu.memtable_protect(z, offs, pb)
+            assert (out == comp).all() and (pst == 0).all()
+            assert (b2[:len(base)] == base).all(), name
+
+
+def test_emu_write_batch_vs_reference(kv_sites):
+    import kvsites
+
+    base, offs, lens, reps = kvsites.write_batch_case(*kv_sites)
+    prot, first, st, nprot = emu.write_batch_protect(base, offs, lens)
+    for j, (name, status, want) in enumerate(reps):
+        assert O.WB_STATUS[int(st[j])] == status, name
+        got = prot[int(first[j]):int(first[j]) + int(nprot[j])]
+        assert [int(x) for x in got] == [int(x) for x in want][:len(got)], name
+        if status == "OK":
+            assert len(got) == len(want), name
+
+
+def test_emu_block_kv_checksums_vs_reference(kv_sites):
+    """Block::Initialize*BlockProtectionInfo's kv_checksum_ (block.cc:1113-1235)
+    for data / index / metaindex blocks of reference-written SSTs"""
+    import kvsites
+
+    base, offs, sizes, kinds, cases = kvsites.block_case(*kv_sites)
+    for pb in (8, 2):
+        enc, prot, first, st = emu.block_kv_checksum(base, offs, sizes, kinds, pb)
+        for j, c in enumerate(cases):
+            nk = int(first[j + 1] - first[j])
+            want = c[f"keys_{pb}"]
+            if want < 0:
+                assert st[j] != 0 and nk == 0, c
+                continue
+            assert st[j] == 0 and nk == want, (c["src"], c["kind_name"], nk, want)
+            got = enc[int(first[j]) * pb:int(first[j + 1]) * pb].tobytes().hex()
+            assert got == c[f"kv_checksum_{pb}"], (c["src"], c["kind_name"])

@@ -1,0 +1,198 @@
+"""GPU parity for a15 at the reference's own call-site layouts, through the C ABI:
+encoded MemTable entries (db/memtable.cc:273-307, :676-732) and WriteBatch reps
+(db/write_batch.cc:361-716, :3016-3181), decoded on the device.  Pinned by the
+reference-made fixtures (tests/golden/gen_kv_golden.py: the reference's own
+MemTable::Add / VerifyEntryChecksum and WriteBatch::Iterate) and, at full size,
+compared entry for entry with the oracle (itself pinned to those fixtures by
+tests/test_oracle_golden.py)."""
+import struct
+
+import numpy as np
+import pytest
+
+pytestmark = pytest.mark.gpu
+
+torch = pytest.importorskip("torch")
+if not torch.cuda.is_available():
+    pytest.skip("needs a GPU", allow_module_level=True)
+
+from forst_amd import engine  # noqa: E402
+from oracle import oracle as O  # noqa: E402
+import kvsites  # noqa: E402
+
+DEV = "cuda"
+
+
+def d(a):
+    return torch.from_numpy(np.ascontiguousarray(a)).to(DEV)
+
+
+def host(t):
+    return t.cpu().numpy()
+
+
+def test_memtable_fixtures(kv_sites):
+    for name, base, offs, pb, want in kvsites.memtable_cases(*kv_sites):
+        comp, st, bad = engine.memtable_verify_batch(d(base), d(offs.view(np.int64)), pb)
+        st = host(st)
+        assert [O.MEM_STATUS[int(s)] for s in st] == want, name
+        ocomp, _ = O.memtable_verify_batch(base, len(base), offs, pb)
+        assert (host(comp).view(np.uint64) == ocomp).all(), name
+        assert int(host(bad)[0]) == int((st != 0).sum()), name
+        if name.endswith("_corrupt") or name == "crafted":
+            continue
+        z = base.copy()
+        for o in offs:
+            c = kvsites.mem_checksum_pos(base, int(o))
+            z[c:c + pb] = 0
+        g = d(z)
+        out, pst = engine.memtable_protect_batch(g, d(offs.view(np.int64)), pb)
+        assert (host(pst) == 0).all() and (host(out).view(np.uint64) == ocomp).all(), name
+        assert (host(g) == base).all(), name  # UpdateEntryChecksum wrote the reference's bytes
+
+
+def _varint_bytes(v):
+    """varint32 encodings of v (< 2^21) as (bytes u8[n, 3], lengths)"""
+    v = v.astype(np.uint64)
+    n = 1 + (v >= 128).astype(np.int64) + (v >= 1 << 14).astype(np.int64)
+    b = np.zeros((len(v), 3), np.uint8)
+    b[:, 0] = (v & 127) | np.where(n > 1, 128, 0)
+    b[:, 1] = ((v >> 7) & 127) | np.where(n > 2, 128, 0)
+    b[:, 2] = (v >> 14) & 127
+    return b, n
+
+
+def make_memtable(n, prot_bytes, seed):
+    """n MemTable::Add-layout entries (memtable.cc:696-732) back to back:
+    varint32(klen + 8) | user key | LE64(seq << 8 | type) | varint32(vlen) |
+    value | prot_bytes checksum (zero: written by the protect call)"""
+    rng = np.random.default_rng(seed)
+    kl = rng.integers(16, 65, n)
+    vl = rng.integers(0, 1001, n)
+    kl[:8] = [0, 1, 119, 120, 200, 241, 1500, 16383 - 8]
+    vl[:8] = [0, 127, 128, 240, 241, 1024, 5000, 16384]
+    kb, kn = _varint_bytes(kl + 8)
+    vb, vn = _varint_bytes(vl)
+    size = kn + kl + 8 + vn + vl + prot_bytes
+    offs = np.zeros(n, np.int64)
+    offs[1:] = np.cumsum(size[:-1])
+    total = int(offs[-1] + size[-1])
+    base = rng.integers(0, 256, (total + 255) // 256 * 256, dtype=np.uint8)
+    types = rng.choice(np.array([0, 1, 2, 7, 17], np.uint64), n)
+    seqs = rng.integers(1, 2**56, n, dtype=np.uint64)
+    tag = (seqs << np.uint64(8)) | types
+    for j in range(3):  # klen varint
+        m = kn > j
+        base[offs[m] + j] = kb[m, j]
+    kp = offs + kn
+    tp = kp + kl
+    tb = tag.view(np.uint8).reshape(n, 8)
+    for j in range(8):
+        base[tp + j] = tb[:, j]
+    for j in range(3):
+        m = vn > j
+        base[tp[m] + 8 + j] = vb[m, j]
+    cp = tp + 8 + vn + vl
+    for j in range(prot_bytes):
+        base[cp + j] = 0
+    return base, offs, cp
+
+
+@pytest.mark.parametrize("prot_bytes", [8, 1])
+def test_memtable_full_size(prot_bytes):
+    """1 M entries (the a15 bench shape: 16-64 B keys, 0-1000 B values, plus
+    every varint width): protect in place, every checksum byte and value
+    against the oracle, verify clean, then 60 flips found exactly"""
+    n = 1 << 20
+    base, offs, cp = make_memtable(n, prot_bytes, 0xA15F + prot_bytes)
+    g = d(base)
+    go = d(offs)
+    out, st = engine.memtable_protect_batch(g, go, prot_bytes)
+    assert (host(st) == 0).all()
+    hb = host(g)
+    ocomp, ost = O.memtable_verify_batch(hb, len(hb), offs.view(np.uint64), prot_bytes)
+    assert (ost == 0).all(), "the protect call wrote checksums the oracle rejects"
+    assert (host(out).view(np.uint64) == ocomp).all()
+    comp, st, bad = engine.memtable_verify_batch(g, go, prot_bytes)
+    assert int(host(bad)[0]) == 0 and (host(st) == 0).all()
+    rng = np.random.default_rng(5)
+    victims = np.sort(rng.choice(np.arange(8, n), 60, replace=False))
+    kp = offs[victims] + 1  # key bytes (these entries' klen varints are 1 byte)
+    g[d(kp)] ^= 0x10
+    comp, st, bad = engine.memtable_verify_batch(g, go, prot_bytes)
+    failed = np.nonzero(host(st))[0]
+    assert set(failed.tolist()) <= set(victims.tolist())
+    assert (host(st)[failed] == 4).all() and int(host(bad)[0]) == len(failed)
+    if prot_bytes == 8:
+        assert len(failed) == 60
+
+
+def test_memtable_out_of_range():
+    base = np.zeros(64, np.uint8)
+    base[60] = 0x20  # klen 32: runs past the buffer
+    base[0] = 0x0b  # klen 11, tag, vlen 0 ... checksum past the end at offset 52
+    offs = np.array([60, 0, 70, 52], np.int64)
+    comp, st, bad = engine.memtable_verify_batch(d(base), d(offs), 8)
+    assert host(st).tolist()[0] == 5 and host(st).tolist()[2] == 5
+    assert int(host(bad)[0]) == 4
+
+
+def test_write_batch_fixtures(kv_sites):
+    base, offs, lens, reps = kvsites.write_batch_case(*kv_sites)
+    prot, first, st, nprot = engine.write_batch_protect_batch(
+        d(base), d(offs.view(np.int64)), d(lens.view(np.int32)))
+    prot, first, st, nprot = host(prot).view(np.uint64), host(first), host(st), host(nprot)
+    for j, (name, status, want) in enumerate(reps):
+        assert O.WB_STATUS[int(st[j])] == status, name
+        got = prot[first[j]:first[j] + nprot[j]]
+        assert got.tolist() == [int(x) for x in want][:len(got)], name
+        if status == "OK":
+            assert len(got) == len(want) == first[j + 1] - first[j], name
+
+
+def _wb_rep(rng, nrec):
+    """a WriteBatch rep (write_batch.cc record layout) of nrec random records"""
+    out = bytearray(struct.pack("<QI", int(rng.integers(0, 2**56)), 0))
+    cnt = 0
+    for _ in range(nrec):
+        tag = int(rng.choice([0x01, 0x05, 0x00, 0x04, 0x07, 0x08, 0x02, 0x06, 0x0F, 0x0E, 0x11,
+                              0x10, 0x16, 0x17, 0x03, 0x0D]))
+        out.append(tag)
+        if tag in (0x05, 0x04, 0x08, 0x06, 0x0E, 0x10, 0x17):
+            cf = int(rng.integers(1, 300))
+            while cf >= 128:
+                out.append((cf & 127) | 128)
+                cf >>= 7
+            out.append(cf)
+        parts = {0x03: 1, 0x0D: 0, 0x00: 1, 0x04: 1, 0x07: 1, 0x08: 1}.get(tag, 2)
+        for p in range(parts):
+            ln = int(rng.integers(0, 300 if p == 0 else 1500))
+            v = ln
+            while v >= 128:
+                out.append((v & 127) | 128)
+                v >>= 7
+            out.append(v)
+            out += rng.integers(0, 256, ln, dtype=np.uint8).tobytes()
+        cnt += tag not in (0x03, 0x0D)
+    out[8:12] = struct.pack("<I", cnt)
+    return bytes(out)
+
+
+def test_write_batch_many_reps():
+    """5000 reps of 0-40 records (recovery-shaped): every protection value and
+    status against the oracle's restatement"""
+    rng = np.random.default_rng(77)
+    reps = [_wb_rep(rng, int(rng.integers(0, 41))) for _ in range(5000)]
+    reps[7] = reps[7][:-1]  # truncated
+    offs = np.cumsum([0] + [len(r) + int(rng.integers(0, 4)) for r in reps[:-1]]).astype(np.int64)
+    base = np.zeros(int(offs[-1]) + len(reps[-1]) + 64, np.uint8)
+    for o, r in zip(offs, reps):
+        base[o:o + len(r)] = np.frombuffer(r, np.uint8)
+    lens = np.array([len(r) for r in reps], np.int32)
+    prot, first, st, nprot = engine.write_batch_protect_batch(d(base), d(offs), d(lens))
+    prot, first, st, nprot = host(prot).view(np.uint64), host(first), host(st), host(nprot)
+    for j, r in enumerate(reps):
+        code, want = O.write_batch_protect(r)
+        assert int(st[j]) == code, j
+        assert prot[first[j]:first[j] + nprot[j]].tolist() == want[:nprot[j]], j
+    assert int(st[7]) != 0

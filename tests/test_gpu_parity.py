@@ -523,44 +523,56 @@ def test_kv_out_of_range_and_bad_args():
         engine.kv_verify_batch(base, o, s, o, s, 3, c)
 
 
-def test_kv_full_size_roundtrip():
-    """1 M memtable-shaped entries (16-64 B keys, 0-1000 B values, 8-byte
-    protection): write side computes, read side verifies, a 2000-entry sample
-    against the oracle, 50 injected flips detected exactly."""
+@pytest.mark.parametrize("prot_bytes,flags", [(8, (True, True, False)), (1, (False, False, False)),
+                                              (4, (True, True, True)), (2, (True, False, True))])
+def test_kv_full_size_roundtrip(prot_bytes, flags):
+    """1 M memtable-shaped entries (16-64 B keys, 0-1000 B values, the bench's
+    a15 batch), at the four (protection_bytes, op/seq/cf) shapes the reference
+    uses: write side computes, EVERY entry's protection is compared with the
+    oracle, the read side verifies, 50 injected flips are detected exactly."""
+    with_ops, with_seq, with_cf = flags
     n = 1 << 20
     rng = np.random.default_rng(99)
     ks = rng.integers(16, 65, n).astype(np.int64)
     vs = rng.integers(0, 1001, n).astype(np.int64)
     ko = np.zeros(n, np.int64)
-    ko[1:] = np.cumsum(ks[:-1] + vs[:-1] + 8)
+    ko[1:] = np.cumsum(ks[:-1] + vs[:-1] + prot_bytes)
     vo = ko + ks
     co = vo + vs
-    total = int(co[-1]) + 8
+    total = int(co[-1]) + prot_bytes
     alloc = (total + 255) // 256 * 256
     base = torch.empty(alloc, dtype=torch.uint8, device=DEV)
-    engine.fill_stream(base, 0, 0xF0E57000A15)
+    engine.fill_stream(base, 0, 0xF0E57000A15 + prot_bytes)
     dko, dks, dvo, dvs = d(ko), d(ks.astype(np.int32)), d(vo), d(vs.astype(np.int32))
-    ops = d(rng.integers(0, 26, n).astype(np.uint8))
-    seqs = d(rng.integers(0, 2**62, n).astype(np.int64))
-    prot = engine.kv_protect_batch(base, dko, dks, dvo, dvs, ops, seqs)
-    # Encode(8): LE bytes at co
-    pb = prot.view(torch.uint8).view(n, 8)
-    idx = d(co)[:, None] + torch.arange(8, device=DEV)[None, :]
-    base[idx.reshape(-1)] = pb.reshape(-1)
-    comp, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, 8, d(co), ops, seqs)
-    assert int(host(bad)[0]) == 0
+    hops = rng.integers(0, 26, n).astype(np.uint8) if with_ops else None
+    hseq = rng.integers(0, 2**62, n).astype(np.uint64) if with_seq else None
+    hcf = rng.integers(0, 2**32, n, dtype=np.uint64).astype(np.uint32) if with_cf else None
+    ops = None if hops is None else d(hops)
+    seqs = None if hseq is None else d(hseq.view(np.int64))
+    cfs = None if hcf is None else d(hcf.view(np.int32))
+    prot = engine.kv_protect_batch(base, dko, dks, dvo, dvs, ops, seqs, cfs)
     hb = host(base)
-    hp = host(prot).view(np.uint64)
-    hops, hseq = host(ops), host(seqs).view(np.uint64)
-    for i in rng.choice(n, 2000, replace=False):
-        want = O.kv_protect(hb[ko[i]:ko[i] + ks[i]], hb[vo[i]:vo[i] + vs[i]], int(hops[i]),
-                            seq=int(hseq[i]))
-        assert int(hp[i]) == want
+    want = O.kv_protect_batch(hb, ko.view(np.uint64), ks, vo.view(np.uint64), vs, hops, hseq, hcf)
+    got = host(prot).view(np.uint64)
+    bad_i = np.nonzero(got != want)[0]
+    assert len(bad_i) == 0, f"{len(bad_i)} of {n} entries differ, first {bad_i[:8].tolist()}"
+    # Encode(prot_bytes): the low LE bytes at co
+    pb = prot.view(torch.uint8).view(n, 8)[:, :prot_bytes]
+    idx = d(co)[:, None] + torch.arange(prot_bytes, device=DEV)[None, :]
+    base[idx.reshape(-1)] = pb.reshape(-1)
+    comp, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, prot_bytes, d(co), ops, seqs,
+                                           cfs)
+    assert int(host(bad)[0]) == 0
+    assert (host(comp).view(np.uint64) == want).all()
     victims = rng.choice(n, 50, replace=False)
     base[d(ko[victims] + 3)] ^= 0x20
-    _, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, 8, d(co), ops, seqs)
-    assert int(host(bad)[0]) == 50
-    assert set(np.nonzero(host(ok) == 0)[0].tolist()) == set(victims.tolist())
+    _, ok, bad = engine.kv_verify_batch(base, dko, dks, dvo, dvs, prot_bytes, d(co), ops, seqs, cfs)
+    # a 1-byte truncation lets a flip pass with probability 1/256 (kv_checksum.h:117-133);
+    # every detected entry must be a victim, and with 8 bytes all must be
+    failed = set(np.nonzero(host(ok) == 0)[0].tolist())
+    assert failed <= set(victims.tolist()) and int(host(bad)[0]) == len(failed)
+    if prot_bytes >= 4:
+        assert failed == set(victims.tolist())
 
 
 # ---- C5: WAL images built on the device -----------------------------------

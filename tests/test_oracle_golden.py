@@ -218,3 +218,32 @@ def test_kv_protect_composition(ref_vectors):
         assert O.kv_protect(key, val, op) == hk ^ r["hash64_s1"] ^ hop
         assert O.kv_protect(key, val, op, seq=seq) == hk ^ r["hash64_s1"] ^ hop ^ hseq
         assert O.kv_protect(key, val, op, seq=seq, cf=cf) == hk ^ r["hash64_s1"] ^ hop ^ hseq ^ hcf
+
+
+# ---- a15 call sites: the oracle against the reference's own call-site code --
+def test_oracle_memtable_entries_vs_reference(kv_sites):
+    """MemTable::Add entries and MemTable::VerifyEntryChecksum statuses
+    (db/memtable.cc:273-307, :696-732) on intact, corrupted and crafted entries"""
+    import kvsites
+
+    meta, arrays = kv_sites
+    cases = kvsites.memtable_cases(meta, arrays)
+    assert len(cases) == 9
+    for name, base, offs, pb, want in cases:
+        comp, st = O.memtable_verify_batch(base, len(base), offs, pb)
+        got = [O.MEM_STATUS[int(s)] for s in st]
+        assert got == want, name
+        assert (comp[st == 0] != 0).all()
+
+
+def test_oracle_write_batch_vs_reference(kv_sites):
+    """WriteBatch::Iterate statuses and ProtectionInfoUpdater values
+    (db/write_batch.cc:361-716, :3016-3080) on every fixture rep"""
+    import kvsites
+
+    base, offs, lens, reps = kvsites.write_batch_case(*kv_sites)
+    assert len(reps) > 280
+    for (name, status, prot), o, n in zip(reps, offs, lens):
+        code, got = O.write_batch_protect(base[int(o):int(o) + int(n)].tobytes())
+        assert O.WB_STATUS[code] == status, name
+        assert [int(x) for x in prot] == got, name

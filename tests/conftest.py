@@ -11,6 +11,14 @@ if GOLDEN not in sys.path:
     sys.path.insert(0, GOLDEN)
 
 
+# Test infrastructure only: the sanitizer run (tools/asan_cpu.sh) points the
+# tests at lib/libforst_checksum_asan.so; the product reads no such variable.
+if os.environ.get("FORST_TEST_LIB"):
+    from forst_amd import _lib as _forst_lib
+
+    _forst_lib.use_library(os.environ["FORST_TEST_LIB"])
+
+
 def pytest_configure(config):
     config.addinivalue_line("markers", "gpu: needs a real MI355X (runs through the HIP C-ABI)")
     config.addinivalue_line("markers", "slow: long-running CPU test")

@@ -53,7 +53,7 @@ def test_memtable_fixtures(kv_sites):
 
 def _varint_bytes(v):
     """varint32 encodings of v (< 2^21) as (bytes u8[n, 3], lengths)"""
-    v = v.astype(np.uint64)
+    v = v.astype(np.int64)
     n = 1 + (v >= 128).astype(np.int64) + (v >= 1 << 14).astype(np.int64)
     b = np.zeros((len(v), 3), np.uint8)
     b[:, 0] = (v & 127) | np.where(n > 1, 128, 0)
@@ -196,3 +196,53 @@ def test_write_batch_many_reps():
         assert int(st[j]) == code, j
         assert prot[first[j]:first[j] + nprot[j]].tolist() == want[:nprot[j]], j
     assert int(st[7]) != 0
+
+
+def test_block_kv_checksums_fixtures(kv_sites):
+    """Block::Initialize{Data,Index,MetaIndex}BlockProtectionInfo's kv_checksum_
+    (block.cc:1113-1235) for the blocks of reference-written SSTs and damaged
+    blocks, protection bytes 8 and 2"""
+    base, offs, sizes, kinds, cases = kvsites.block_case(*kv_sites)
+    for pb in (8, 2):
+        enc, prot, first, st = engine.block_kv_checksum_batch(
+            d(base), d(offs.view(np.int64)), d(sizes.view(np.int32)), d(kinds), pb)
+        enc, prot, first, st = host(enc), host(prot).view(np.uint64), host(first), host(st)
+        for j, c in enumerate(cases):
+            nk = int(first[j + 1] - first[j])
+            want = c[f"keys_{pb}"]
+            if want < 0:
+                assert st[j] != 0 and nk == 0, c
+                continue
+            assert st[j] == 0 and nk == want, (c["src"], c["kind_name"], nk, want)
+            got = enc[int(first[j]) * pb:int(first[j + 1]) * pb].tobytes().hex()
+            assert got == c[f"kv_checksum_{pb}"], (c["src"], c["kind_name"])
+            low = [int(x) & ((1 << (8 * pb)) - 1) for x in prot[int(first[j]):int(first[j + 1])]]
+            assert low == [int.from_bytes(bytes.fromhex(got)[k * pb:(k + 1) * pb], "little")
+                           for k in range(nk)]
+
+
+def test_block_kv_checksums_many_blocks(kv_sites):
+    """every fixture block repeated 300 times at shifted offsets (35 K blocks,
+    one launch): the same kv_checksum_ bytes each time"""
+    base, offs, sizes, kinds, cases = kvsites.block_case(*kv_sites)
+    good = [j for j, c in enumerate(cases) if c["keys_8"] > 0]
+    blobs = [base[int(offs[j]):int(offs[j]) + int(sizes[j])] for j in good]
+    reps = 300
+    pos, parts = 0, []
+    for r in range(reps):
+        for j, b in zip(good, blobs):
+            pos += 1 + (r + j) % 7
+            parts.append((pos, j))
+            pos += len(b)
+    big = np.zeros(pos + 64, np.uint8)
+    for (o, j), b in zip(parts, blobs * reps):
+        big[o:o + len(b)] = b
+    o2 = np.array([o for o, _ in parts], np.int64)
+    s2 = np.array([int(sizes[j]) for _, j in parts], np.int32)
+    k2 = np.array([int(kinds[j]) for _, j in parts], np.uint8)
+    enc, prot, first, st = engine.block_kv_checksum_batch(d(big), d(o2), d(s2), d(k2), 8)
+    enc, first, st = host(enc), host(first), host(st)
+    assert (st == 0).all()
+    for q, (o, j) in enumerate(parts):
+        got = enc[int(first[q]) * 8:int(first[q + 1]) * 8].tobytes().hex()
+        assert got == cases[j]["kv_checksum_8"], (q, j)

@@ -402,6 +402,10 @@ FULL_SIZE = {  # bench.py CONFIGS: (blocks, size spec, checksum type, seed)
     # C3's blocks sorted by size: the byte-balanced workgroup ranges
     "C3S": (1 << 20, ("sorted", (4096, 16384, 65536)), CT.kXXH3, workload.SEEDS["C3"]),
     "C3S_CRC": (1 << 20, ("sorted", (4096, 16384, 65536)), CT.kCRC32c, workload.SEEDS["C3"]),
+    # kxxHash / kxxHash64 at the benched 1 M x 16 KiB: the lane kernel and its
+    # ticket-claimed batch feed (xxhash_legacy.hip), every block vs the oracle
+    "NS16H32": (1 << 20, 16384, CT.kxxHash, workload.SEEDS["C2"]),
+    "NS16H64": (1 << 20, 16384, CT.kxxHash64, workload.SEEDS["C2"]),
 }
 
 

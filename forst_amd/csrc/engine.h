@@ -273,9 +273,10 @@ hipError_t launch_xxh3_frag(const BlockArgs& a, hipStream_t stream, const char**
 // same loads (wal_recover.hip): long records (> 240 B) only
 hipError_t launch_xxh3_frag_crc(const BlockArgs& a, hipStream_t stream, const char** kernel_name);
 // WAL recovery's short candidates (one fragment, <= 240 B) off the fused
-// kernel: their CRC on the raw path's lane kernel, their XXH3 one per lane
-// (launch_xxh3_short_sel), both ahead of the fused kernel, which is then
-// built for records > 240 B only (1); or in the fused kernel's rows (0)
+// kernel: their CRC and XXH3 in one pass, a record per 16-lane row
+// (launch_wal_short_rows; FORST_REC_SHORT_ROWS=0: launch_crc32c_raw_lanes +
+// launch_xxh3_short_rows), ahead of the fused kernel, which is then built
+// for records > 240 B only (1); or in the fused kernel's rows (0)
 #ifndef FORST_REC_SHORT
 #define FORST_REC_SHORT 1
 #endif

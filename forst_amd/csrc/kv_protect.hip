@@ -46,12 +46,6 @@ namespace {
 constexpr uint32_t kWaves = 4;
 constexpr uint32_t kThreads = kWaves * 64;
 constexpr uint32_t kSecWords = 26;  // kSecret as 24 LE u64 words + 2 zero words
-#ifndef FORST_KV_WAVES
-#define FORST_KV_WAVES 4  // resident waves per SIMD the register budget is cut for
-#endif
-#ifndef FORST_KV_PREFETCH
-#define FORST_KV_PREFETCH 1  // (build knob for the A/B: 0 = no next-round prefetch)
-#endif
 
 // db/kv_checksum.h:84-88
 constexpr uint64_t kSeedK = 0;
@@ -211,17 +205,22 @@ __device__ uint64_t row_long(const uint64_t* S, const uint8_t* p, uint32_t len, 
   uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;  // INIT_ACC
   uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
   const uint32_t nb = act ? len >> 10 : 0;
+  // the chunk secrets: stripe st's at 8 st + 16 pp (aligned words)
+  uint64_t k0[4], k1[4];
+#pragma unroll
+  for (uint32_t k = 0; k < 4; ++k) {
+    const uint32_t off = 8 * ((t >> 2) + 4 * k) + 16 * pp;
+    k0[k] = psec(S, off, seed);
+    k1[k] = psec(S, off + 8, seed);
+  }
   const uint64_t ks0 = psec(S, 128 + 16 * pp, seed), ks1 = psec(S, 136 + 16 * pp, seed);
   for (uint32_t g = 0;; ++g) {
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
     for (uint32_t k = 0; k < 4; ++k)
       if (b.mask & (1u << k)) {  // acc_64bits: acc[i] += data + lo*hi(data ^ key)
-        // stripe st's secret at 8 st + 16 pp (aligned words), read from LDS
-        // where used rather than held across the loop (registers = loads in flight)
-        const uint32_t off = fresh(8 * ((t >> 2) + 4 * k) + 16 * pp);
-        c0 += b.d0[k] + mul32to64(b.d0[k] ^ psec(S, off, seed));
-        c1 += b.d1[k] + mul32to64(b.d1[k] ^ psec(S, off + 8, seed));
+        c0 += b.d0[k] + mul32to64(b.d0[k] ^ k0[k]);
+        c1 += b.d1[k] + mul32to64(b.d1[k] ^ k1[k]);
       }
     c0 += row_ror64<4>(c0);
     c1 += row_ror64<4>(c1);
@@ -245,20 +244,6 @@ __device__ uint64_t row_long(const uint64_t* S, const uint8_t* p, uint32_t len, 
   h += quad_xor64<1>(h);
   h += quad_xor64<2>(h);
   return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + h);
-}
-
-// Pull the 64-byte line at p toward the CU one round ahead: a dword loaded
-// straight into an LDS scratch word (global_load_lds_dword), so the prefetch
-// holds no register; the next round's loads then meet lines already on the way.
-__device__ __forceinline__ void prefetch_line(const uint8_t* p, uint32_t* lds_junk) {
-#ifndef FORST_HOST_EMULATION
-  __builtin_amdgcn_global_load_lds(
-      (const __attribute__((address_space(1))) void*)(reinterpret_cast<uint64_t>(p) & ~3ull),
-      (__attribute__((address_space(3))) void*)lds_junk, 4, 0, 0);
-#else
-  (void)p;
-  (void)lds_junk;
-#endif
 }
 
 __device__ __forceinline__ bool in_range(uint64_t off, uint64_t len, uint64_t base_len) {
@@ -355,11 +340,9 @@ __device__ __forceinline__ uint32_t field_class(bool valid, uint32_t len) {
 
 // MODE: kKvHash (Hash64 per buffer), kKvProtect, kKvVerify
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES) kv_kernel(KvArgs a) {
+__global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
   __shared__ uint64_t s_sec[kSecWords];
   __shared__ uint64_t s_slot[kWaves][64];
-  __shared__ uint64_t s_slot2[kWaves][64];  // verify: the stored checksum bytes
-  __shared__ uint32_t s_junk[kWaves][64];   // prefetch_line's destination
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15;
@@ -369,91 +352,65 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES) k
   // this lane's mix16B secret pair (seed applied per field)
   const uint64_t SA = psec(S, term_secret(t), 0), SB = psec(S, term_secret(t) + 8, 0);
   uint64_t* slot = s_slot[wave];
-  uint64_t* slot2 = s_slot2[wave];
-  uint32_t* junk = s_junk[wave];
-
-  // a tile's descriptors live in LDS, not registers: the rounds read their
-  // entry's with row-uniform ds_reads, and every register is left for loads
-  // in flight
-  __shared__ uint64_t s_ko[kWaves][64], s_vo[kWaves][64], s_co[kWaves][64];
-  __shared__ uint32_t s_kl[kWaves][64], s_vl[kWaves][64];
-  __shared__ uint64_t s_ks[MODE == kKvHash ? kWaves : 1][64];
-  uint64_t* dko = s_ko[wave];
-  uint64_t* dvo = s_vo[wave];
-  uint64_t* dco = s_co[wave];
-  uint32_t* dkl = s_kl[wave];
-  uint32_t* dvl = s_vl[wave];
-  uint64_t* dks = s_ks[MODE == kKvHash ? wave : 0];
 
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves * 64;
   for (uint64_t b0 = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * 64; b0 < a.n;
        b0 += stride) {
-    uint64_t vmask;
-    uint32_t mst = kMemOk;
-    {  // ---- lane = entry: descriptors and the op / seq / cf hashes
-      const uint64_t i = b0 + lane;
-      const bool act = i < a.n;
-      uint64_t ko = 0, vo = 0, co = 0, kseed = kSeedK, hs = 0;
-      uint32_t kl = 0, vl = 0;
-      bool valid = false;
-      if (MODE == kKvMemVerify || MODE == kKvMemProtect) {
-        if (act) {
-          uint64_t tag = 0;
-          mst = decode_mem_entry(a, a.key_off[i], ko, kl, vo, vl, co, tag);
-          valid = mst == kMemOk;
-          // ProtectKVO(user_key, value, type).ProtectS(seq) (memtable.cc:298-302)
-          const uint32_t op = static_cast<uint32_t>(tag & 0xff);
-          hs = xxph3_1to3(op, op, op, 1, kSeedO) ^ xxph3_4to8(tag >> 8, 8, kSeedS);
+    // ---- lane = entry: descriptors and the op / seq / cf hashes
+    const uint64_t i = b0 + lane;
+    const bool act = i < a.n;
+    uint64_t ko = 0, vo = 0, co = 0, kseed = kSeedK, hs = 0;
+    uint32_t kl = 0, vl = 0, mst = kMemOk;
+    bool valid = false;
+    if (MODE == kKvMemVerify || MODE == kKvMemProtect) {
+      if (act) {
+        uint64_t tag = 0;
+        mst = decode_mem_entry(a, a.key_off[i], ko, kl, vo, vl, co, tag);
+        valid = mst == kMemOk;
+        // ProtectKVO(user_key, value, type).ProtectS(seq) (memtable.cc:298-302)
+        const uint32_t op = static_cast<uint32_t>(tag & 0xff);
+        hs = xxph3_1to3(op, op, op, 1, kSeedO) ^ xxph3_4to8(tag >> 8, 8, kSeedS);
+      }
+    } else if (act) {
+      ko = a.key_off[i];
+      kl = a.key_len[i];
+      valid = in_range(ko, kl, a.key_base ? a.key_base_len : a.base_len);
+      if (MODE == kKvHash) {
+        kseed = a.seeds ? a.seeds[i] : a.seed;
+      } else {
+        vo = a.val_off[i];
+        vl = a.val_len[i];
+        valid = valid && in_range(vo, vl, a.base_len);
+        if (a.ops) {  // NPHash64(&op_type, 1, kSeedO)
+          const uint32_t op = a.ops[i];
+          hs ^= xxph3_1to3(op, op, op, 1, kSeedO);
         }
-      } else if (act) {
-        ko = a.key_off[i];
-        kl = a.key_len[i];
-        valid = in_range(ko, kl, a.key_base ? a.key_base_len : a.base_len);
-        if (MODE == kKvHash) {
-          kseed = a.seeds ? a.seeds[i] : a.seed;
-        } else {
-          vo = a.val_off[i];
-          vl = a.val_len[i];
-          valid = valid && in_range(vo, vl, a.base_len);
-          if (a.ops) {  // NPHash64(&op_type, 1, kSeedO)
-            const uint32_t op = a.ops[i];
-            hs ^= xxph3_1to3(op, op, op, 1, kSeedO);
-          }
-          if (a.seqs) hs ^= xxph3_4to8(a.seqs[i], 8, kSeedS);  // native LE bytes
-          if (a.cfs) {
-            const uint64_t cf = a.cfs[i];
-            hs ^= xxph3_4to8(cf | (cf << 32), 4, kSeedC);
-          }
-        }
-        if (MODE == kKvVerify) {
-          co = a.chk_off[i];
-          valid = valid && in_range(co, a.prot_bytes, a.base_len);
+        if (a.seqs) hs ^= xxph3_4to8(a.seqs[i], 8, kSeedS);  // native LE bytes
+        if (a.cfs) {
+          const uint64_t cf = a.cfs[i];
+          hs ^= xxph3_4to8(cf | (cf << 32), 4, kSeedC);
         }
       }
-      vmask = __ballot(valid);
-      dko[lane] = ko;
-      dkl[lane] = kl;
-      dvo[lane] = vo;
-      dvl[lane] = vl;
-      dco[lane] = co;
-      if (MODE == kKvHash) dks[lane] = kseed;
-      slot[lane] = hs;  // the rows XOR their key / value hashes in
-      wave_lds_sync();
+      if (MODE == kKvVerify) {
+        co = a.chk_off[i];
+        valid = valid && in_range(co, a.prot_bytes, a.base_len);
+      }
     }
+    const uint64_t vmask = __ballot(valid);
 
     // ---- 16 rounds: row R hashes the key and value of entry 16R + r
     for (uint32_t r = 0; r < 16; ++r) {
       const uint32_t src = (lane & 48) | r;
       if (!(vmask & (0x0001000100010001ull << r))) continue;  // (wave-uniform)
       const bool rv = (vmask >> src) & 1;
-      const uint64_t rko = dko[src];
-      const uint32_t rkl = dkl[src];
-      const uint64_t rks = MODE == kKvHash ? dks[src] : kSeedK;
+      const uint64_t rko = shfl64(ko, src);
+      const uint32_t rkl = __shfl(kl, src);
+      const uint64_t rks = MODE == kKvHash ? shfl64(kseed, src) : kSeedK;
       uint64_t rvo = 0;
       uint32_t rvl = 0;
       if (MODE != kKvHash) {
-        rvo = dvo[src];
-        rvl = dvl[src];
+        rvo = shfl64(vo, src);
+        rvl = __shfl(vl, src);
       }
       const uint32_t kc = field_class(rv, rkl);
       const uint32_t vc = MODE == kKvHash ? kNone : field_class(rv, rvl);
@@ -483,39 +440,6 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES) k
       uint64_t vl0, vl1;
       long_block_load(vp, rvl, 0, t, vc == kLong, vb);
       long_last_load(vp, rvl, t, vc == kLong, vl0, vl1);
-      uint64_t sw = 0;  // verify: lane 5 reads the stored checksum's bytes
-      if (MODE == kKvVerify || MODE == kKvMemVerify) {
-        const uint64_t rco = dco[src];
-        if (rv && t == 5) {
-          const uint8_t* c = a.base + rco;
-          if (a.prot_bytes == 8) {
-            sw = ldu64(c);
-          } else if (a.prot_bytes == 4) {
-            sw = ldu32(c);
-          } else {
-            for (uint32_t b = 0; b < a.prot_bytes; ++b)
-              sw |= static_cast<uint64_t>(ldu8(c + b)) << (8 * b);
-          }
-        }
-      }
-      if (FORST_KV_PREFETCH && r + 1 < 16 && (vmask & (0x0001000100010001ull << (r + 1)))) {
-        // the next round's entry: lanes 0-14 its value's first 15 lines, lane 15
-        // its key's first line
-        const uint32_t ns = src + 1;
-        const bool nv = (vmask >> ns) & 1;
-        const uint64_t nko = dko[ns];
-        uint64_t nvo = 0;
-        uint32_t nvl = 0;
-        if (MODE != kKvHash) {
-          nvo = dvo[ns];
-          nvl = dvl[ns];
-        }
-        const uint64_t nline = (nvo & ~63ull) + 64 * t;
-        const bool pv = MODE != kKvHash && t < 15 && nvl && nline < nvo + nvl;
-        if (nv && (pv || t == 15))
-          prefetch_line(t == 15 ? (a.key_base ? a.key_base : a.base) + nko : a.base + nline,
-                        junk);
-      }
 
       // -- 17..240-byte fields: the row's terms
       uint64_t h = 0;
@@ -550,20 +474,11 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES) k
         const uint64_t hl = row_long(S, kp, rkl, rks, kc == kLong, t, kb, kl0, kl1);
         if (kc == kLong) h ^= hl;
       }
-      if (MODE == kKvVerify || MODE == kKvMemVerify) sw = dpp64<0x122>(sw);  // lane 5 -> 7
-      if (t == 7) {
-        slot[src] ^= h;
-        if (MODE == kKvVerify || MODE == kKvMemVerify) slot2[src] = sw;
-      }
+      if (t == 7) slot[src] = h;
     }
     wave_lds_sync();
-    const uint64_t i = b0 + lane;
-    const bool act = i < a.n;
-    const bool valid = (vmask >> lane) & 1;
-    const uint64_t h = valid ? slot[lane] : 0;
-    const uint64_t stored = valid && (MODE == kKvVerify || MODE == kKvMemVerify) ? slot2[lane] : 0;
-    const uint64_t co = dco[lane];
-    wave_lds_sync();  // (the next tile overwrites the slots and descriptors)
+    uint64_t h = valid ? hs ^ slot[lane] : 0;
+    wave_lds_sync();  // (the next tile's rounds overwrite the slots)
 
     if (MODE == kKvMemProtect) {
       // MemTable::UpdateEntryChecksum (memtable.cc:676-693): Encode(prot_bytes)
@@ -575,6 +490,18 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES) k
       if (act && a.status) a.status[i] = static_cast<uint8_t>(mst);
     } else if (MODE == kKvVerify || MODE == kKvMemVerify) {
       // ProtectionInfo<T>::Verify (kv_checksum.h:117-133): low prot_bytes bytes, LE
+      uint64_t stored = 0;
+      if (valid) {
+        const uint8_t* c = a.base + co;
+        if (a.prot_bytes == 8) {
+          stored = ldu64(c);
+        } else if (a.prot_bytes == 4) {
+          stored = ldu32(c);
+        } else {
+          for (uint32_t b = 0; b < a.prot_bytes; ++b)
+            stored |= static_cast<uint64_t>(ldu8(c + b)) << (8 * b);
+        }
+      }
       const uint64_t mask = a.prot_bytes >= 8 ? ~0ull : ((1ull << (8 * a.prot_bytes)) - 1);
       const bool ok = valid && ((stored ^ h) & mask) == 0;
       if (act && a.out) a.out[i] = h;
@@ -599,10 +526,10 @@ hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char**
   const DeviceInfo& di = device_info();
   if (a.n == 0) return hipSuccess;
   const uint64_t per_wg = uint64_t(kWaves) * 64;
-  static const uint32_t wg_per_cu = [] {
-    const char* e = std::getenv("FORST_KV_WG_PER_CU");
-    return e ? static_cast<uint32_t>(std::max(1, atoi(e))) : 8u;
-  }();
+#ifndef FORST_KV_WG_PER_CU
+#define FORST_KV_WG_PER_CU 8  // (build knob for the A/B: workgroups per CU in the grid)
+#endif
+  const uint32_t wg_per_cu = FORST_KV_WG_PER_CU;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
       1, std::min<uint64_t>((a.n + per_wg - 1) / per_wg, uint64_t(di.num_cus) * wg_per_cu)));
   switch (mode) {

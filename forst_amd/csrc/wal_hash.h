@@ -215,7 +215,13 @@ hipError_t hash_logical_records(const uint8_t* log, uint64_t log_len, const F& f
                                 uint64_t* out, hipStream_t st, const char** name,
                                 bool overlap = true) {
   if (n == 0) return hipSuccess;
+  // (FORST_WH_UNPACKED: the emulator test build forces the unpacked form, so
+  // the branch beyond 2^24 records / 2^40 bytes runs under test too)
+#ifdef FORST_WH_UNPACKED
+  const bool packed = false;
+#else
   const bool packed = n < (uint64_t(1) << 24) && log_len < (uint64_t(1) << kWhPackShift);
+#endif
   const uint64_t nt = n / kScanTile + 2;
   const size_t s8 = wh_up256(8 * n), s4 = wh_up256(4 * n), st8 = wh_up256(8 * nt);
   void* scratch = nullptr;

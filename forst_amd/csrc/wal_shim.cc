@@ -278,3 +278,204 @@ Status WalWriteGroup::Frame(const std::vector<ByteRange>& records, uint32_t bloc
 }
 
 }  // namespace forst_gpu
+
+// ---- per-KV protection at its call sites (a15) ------------------------------
+namespace forst_gpu {
+
+KvProtection::~KvProtection() { (void)hipFree(dev_); }
+
+uint8_t* KvProtection::Grow(uint64_t bytes) {
+  if (bytes > cap_) {
+    (void)hipFree(dev_);
+    dev_ = nullptr;
+    cap_ = 0;
+    grow_status_ = FromHip(hipMalloc(&dev_, bytes), "hipMalloc");
+    if (!grow_status_.ok()) return nullptr;
+    cap_ = bytes;
+  }
+  grow_status_ = Status::OK();
+  return static_cast<uint8_t*>(dev_);
+}
+
+Status KvProtection::VerifyMemtableEntries(const char* arena, uint64_t arena_len,
+                                           const std::vector<uint64_t>& entry_offsets,
+                                           uint32_t protection_bytes,
+                                           std::vector<uint8_t>* status) {
+  const uint64_t n = entry_offsets.size();
+  status->assign(n, 0);
+  if (!n) return Status::OK();
+  const uint64_t a8 = align8(arena_len);
+  uint8_t* d = Grow(a8 + 9 * n);
+  if (!d) return grow_status_;
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(d + a8);
+  uint8_t* d_st = d + a8 + 8 * n;
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  Status s = FromHip(hipMemcpyAsync(d, arena, arena_len, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  if (s.ok())
+    s = FromHip(hipMemcpyAsync(d_off, entry_offsets.data(), 8 * n, hipMemcpyHostToDevice, st),
+                "hipMemcpyAsync");
+  if (s.ok())
+    s = FromRc(forst_memtable_verify_batch(d, arena_len, d_off, n, protection_bytes, nullptr, d_st,
+                                           nullptr, stream_));
+  if (s.ok())
+    s = FromHip(hipMemcpyAsync(status->data(), d_st, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  return s;
+}
+
+// the parts back to back (8-byte aligned) in the device buffer: offs[i]
+Status KvProtection::Stage(const std::vector<KvBytes>& parts, std::vector<uint64_t>* offs) {
+  offs->resize(parts.size());
+  uint64_t total = 0;
+  for (size_t i = 0; i < parts.size(); ++i) {
+    (*offs)[i] = total;
+    total = align8(total + parts[i].size);
+  }
+  std::string img(total + 16, '\0');
+  for (size_t i = 0; i < parts.size(); ++i)
+    if (parts[i].size) std::memcpy(&img[(*offs)[i]], parts[i].data, parts[i].size);
+  uint8_t* d = Grow(img.size());
+  if (!d) return grow_status_;
+  return FromHip(hipMemcpyAsync(d, img.data(), img.size(), hipMemcpyHostToDevice,
+                                static_cast<hipStream_t>(stream_)),
+                 "hipMemcpyAsync");
+}
+
+Status KvProtection::BlockKvChecksums(const std::vector<KvBytes>& blocks,
+                                      const std::vector<uint8_t>& kinds, uint32_t protection_bytes,
+                                      std::vector<std::string>* kv_checksums,
+                                      std::vector<uint8_t>* status) {
+  const uint64_t n = blocks.size();
+  kv_checksums->assign(n, std::string());
+  status->assign(n, 0);
+  if (!n) return Status::OK();
+  if (kinds.size() != n) return Status::InvalidArgument("one kind per block");
+  std::vector<uint64_t> offs;
+  Status s = Stage(blocks, &offs);
+  if (!s.ok()) return s;
+  const uint64_t img = offs.back() + align8(blocks.back().size) + 16;
+  std::vector<uint32_t> sizes(n);
+  for (uint64_t i = 0; i < n; ++i) sizes[i] = static_cast<uint32_t>(blocks[i].size);
+  // device: image | offsets | sizes | kinds | first_key | status, then the checksums
+  void* aux = nullptr;
+  s = FromHip(hipMalloc(&aux, 8 * (2 * n + 1) + 4 * n + 2 * n + 64), "hipMalloc");
+  if (!s.ok()) return s;
+  uint8_t* a = static_cast<uint8_t*>(aux);
+  uint64_t* d_off = reinterpret_cast<uint64_t*>(a);
+  uint64_t* d_first = d_off + n;
+  uint32_t* d_sz = reinterpret_cast<uint32_t*>(d_first + n + 1);
+  uint8_t* d_kind = reinterpret_cast<uint8_t*>(d_sz + n);
+  uint8_t* d_st = d_kind + n;
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  s = FromHip(hipMemcpyAsync(d_off, offs.data(), 8 * n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(d_sz, sizes.data(), 4 * n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(d_kind, kinds.data(), n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  uint64_t total = 0;
+  if (s.ok()) {  // the key total first (capacity 0), then the checksums
+    const int rc = forst_block_kv_checksum_batch(static_cast<uint8_t*>(dev_), img, d_off, d_sz,
+                                                 d_kind, n, protection_bytes, d_first, nullptr,
+                                                 nullptr, 0, d_st, &total, stream_);
+    if (rc != FORST_OK && !(rc == FORST_EINVAL && total > 0)) s = FromRc(rc);
+  }
+  void* d_enc = nullptr;
+  if (s.ok() && total) s = FromHip(hipMalloc(&d_enc, total * protection_bytes), "hipMalloc");
+  if (s.ok() && total)
+    s = FromRc(forst_block_kv_checksum_batch(static_cast<uint8_t*>(dev_), img, d_off, d_sz, d_kind,
+                                             n, protection_bytes, d_first,
+                                             static_cast<uint8_t*>(d_enc), nullptr, total, d_st,
+                                             &total, stream_));
+  std::vector<uint64_t> first(n + 1, 0);
+  std::string enc(total * protection_bytes, '\0');
+  if (s.ok())
+    s = FromHip(hipMemcpyAsync(first.data(), d_first, 8 * (n + 1), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(status->data(), d_st, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok() && total)
+    s = FromHip(hipMemcpyAsync(&enc[0], d_enc, enc.size(), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  (void)hipFree(d_enc);
+  (void)hipFree(aux);
+  if (!s.ok()) return s;
+  for (uint64_t i = 0; i < n; ++i)
+    (*kv_checksums)[i] = enc.substr(first[i] * protection_bytes,
+                                    (first[i + 1] - first[i]) * protection_bytes);
+  return Status::OK();
+}
+
+Status KvProtection::WriteBatchStatus(uint8_t code) {
+  static const char* kText[] = {"",
+                                "malformed WriteBatch (too small)",
+                                "bad WriteBatch Put",
+                                "bad WriteBatch Delete",
+                                "bad WriteBatch DeleteRange",
+                                "bad WriteBatch Merge",
+                                "bad WriteBatch BlobIndex",
+                                "bad WriteBatch Blob",
+                                "bad EndPrepare XID",
+                                "bad commit timestamp",
+                                "bad Commit XID",
+                                "bad Rollback XID",
+                                "bad WriteBatch PutEntity",
+                                "unknown WriteBatch tag",
+                                "WriteBatch has wrong count"};
+  if (code == 0) return Status::OK();
+  if (code < sizeof(kText) / sizeof(kText[0])) return Status::Corruption(kText[code]);
+  return Status::InvalidArgument("WriteBatch rep outside the staged buffer");
+}
+
+Status KvProtection::WriteBatchProtection(const std::vector<KvBytes>& reps,
+                                          std::vector<std::vector<uint64_t>>* prot,
+                                          std::vector<Status>* rep_status) {
+  const uint64_t n = reps.size();
+  prot->assign(n, std::vector<uint64_t>());
+  rep_status->assign(n, Status::OK());
+  if (!n) return Status::OK();
+  std::vector<uint64_t> offs;
+  Status s = Stage(reps, &offs);
+  if (!s.ok()) return s;
+  const uint64_t img = offs.back() + align8(reps.back().size) + 16;
+  std::vector<uint32_t> sizes(n);
+  for (uint64_t i = 0; i < n; ++i) sizes[i] = static_cast<uint32_t>(reps[i].size);
+  void* aux = nullptr;
+  s = FromHip(hipMalloc(&aux, 8 * (2 * n + 1) + 4 * n + 4 * n + n + 64), "hipMalloc");
+  if (!s.ok()) return s;
+  uint64_t* d_off = static_cast<uint64_t*>(aux);
+  uint64_t* d_first = d_off + n;
+  uint32_t* d_sz = reinterpret_cast<uint32_t*>(d_first + n + 1);
+  uint32_t* d_np = d_sz + n;
+  uint8_t* d_st = reinterpret_cast<uint8_t*>(d_np + n);
+  hipStream_t st = static_cast<hipStream_t>(stream_);
+  s = FromHip(hipMemcpyAsync(d_off, offs.data(), 8 * n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(d_sz, sizes.data(), 4 * n, hipMemcpyHostToDevice, st), "hipMemcpyAsync");
+  uint64_t total = 0;
+  if (s.ok()) {
+    const int rc = forst_write_batch_protect_batch(static_cast<uint8_t*>(dev_), img, d_off, d_sz, n,
+                                                   d_first, nullptr, 0, nullptr, nullptr, &total,
+                                                   stream_);
+    if (rc != FORST_OK && !(rc == FORST_EINVAL && total > 0)) s = FromRc(rc);
+  }
+  void* d_prot = nullptr;
+  if (s.ok()) s = FromHip(hipMalloc(&d_prot, 8 * (total ? total : 1)), "hipMalloc");
+  if (s.ok())
+    s = FromRc(forst_write_batch_protect_batch(static_cast<uint8_t*>(dev_), img, d_off, d_sz, n,
+                                               d_first, static_cast<uint64_t*>(d_prot), total,
+                                               d_st, d_np, &total, stream_));
+  std::vector<uint64_t> first(n + 1, 0), all(total ? total : 1);
+  std::vector<uint32_t> np(n);
+  std::vector<uint8_t> code(n);
+  if (s.ok()) s = FromHip(hipMemcpyAsync(first.data(), d_first, 8 * (n + 1), hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(np.data(), d_np, 4 * n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipMemcpyAsync(code.data(), d_st, n, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok() && total)
+    s = FromHip(hipMemcpyAsync(all.data(), d_prot, 8 * total, hipMemcpyDeviceToHost, st), "hipMemcpyAsync");
+  if (s.ok()) s = FromHip(hipStreamSynchronize(st), "hipStreamSynchronize");
+  (void)hipFree(d_prot);
+  (void)hipFree(aux);
+  if (!s.ok()) return s;
+  for (uint64_t i = 0; i < n; ++i) {
+    (*prot)[i].assign(all.begin() + first[i], all.begin() + first[i] + np[i]);
+    (*rep_status)[i] = WriteBatchStatus(code[i]);
+  }
+  return Status::OK();
+}
+
+}  // namespace forst_gpu

@@ -333,4 +333,50 @@ class WalWriteGroup {
   uint64_t dev_cap_ = 0;
 };
 
+
+// Per-KV protection (a15) at the reference's three call sites, over HOST
+// bytes (copied to the device in one piece per call; synchronous):
+//   VerifyMemtableEntries  MemTable::VerifyEntryChecksum (db/memtable.cc:
+//     273-307) for entries at offsets[] of one arena buffer: a status code per
+//     entry (forst_memtable_verify_batch); for a failing entry the caller
+//     returns the reference's own MemTable::VerifyEntryChecksum(entry, ...) --
+//     the exact Status text, allow_data_in_errors included
+//   BlockKvChecksums       Block::Initialize{Data,Index,MetaIndex}Block-
+//     ProtectionInfo (table/block_based/block.cc:1113-1235): each block's
+//     kv_checksum_ bytes (forst_block_kv_checksum_batch)
+//   WriteBatchProtection   WriteBatchInternal::UpdateProtectionInfo(wb, 8)
+//     (db/write_batch.cc:3164-3181): each rep's ProtectionInfoKVOC64 values in
+//     record order and its Iterate status (forst_write_batch_protect_batch)
+struct KvBytes {
+  const char* data;
+  size_t size;
+};
+class KvProtection {
+ public:
+  explicit KvProtection(void* hip_stream = nullptr) : stream_(hip_stream) {}
+  ~KvProtection();
+  KvProtection(const KvProtection&) = delete;
+  KvProtection& operator=(const KvProtection&) = delete;
+  Status VerifyMemtableEntries(const char* arena, uint64_t arena_len,
+                               const std::vector<uint64_t>& entry_offsets,
+                               uint32_t protection_bytes, std::vector<uint8_t>* status);
+  // kinds[i]: forst_block_kv_checksum_batch's block kind | flags
+  Status BlockKvChecksums(const std::vector<KvBytes>& blocks, const std::vector<uint8_t>& kinds,
+                          uint32_t protection_bytes, std::vector<std::string>* kv_checksums,
+                          std::vector<uint8_t>* status);
+  Status WriteBatchProtection(const std::vector<KvBytes>& reps,
+                              std::vector<std::vector<uint64_t>>* prot,
+                              std::vector<Status>* rep_status);
+  // the Corruption text of a WriteBatch status code (write_batch.cc:361-716)
+  static Status WriteBatchStatus(uint8_t code);
+
+ private:
+  Status Stage(const std::vector<KvBytes>& parts, std::vector<uint64_t>* offs);
+  uint8_t* Grow(uint64_t bytes);
+  void* stream_;
+  void* dev_ = nullptr;
+  uint64_t cap_ = 0;
+  Status grow_status_;
+};
+
 }  // namespace forst_gpu

@@ -523,7 +523,12 @@ const char* forst_host_last_error(void);
  * forst_host_context_stats reports how many contexts exist and the device /
  * pinned bytes they hold; forst_host_context_trim gives the buffers of every
  * context not in use back to the driver (*released_bytes, nullable), e.g.
- * after a burst of concurrent callers. */
+ * after a burst of concurrent callers.  What a context keeps for the life of
+ * the process (trim does not end them): the first copy of >= 4 MiB through it
+ * starts 3 detached helper threads of its copier (host_batch.cc Copier), and
+ * its WAL copy stream with its per-window copied[] events stays created; so
+ * threads and streams grow with the PEAK number of concurrent contexts per
+ * device, not with the number of calls.  Contexts are never freed. */
 int forst_host_context_stats(uint32_t* contexts, uint64_t* device_bytes,
                              uint64_t* pinned_bytes);
 int forst_host_context_trim(uint64_t* released_bytes);

@@ -12,15 +12,37 @@ import tempfile
 import numpy as np
 
 HERE = os.path.dirname(os.path.abspath(__file__))
-_lib = None
+_libs = {}
+_defines = ""  # extra -D options of the build lib() returns (variant())
+
+
+class variant:
+    """with emu.variant("-DFOO=1"): ... -- the calls inside go through a build
+    of the kernel sources with those build knobs (built once, cached)"""
+
+    def __init__(self, defines):
+        self.defines = defines
+
+    def __enter__(self):
+        global _defines
+        self.prev, _defines = _defines, self.defines
+        return self
+
+    def __exit__(self, *exc):
+        global _defines
+        _defines = self.prev
 
 
 def lib():
-    global _lib
-    if _lib is None:
-        out = os.path.join(tempfile.gettempdir(), f"libforst_emu_{os.getpid()}.so")
+    L = _libs.get(_defines)
+    if L is None:
+        tag = abs(hash(_defines)) if _defines else 0
+        out = os.path.join(tempfile.gettempdir(), f"libforst_emu_{os.getpid()}_{tag}.so")
+        env = dict(os.environ)
+        if _defines:
+            env["EMU_DEFINES"] = (env.get("EMU_DEFINES", "") + " " + _defines).strip()
         subprocess.check_call([os.path.join(HERE, "build_emu.sh"), out],
-                              stdout=subprocess.DEVNULL)
+                              stdout=subprocess.DEVNULL, env=env)
         L = ctypes.CDLL(out)
         vp, u64, u32, i = ctypes.c_void_p, ctypes.c_uint64, ctypes.c_uint32, ctypes.c_int
         sigs = {
@@ -50,8 +72,8 @@ def lib():
         for name, (res, args) in sigs.items():
             f = getattr(L, name)
             f.restype, f.argtypes = res, args
-        _lib = L
-    return _lib
+        _libs[_defines] = L
+    return L
 
 
 def _p(a):

@@ -399,7 +399,7 @@ def test_emu_rows_extra_dword_windows():
 @pytest.mark.parametrize("recyclable", [False, True])
 def test_emu_raw_split_short_and_long(recyclable):
     """Raw batches big enough for the global feed (>= 64 descriptors per wave
-    of the grid) are split by length (crc32c.hip FORST_RAW_SPLIT, 512 B):
+    of the grid) are split by length (crc32c.hip FORST_RAW_SPLIT, 256 B):
     shorter messages one per lane (crc32c_raw_lane_kernel), the rest on the
     rows kernel, which drops the short ones from each batch as it loads it
     (crc32c_rows_raw_filt_kernel).  Every length around the split, every start
@@ -411,7 +411,8 @@ def test_emu_raw_split_short_and_long(recyclable):
     rng = np.random.default_rng(52 + int(recyclable))
     n = 3000
     sizes = rng.integers(0, 1500, n).astype(np.uint32)
-    sizes[:64] = 480 + np.arange(64)
+    split = 256  # FORST_RAW_SPLIT: the 64 lengths straddle it (split - 32 .. split + 31)
+    sizes[:64] = split - 32 + np.arange(64)
     sizes[64:80] = np.arange(16)
     offs = np.zeros(n, np.uint64)
     offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + rng.integers(0, 4, n - 1).astype(np.uint64))
@@ -427,8 +428,11 @@ def test_emu_raw_split_short_and_long(recyclable):
     o2[6], s2[6] = total - 100, 600              # long, past the end
     o2[7], s2[7] = 1 << 59, 600                  # long, offset >= 2^58
     o2[8], s2[8] = (1 << 58) - 1, 700            # long, just below 2^58
-    o2[9], s2[9] = total - 509, 509              # short, ends at the buffer end
+    o2[9], s2[9] = total - 509, 509              # long, ends at the buffer end
     o2[10], s2[10] = total - 1300, 1300          # long, ends at the buffer end
+    o2[11], s2[11] = total - 255, 255            # short (split - 1), ends at the buffer end:
+    o2[12], s2[12] = total - 256, 256            # the lane kernel's end-of-buffer fallback,
+    o2[13], s2[13] = total - 77, 77              # then the split itself
     got = emu.crc32c(base, o2, s2)
     for k in range(n):
         o, s = int(o2[k]), int(s2[k])
@@ -533,3 +537,18 @@ def test_emu_block_kv_checksums_vs_reference(kv_sites):
             assert st[j] == 0 and nk == want, (c["src"], c["kind_name"], nk, want)
             got = enc[int(first[j]) * pb:int(first[j + 1]) * pb].tobytes().hex()
             assert got == c[f"kv_checksum_{pb}"], (c["src"], c["kind_name"])
+
+
+@pytest.mark.parametrize("recyclable", [False, True])
+def test_emu_wal_record_xxh3_unpacked_form(recyclable):
+    """a14's unpacked bookkeeping (wal_hash.h: the flag kernel, a second scan
+    and gpos, taken beyond 2^24 records or a 2^40-byte log; the patch kernel
+    then writes straight into out) forced on with FORST_WH_UNPACKED: the same
+    fragment-edge log as above, every logical record's hash equals XXH3 of its
+    payload"""
+    import walcases as W
+    buf, po, payload, lens, targets = W.frag_edge_log(recyclable, seed=9 + recyclable)
+    with emu.variant("-DFORST_WH_UNPACKED"):
+        h, f = emu.wal_record_xxh3(buf, po)
+    assert len(h) == len(lens)
+    assert (np.asarray(h).view(np.uint64) == W.expected_hashes(payload, lens)).all()

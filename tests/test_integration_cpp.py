@@ -87,6 +87,40 @@ struct WalWriterFields {
   }
 };
 
+// a15 at its call sites: a memtable arena block before flush ...
+Status KvMemtableSnippet(const char* arena, uint64_t arena_len,
+                         const std::vector<uint64_t>& entry_offsets,
+                         uint32_t protection_bytes_per_key, bool allow_data_in_errors,
+                         void* stream) {
+  Status s;
+@KV_MEMTABLE@
+  return s;
+}
+
+// ... the members of Block (table/block_based/block.h:276-290) the block
+// snippet fills ...
+struct BlockProtFields {
+  const char* data_;
+  size_t size_;
+  char* kv_checksum_ = nullptr;
+  uint32_t checksum_size_ = 0;
+  uint8_t protection_bytes_per_key_ = 0;
+};
+Status KvBlockSnippet(std::vector<BlockProtFields*>& blocks, uint8_t kind,
+                      uint8_t protection_bytes_per_key, void* stream) {
+  Status s;
+@KV_BLOCK@
+  return s;
+}
+
+// ... and the write batches of a recovery
+Status KvWriteBatchSnippet(const std::vector<Slice>& records, void* stream,
+                           std::vector<std::vector<uint64_t>>* prot) {
+  Status s;
+@KV_WRITE_BATCH@
+  return s;
+}
+
 }  // namespace ROCKSDB_NAMESPACE
 '''
 
@@ -102,8 +136,11 @@ int main(int argc, char**) {
   using namespace ROCKSDB_NAMESPACE;
   void* fns[] = {reinterpret_cast<void*>(&VerifySnippet), reinterpret_cast<void*>(&WriterSnippet),
                  reinterpret_cast<void*>(&WalRecoverSnippet),
-                 reinterpret_cast<void*>(&WalWriterFields::AddRecordGroup)};
-  if (argc > 99) std::printf("%p", fns[argc % 4]);  // never run: link check only
+                 reinterpret_cast<void*>(&WalWriterFields::AddRecordGroup),
+                 reinterpret_cast<void*>(&KvMemtableSnippet),
+                 reinterpret_cast<void*>(&KvBlockSnippet),
+                 reinterpret_cast<void*>(&KvWriteBatchSnippet)};
+  if (argc > 99) std::printf("%p", fns[argc % 7]);  // never run: link check only
   return 0;
 }
 '''
@@ -124,7 +161,8 @@ def split_includes(code):
 
 
 SNIPPETS = {"verify": "@VERIFY@", "writer": "@WRITER@", "wal_recover": "@WAL_RECOVER@",
-            "wal_writer": "@WAL_WRITER@"}
+            "wal_writer": "@WAL_WRITER@", "kv_memtable": "@KV_MEMTABLE@", "kv_block": "@KV_BLOCK@",
+            "kv_write_batch": "@KV_WRITE_BATCH@"}
 
 
 def integration_source():
@@ -141,10 +179,11 @@ def integration_source():
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "rocksdb")),
                     reason="needs the reference headers (/root/reference)")
 def test_integration_snippets_compile_inside_forst(tmp_path):
-    """INTEGRATION.md's four call-site snippets (block verify, table writer,
-    WAL recovery loop, WAL write group) type-check against the reference's
-    own headers (db/log_reader.h, db/log_writer.h, db/write_batch_internal.h
-    for the WAL ones)"""
+    """INTEGRATION.md's call-site snippets (block verify, table writer, WAL
+    recovery loop, WAL write group, and a15's memtable / block / WriteBatch
+    sites) type-check against the reference's own headers (db/log_reader.h,
+    db/log_writer.h, db/write_batch_internal.h for the WAL ones,
+    db/memtable.h for the memtable one)"""
     f = tmp_path / "integration_snippets.cc"
     f.write_text(integration_source())
     r = subprocess.run(["g++", "-std=c++17", "-fsyntax-only", "-Wall", "-Werror=shadow",
@@ -208,6 +247,9 @@ def test_integration_snippets_link_against_reference_objects(tmp_path):
     assert "rocksdb::WriteBatchInternal::SetContents" in syms or \
         "forstdb::WriteBatchInternal::SetContents" in syms
     assert "forst_gpu::WalRecovery::Next" in syms and "forst_gpu::WalWriteGroup::Frame" in syms
+    assert "forst_gpu::KvProtection::VerifyMemtableEntries" in syms
+    assert "rocksdb::MemTable::VerifyEntryChecksum" in syms or \
+        "forstdb::MemTable::VerifyEntryChecksum" in syms
 
 
 @pytest.mark.skipif(not os.path.isdir(os.path.join(REF, "include", "rocksdb")),

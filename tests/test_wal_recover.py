@@ -72,8 +72,8 @@ def test_recover_on_gpu(recyclable):
 
 
 def _short_lengths_log(recyclable, reps, seed):
-    """Full records of every short length 0..240 (their XXH3 on the lane
-    kernel, xxh3_short_sel, their CRCs on the raw path), each length at
+    """Full records of every short length 0..240 (their CRC and XXH3 in
+    wal_short_rows_kernel, a record per 16-lane row), each length at
     every payload alignment mod 4 over the repeats, between long records;
     one record's type byte flipped (a CRC mismatch on the raw path)"""
     rng = np.random.default_rng(seed)
@@ -101,8 +101,10 @@ def test_recover_short_lengths_on_emulator():
 @pytest.mark.gpu
 @pytest.mark.parametrize("recyclable", [False, True])
 def test_recover_short_lengths_on_gpu(recyclable):
-    """the same on the GPU, with enough short records (> 64 K raw-list
-    entries) that the raw path runs ahead of the fused kernel"""
+    """the same on the GPU at scale (300 repeats): the Full records of
+    <= 240 B are short candidates (head 2) and take wal_short_rows_kernel;
+    they are not on the raw list, so this log does not reach the kRawFirst
+    branch -- test_recover_many_raw_records_on_gpu covers that"""
     import torch
     from forst_amd import engine
     log = _short_lengths_log(recyclable, 300, 4)

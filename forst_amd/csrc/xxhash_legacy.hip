@@ -245,24 +245,27 @@ __global__ void __launch_bounds__(kThreads) xxhash_legacy_kernel(BlockArgs a) {
 // copied into the lane's LDS slot with independent loads and finished there.
 constexpr uint32_t kLWaves = 4;
 constexpr uint32_t kLThreads = kLWaves * 64;
-// 256 bytes per lane and step (64 dwords in flight per lane), one 4-wave
-// workgroup per CU: each lane consumes whole cache lines per step, and the
-// CU streams 256 messages at once.  A/B on one box, 1 M x 16 KiB, verify /
-// trailer fraction of the HBM peak (profiles/ab_r05/
-// xxhash_lane_step_occupancy.log): the group kernel 0.21 / 0.21 (XXH32),
-// 0.32 / 0.31 (XXH64); 64-byte steps at 8 workgroups per CU 0.41 / 0.40;
-// 128 B at 2 per CU 0.53 / 0.50, at 1 per CU 0.56 / 0.57; 256 B at 2 per CU
-// 0.61 / 0.58, at 1 per CU 0.61-0.62 / 0.62 (both hashes) -- with 64-byte
-// steps thousands of lanes each read half a line at a time, and the other
-// half was gone from the caches by the next step.
-#ifndef FORST_LANE_STEP
-#define FORST_LANE_STEP 256
-#endif
+// 256 bytes per message and step, one 4-wave workgroup per CU (the CU streams
+// 256 messages at once).  Round 6: the step's bytes are loaded COALESCED --
+// 16 lanes read one message's 256 bytes with one 16-byte load each, 4
+// messages per load instruction -- and written to the owning lanes' LDS
+// slots, from which each lane reads its own 256 bytes back.  Per-lane 16-byte
+// loads (round 5) touched 64 lines per instruction and stopped at 0.61 of the
+// HBM peak whatever the step size, occupancy or prefetch depth; the
+// transposed form touches 8.  A/B, 1 M x 16 KiB, verify / trailer fraction
+// of the HBM peak (profiles/ab_r06/xxhash_lane_xpose_r06bc.log,
+// xxhash_lane_pf_s512_r06a.log; profiles/ab_r05/xxhash_lane_step_occupancy.log):
+// round 4's group kernel 0.21 / 0.21 (XXH32), 0.32 / 0.31 (XXH64); per-lane
+// loads, 64-byte steps 0.41 / 0.40, 128 B 0.56 / 0.57, 256 B 0.61 / 0.62,
+// 512 B 0.58 / 0.56, 256 B with the next step loaded one iteration ahead
+// 0.60 / 0.62; transposed 0.675 / 0.722 (XXH32), 0.66 / 0.716 (XXH64), with
+// the prefetch as well 0.66 / 0.71, at 2 workgroups per CU 0.655 / 0.63.
 #ifndef FORST_LANE_WG_PER_CU
 #define FORST_LANE_WG_PER_CU 1
 #endif
-constexpr uint32_t kLStep = FORST_LANE_STEP;  // bytes per lane and step (64 or 128)
-constexpr uint32_t kLSlot = kLStep + 16;      // LDS bytes per lane: the < kLStep + 4 tail bytes
+constexpr uint32_t kLStep = 256;          // bytes per message and step: 16 lanes x 16
+constexpr uint32_t kLSlot = kLStep + 16;  // LDS bytes per lane: a step's row, or the
+                                          // < kLStep + 8 tail bytes (16-byte multiple)
 
 // little-endian word at byte o of a lane's slot (o + 8 <= kLSlot)
 __device__ __forceinline__ uint32_t slot32(const uint8_t* sl, uint32_t o) {
@@ -275,7 +278,7 @@ __device__ __forceinline__ uint64_t slot64(const uint8_t* sl, uint32_t o) {
 
 template <int MODE, bool X64>
 __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
-  __shared__ uint32_t slots[kLThreads * kLSlot / 4];
+  __shared__ __attribute__((aligned(16))) uint32_t slots[kLThreads * kLSlot / 4];
   constexpr uint32_t S = X64 ? 32 : 16;  // stripe bytes
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
@@ -318,8 +321,8 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
         if (!valid) {
           nmem = 0;
         } else if (MODE == kModeVerify) {
-          nmem = size + 1;  // ComputeBuiltinChecksum(type, data, size+1)
-          stored = ldu32(p + size + 1);
+          nmem = size + 1;  // ComputeBuiltinChecksum(type, data, size+1); the
+                            // stored word after it is read from the tail slot
         } else if (MODE == kModeRaw) {
           nmem = size;
         } else {
@@ -362,19 +365,46 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
     if (!__ballot(have)) break;
     // ---- one kLStep-byte step of every lane that has one left
     const bool vec = have && pos < vend;
-    if (__ballot(vec)) {
-      const uint8_t* q = (vec ? pa + pos : a.base) + vzero();
+    const uint64_t vmask = __ballot(vec);
+    if (vmask) {
       constexpr int kW = kLStep / 4;  // dwords per step
       uint32_t d[kW + 1];
+      // coalesced: lane 16g + j loads chunk j of message 4k + g's step for
+      // k = 0..15 into that message's row (its lane's slot); then each lane
+      // reads its own row (rows 272 bytes apart: conflict-free b128 reads)
+      const uint64_t qa = reinterpret_cast<uint64_t>(pa + pos);
+      const uint32_t j = lane & 15;
+      uint8_t* const wl = reinterpret_cast<uint8_t*>(slots) + (threadIdx.x & ~63u) * kLSlot;
+      u32x4a4 x[16];
+      const uint8_t* sp[16];  // message 4k + (lane >> 4)'s step address (all lanes
+#pragma unroll                // take part in the shuffles: no selects around them)
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t src = 4 * k + (lane >> 4);
+        const uint32_t lo = __shfl(static_cast<uint32_t>(qa), src);
+        const uint32_t hi = __shfl(static_cast<uint32_t>(qa >> 32), src);
+        sp[k] = reinterpret_cast<const uint8_t*>((static_cast<uint64_t>(hi) << 32) | lo);
+      }
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t src = 4 * k + (lane >> 4);
+        x[k] = ld16_a4(((vmask >> src) & 1 ? sp[k] : a.base) + 16 * j + vzero());
+      }
+      d[kW] = ld4_a4((vec ? pa + pos : a.base) + kLStep + vzero());
+#pragma unroll
+      for (int k = 0; k < 16; ++k) {
+        const uint32_t src = 4 * k + (lane >> 4);
+        *reinterpret_cast<u32x4a4*>(wl + src * kLSlot + 16 * j) = x[k];
+      }
+      __builtin_amdgcn_wave_barrier();
 #pragma unroll
       for (int k = 0; k < kW / 4; ++k) {
-        const u32x4a4 x = ld16_a4(q + 16 * k);
-        d[4 * k] = x.x;
-        d[4 * k + 1] = x.y;
-        d[4 * k + 2] = x.z;
-        d[4 * k + 3] = x.w;
+        const u32x4a4 y = *reinterpret_cast<const u32x4a4*>(sl + 16 * k);
+        d[4 * k] = y.x;
+        d[4 * k + 1] = y.y;
+        d[4 * k + 2] = y.z;
+        d[4 * k + 3] = y.w;
       }
-      d[kW] = ld4_a4(q + kLStep);
+      __builtin_amdgcn_wave_barrier();
       if (vec) {
         uint32_t w[kW];
 #pragma unroll
@@ -405,19 +435,22 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
     if (!__ballot(fin)) continue;
     if (fin) {
       // bytes [vend, nmem) as the dword-aligned words from pa + vend (at slot
-      // byte m + x for message byte vend + x); words past the message are 0
+      // byte m + x for message byte vend + x), in verify mode with the 4
+      // stored checksum bytes after them; words past those are 0
       const uint32_t span = m + (nmem - vend);  // < kLStep + 4
+      const uint32_t want = span + (MODE == kModeVerify ? 4u : 0u);
       const uint8_t* q = pa + vend;
-      constexpr int kT = kLStep / 4 + 1;
+      constexpr int kT = kLStep / 4 + (MODE == kModeVerify ? 2 : 1);
       uint32_t t[kT];
 #pragma unroll
-      for (int k = 0; k < kT; ++k) t[k] = 4u * k < span ? ld4_a4(q + 4 * k + vzero()) : 0u;
+      for (int k = 0; k < kT; ++k) t[k] = 4u * k < want ? ld4_a4(q + 4 * k + vzero()) : 0u;
       uint32_t* sw = reinterpret_cast<uint32_t*>(sl);
 #pragma unroll
       for (int k = 0; k < kT; ++k) sw[k] = t[k];
 #pragma unroll
       for (int k = kT; k < static_cast<int>(kLSlot / 4); ++k) sw[k] = 0u;
       if (nv) sl[span] = static_cast<uint8_t>(vb);
+      if (MODE == kModeVerify) stored = slot32(sl, span);
     }
     if (fin) {
       const uint32_t total = nmem + nv;

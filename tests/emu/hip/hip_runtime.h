@@ -113,6 +113,11 @@ void launch(K kernel, dim3 grid, dim3 block, Args... args) {
 #define blockDim (::emu::g_block)
 
 inline void __syncthreads() { emu::tl_group->bar->arrive_and_wait(); }
+// the lanes of a wave run in lockstep on the hardware: LDS written by one lane
+// before this point is visible to the others after it
+inline void __builtin_amdgcn_wave_barrier() {
+  emu::tl_group->waves[emu::tl_tid.x >> 6].bar->arrive_and_wait();
+}
 inline uint32_t __shfl_xor(uint32_t v, int mask) {
   return emu::exchange(v, (emu::tl_tid.x & 63) ^ static_cast<uint32_t>(mask));
 }

@@ -81,6 +81,38 @@ def test_emu_trailer_roundtrip_mixed():
         assert bad == 0 and ok.all()
 
 
+def test_emu_lane_kernel_unaligned_and_corrupt():
+    """kxxHash / kxxHash64 through the lane kernel (buffers >= 4 KiB): ragged
+    sizes at unaligned offsets (the transposed 16-lane loads and the
+    realignment dword), 16 KiB blocks, the tail slot's stored word in verify
+    mode; then one flipped byte per 7th block is found exactly there"""
+    rng = np.random.default_rng(61)
+    sizes = np.concatenate([rng.integers(0, 9000, 200), rng.integers(0, 600, 60),
+                            [16384] * 12, [255, 256, 257, 259, 260, 511, 512, 513]]).astype(np.uint32)
+    offs = np.zeros(len(sizes), np.uint64)
+    gaps = rng.integers(0, 4, len(sizes) - 1).astype(np.uint64)
+    offs[1:] = np.cumsum(sizes[:-1].astype(np.uint64) + 5 + gaps)
+    total = int(offs[-1]) + int(sizes[-1]) + 5
+    base = rng.integers(0, 256, total, dtype=np.uint8)
+    types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
+    mods = rng.integers(0, 2**32, len(sizes), dtype=np.uint64).astype(np.uint32)
+    for t in (2, 3):
+        b2, out = emu.block_trailer(t, base, offs, sizes, types, mods)
+        want = O.block_checksum_batch(t, base, offs, sizes, last_bytes=types, modifiers=mods)
+        assert (out == want).all()
+        got = emu.block_checksum(t, base, offs, sizes, last=types)
+        assert (got == O.block_checksum_batch(t, base, offs, sizes, last_bytes=types)).all()
+        comp, st, ok, bad = emu.block_verify(t, b2, offs, sizes, mods)
+        assert bad == 0 and ok.all()
+        b3 = b2.copy()
+        hit = np.arange(0, len(sizes), 7)
+        hit = hit[sizes[hit] > 0]
+        for k in hit:
+            b3[int(offs[k]) + int(rng.integers(0, int(sizes[k])))] ^= 0x10
+        comp, st, ok, bad = emu.block_verify(t, b3, offs, sizes, mods)
+        assert bad == len(hit) and (np.flatnonzero(ok == 0) == hit).all()
+
+
 def test_emu_wal():
     rng = np.random.default_rng(1)
     lens = rng.integers(0, 40000, 60).astype(np.uint32)

@@ -632,6 +632,9 @@ def _norm_kernel(name):
     # xxhash_lane_kernel<MODE, X64> (rocprof) -> xxhash32/64_lane_kernel<mode> (engine)
     n = re.sub(r"^xxhash_lane_kernel<(\d), (true|false)>$",
                lambda m: f"xxhash{64 if m.group(2) == 'true' else 32}_lane_kernel<{m.group(1)}>", n)
+    if n.startswith("kv_kernel<"):  # KvMode (engine.h), not the block modes
+        kv = {"0": "hash64", "1": "protect", "2": "verify", "3": "mem_verify", "4": "mem_protect"}
+        return re.sub(r"<(\d)>", lambda m: "<" + kv[m.group(1)] + ">", n)
     return re.sub(r"<(\d)>", lambda m: "<" + modes[m.group(1)] + ">", n)
 
 

@@ -265,7 +265,7 @@ constexpr uint32_t kLThreads = kLWaves * 64;
 #endif
 constexpr uint32_t kLStep = 256;          // bytes per message and step: 16 lanes x 16
 constexpr uint32_t kLSlot = kLStep + 16;  // LDS bytes per lane: a step's row, or the
-                                          // < kLStep + 8 tail bytes (16-byte multiple)
+                                          // < kLStep + 11 tail bytes (16-byte multiple)
 
 // little-endian word at byte o of a lane's slot (o + 8 <= kLSlot)
 __device__ __forceinline__ uint32_t slot32(const uint8_t* sl, uint32_t o) {
@@ -331,8 +331,11 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
           vb = a.last_bytes ? a.last_bytes[i] : ldu8(p + size);
         }
         // steps whose aligned window [pa + pos, + kLStep + 4) lies in the
-        // message's own bytes
-        vend = nmem + m >= kLStep + 4 ? ((nmem + m - 4) & ~(kLStep - 1)) : 0u;
+        // message's own bytes, counted without m: messages of one size take
+        // the same number of steps whatever their alignment, so the lanes of
+        // a wave stay in step (with m in the count, verify's 16 KiB + 1 byte
+        // messages took 63 or 64 steps and the wave's lanes drifted apart)
+        vend = nmem >= kLStep + 4 ? ((nmem - 4) & ~(kLStep - 1)) : 0u;
         pos = 0;
         if (X64) {
           v0 = Q64_1 + Q64_2;
@@ -437,10 +440,10 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
       // bytes [vend, nmem) as the dword-aligned words from pa + vend (at slot
       // byte m + x for message byte vend + x), in verify mode with the 4
       // stored checksum bytes after them; words past those are 0
-      const uint32_t span = m + (nmem - vend);  // < kLStep + 4
+      const uint32_t span = m + (nmem - vend);  // < kLStep + 7
       const uint32_t want = span + (MODE == kModeVerify ? 4u : 0u);
       const uint8_t* q = pa + vend;
-      constexpr int kT = kLStep / 4 + (MODE == kModeVerify ? 2 : 1);
+      constexpr int kT = kLStep / 4 + (MODE == kModeVerify ? 3 : 2);
       uint32_t t[kT];
 #pragma unroll
       for (int k = 0; k < kT; ++k) t[k] = 4u * k < want ? ld4_a4(q + 4 * k + vzero()) : 0u;

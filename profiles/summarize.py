@@ -24,6 +24,7 @@ from collections import defaultdict
 
 ROOT = os.path.dirname(os.path.dirname(os.path.abspath(__file__)))
 MODES = {"0": "compute", "1": "trailer", "2": "verify", "3": "raw"}
+KV_MODES = {"0": "hash64", "1": "protect", "2": "verify", "3": "mem_verify", "4": "mem_protect"}
 TIMED = 10  # bench.py --steps default (profiles/profile.sh runs the same count)
 
 
@@ -31,6 +32,8 @@ def short(name):
     """rocprof's demangled name -> the engine's kernel name"""
     n = name.replace("forst::(anonymous namespace)::", "").replace("void ", "")
     n = n.split("(forst::")[0].split("(unsigned")[0].split("(")[0].strip()
+    if n.startswith("kv_kernel<"):  # KvMode (engine.h), not the block modes
+        return re.sub(r"<(\d)>", lambda m: "<" + KV_MODES[m.group(1)] + ">", n)
     return re.sub(r"<(\d)>", lambda m: "<" + MODES[m.group(1)] + ">", n)
 
 

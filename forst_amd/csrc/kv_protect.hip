@@ -199,21 +199,36 @@ __device__ __forceinline__ void long_last_load(const uint8_t* p, uint32_t len, u
 // first block `b` and last stripe (l0, l1) are already loaded; every lane of
 // a row with act gets the hash.  Rows may differ in length: the block loop
 // runs to the wave's largest, uniform around the DPP row sums.
-__device__ uint64_t row_long(const uint64_t* S, const uint8_t* p, uint32_t len, uint64_t seed,
-                             bool act, uint32_t t, Block& b, uint64_t l0, uint64_t l1) {
+// The 14 secret words lane t of a row uses for a > 240-byte field: the chunk
+// pairs of stripes t/4 + 4k (j = 2k, 2k + 1), the scramble pair (8, 9), the
+// last-stripe pair (10, 11) and the merge pair (12, 13).
+constexpr uint32_t kLongSec = 14;
+__device__ __forceinline__ uint32_t long_sec_off(uint32_t t, uint32_t j) {
+  const uint32_t pp = t & 3;
+  if (j < 8) return 8 * ((t >> 2) + 4 * (j >> 1)) + 16 * pp + 8 * (j & 1);
+  constexpr uint32_t kBase[6] = {128, 136, 121, 129, 11, 19};
+  return kBase[j - 8] + 16 * pp;
+}
+
+// TAB: T = lane t's kLongSec words for `seed`, precomputed in LDS (the value
+// seed: every round's long value), else derived from S here (keys)
+template <bool TAB>
+__device__ uint64_t row_long(const uint64_t* S, const uint64_t* T, const uint8_t* p, uint32_t len,
+                             uint64_t seed, bool act, uint32_t t, Block& b, uint64_t l0,
+                             uint64_t l1) {
   const uint32_t pp = t & 3;
   uint64_t acc0 = pp == 0 ? P32_3 : pp == 1 ? P64_2 : pp == 2 ? P64_4 : P64_5;  // INIT_ACC
   uint64_t acc1 = pp == 0 ? P64_1 : pp == 1 ? P64_3 : pp == 2 ? P32_2 : P32_1;
   const uint32_t nb = act ? len >> 10 : 0;
+  auto sec = [&](uint32_t j) { return TAB ? T[j] : psec(S, long_sec_off(t, j), seed); };
   // the chunk secrets: stripe st's at 8 st + 16 pp (aligned words)
   uint64_t k0[4], k1[4];
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
-    const uint32_t off = 8 * ((t >> 2) + 4 * k) + 16 * pp;
-    k0[k] = psec(S, off, seed);
-    k1[k] = psec(S, off + 8, seed);
+    k0[k] = sec(2 * k);
+    k1[k] = sec(2 * k + 1);
   }
-  const uint64_t ks0 = psec(S, 128 + 16 * pp, seed), ks1 = psec(S, 136 + 16 * pp, seed);
+  const uint64_t ks0 = sec(8), ks1 = sec(9);
   for (uint32_t g = 0;; ++g) {
     uint64_t c0 = 0, c1 = 0;
 #pragma unroll
@@ -236,11 +251,11 @@ __device__ uint64_t row_long(const uint64_t* S, const uint8_t* p, uint32_t len, 
     long_block_load(p, len, g + 1, t, act && g < nb, b);
   }
   if (len & 63) {
-    acc0 += l0 + mul32to64(l0 ^ psec(S, 121 + 16 * pp, seed));
-    acc1 += l1 + mul32to64(l1 ^ psec(S, 129 + 16 * pp, seed));
+    acc0 += l0 + mul32to64(l0 ^ sec(10));
+    acc1 += l1 + mul32to64(l1 ^ sec(11));
   }
   // XXPH3_mergeAccs from secret + 11 (xxph3.h:1554-1582)
-  uint64_t h = mul128_fold64(acc0 ^ psec(S, 11 + 16 * pp, seed), acc1 ^ psec(S, 19 + 16 * pp, seed));
+  uint64_t h = mul128_fold64(acc0 ^ sec(12), acc1 ^ sec(13));
   h += quad_xor64<1>(h);
   h += quad_xor64<2>(h);
   return xxph3_avalanche(static_cast<uint64_t>(len) * P64_1 + h);
@@ -343,12 +358,18 @@ template <int MODE>
 __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
   __shared__ uint64_t s_sec[kSecWords];
   __shared__ uint64_t s_slot[kWaves][64];
+  __shared__ uint64_t s_vsec[16 * kLongSec];  // the value seed's long-field secrets per t
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15;
   if (threadIdx.x < kSecWords) s_sec[threadIdx.x] = threadIdx.x < 24 ? sec64(8 * threadIdx.x) : 0;
   __syncthreads();
   const uint64_t* S = s_sec;
+  static_assert(16 * kLongSec <= kThreads, "one table word per thread");
+  if (threadIdx.x < 16 * kLongSec)
+    s_vsec[threadIdx.x] = psec(S, long_sec_off(threadIdx.x / kLongSec, threadIdx.x % kLongSec), kSeedV);
+  __syncthreads();
+  const uint64_t* VT = s_vsec + t * kLongSec;
   // this lane's mix16B secret pair (seed applied per field)
   const uint64_t SA = psec(S, term_secret(t), 0), SB = psec(S, term_secret(t) + 8, 0);
   uint64_t* slot = s_slot[wave];
@@ -443,12 +464,21 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
 
       // -- 17..240-byte fields: the row's terms
       uint64_t h = 0;
-      {
+#ifdef FORST_KV_PROBE  // diagnostics: the round's loads only (no hashing)
+      h = kd0 ^ kd1 ^ vd0 ^ vd1 ^ vl0 ^ vl1;
+#pragma unroll
+      for (int k = 0; k < 4; ++k) h ^= vb.d0[k] ^ vb.d1[k];
+      h ^= row_ror64<8>(h);
+      if (t == 7) slot[src] = h;
+      continue;
+#endif
+      // (each class's code only when one of the wave's four rows needs it)
+      if (__ballot(kc == kShort)) {
         const uint64_t tk = kterm ? mul128_fold64(kd0 ^ (SA + rks), kd1 ^ (SB - rks)) : 0;
         const uint64_t fk = short_finish(tk, rkl);
         if (kc == kShort) h ^= fk;
       }
-      if (MODE != kKvHash) {
+      if (MODE != kKvHash && __ballot(vc == kShort)) {
         const uint64_t tv = vterm ? mul128_fold64(vd0 ^ (SA + kSeedV), vd1 ^ (SB - kSeedV)) : 0;
         const uint64_t fv = short_finish(tv, rvl);
         if (vc == kShort) h ^= fv;
@@ -463,7 +493,7 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       }
       // -- > 240-byte fields
       if (__ballot(vc == kLong)) {
-        const uint64_t hl = row_long(S, vp, rvl, kSeedV, vc == kLong, t, vb, vl0, vl1);
+        const uint64_t hl = row_long<true>(S, VT, vp, rvl, kSeedV, vc == kLong, t, vb, vl0, vl1);
         if (vc == kLong) h ^= hl;
       }
       if (__ballot(kc == kLong)) {  // (keys over 240 bytes: rare, loaded here)
@@ -471,7 +501,7 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
         uint64_t kl0, kl1;
         long_block_load(kp, rkl, 0, t, kc == kLong, kb);
         long_last_load(kp, rkl, t, kc == kLong, kl0, kl1);
-        const uint64_t hl = row_long(S, kp, rkl, rks, kc == kLong, t, kb, kl0, kl1);
+        const uint64_t hl = row_long<false>(S, nullptr, kp, rkl, rks, kc == kLong, t, kb, kl0, kl1);
         if (kc == kLong) h ^= hl;
       }
       if (t == 7) slot[src] = h;

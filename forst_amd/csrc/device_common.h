@@ -22,6 +22,14 @@ __device__ __forceinline__ uint64_t uniform64(uint64_t v) {
   return (static_cast<uint64_t>(hi) << 32) | lo;
 }
 
+// a kernel's register budget for n waves per SIMD (the compiler spills
+// rather than exceed it); nothing in the host emulation (tests/emu)
+#ifdef FORST_HOST_EMULATION
+#define FORST_WAVES_PER_EU(n)
+#else
+#define FORST_WAVES_PER_EU(n) __attribute__((amdgpu_waves_per_eu(n)))
+#endif
+
 // 16-byte vector with only 4-byte alignment: lowers to one global_load_dwordx4
 // on gfx950 (dword-aligned multi-dword loads are legal), so lane segments that
 // start at any dword boundary are read with one instruction.

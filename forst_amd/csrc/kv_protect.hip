@@ -34,6 +34,7 @@
 // lines per load -- and long values in a second pass that fetched the same
 // lines again: 0.18 of peak, 1.4x traffic.)
 #include <cstdlib>
+#include <type_traits>
 
 #include "device_common.h"
 #include "engine.h"
@@ -88,18 +89,52 @@ __device__ __forceinline__ uint64_t xxph3_1to3(uint32_t c1, uint32_t c2, uint32_
   return xxph3_avalanche(keyed * P64_1);
 }
 
+// Where a round's field bytes come from: global memory (GSrc) or the wave's
+// LDS stage (LSrc, the sub-tile's byte span loaded coalesced); offsets are
+// bytes from the field start.
+struct GSrc {
+  const uint8_t* p;
+  __device__ __forceinline__ void ld16(uint32_t o, uint64_t& d0, uint64_t& d1) const {
+    const uint8_t* e = p + o;
+    const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(e) & 3);
+    ld16u(e - m, m, d0, d1);
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t o) const { return ldu64(p + o); }
+  __device__ __forceinline__ uint32_t u32(uint32_t o) const { return ldu32(p + o); }
+  __device__ __forceinline__ uint32_t u8(uint32_t o) const { return ldu8(p + o); }
+};
+struct LSrc {
+  const uint32_t* L;  // the wave's stage (dwords)
+  uint32_t x;         // the field's byte offset in it
+  __device__ __forceinline__ uint32_t u32(uint32_t o) const {
+    const uint32_t b = x + o;
+    return __builtin_amdgcn_alignbyte(L[(b >> 2) + 1], L[b >> 2], b & 3);
+  }
+  __device__ __forceinline__ void ld16(uint32_t o, uint64_t& d0, uint64_t& d1) const {
+    const uint32_t b = x + o, w = b >> 2, sh = b & 3;
+    const uint32_t v0 = L[w], v1 = L[w + 1], v2 = L[w + 2], v3 = L[w + 3], v4 = L[w + 4];
+    d0 = mk64(__builtin_amdgcn_alignbyte(v1, v0, sh), __builtin_amdgcn_alignbyte(v2, v1, sh));
+    d1 = mk64(__builtin_amdgcn_alignbyte(v3, v2, sh), __builtin_amdgcn_alignbyte(v4, v3, sh));
+  }
+  __device__ __forceinline__ uint64_t u64(uint32_t o) const { return mk64(u32(o), u32(o + 4)); }
+  __device__ __forceinline__ uint32_t u8(uint32_t o) const {
+    const uint32_t b = x + o;
+    return (L[b >> 2] >> (8 * (b & 3))) & 0xffu;
+  }
+};
+
 // The bytes a 0..16-byte field's formula reads (xxph3.h:1082-1140), loaded
 // exactly: 9..16 -> d0 = first 8, d1 = last 8; 4..8 -> d0 = first 4 | last 4
 // << 32; 1..3 -> d0 = in[0] | in[len/2] << 8 | in[len-1] << 16.
-__device__ __forceinline__ void tiny_load(const uint8_t* in, uint32_t len, uint64_t& d0,
-                                          uint64_t& d1) {
+template <class Src>
+__device__ __forceinline__ void tiny_load(const Src& in, uint32_t len, uint64_t& d0, uint64_t& d1) {
   if (len > 8) {
-    d0 = ldu64(in);
-    d1 = ldu64(in + len - 8);
+    d0 = in.u64(0);
+    d1 = in.u64(len - 8);
   } else if (len >= 4) {
-    d0 = ldu32(in) | (static_cast<uint64_t>(ldu32(in + len - 4)) << 32);
+    d0 = in.u32(0) | (static_cast<uint64_t>(in.u32(len - 4)) << 32);
   } else if (len) {
-    d0 = ldu8(in) | (ldu8(in + (len >> 1)) << 8) | (ldu8(in + len - 1) << 16);
+    d0 = in.u8(0) | (in.u8(len >> 1) << 8) | (in.u8(len - 1) << 16);
   }
 }
 __device__ __forceinline__ uint64_t tiny_hash(uint64_t d0, uint64_t d1, uint32_t len, uint64_t seed) {
@@ -168,31 +203,27 @@ struct Block {
   uint64_t d0[4], d1[4];
   uint32_t mask;
 };
-__device__ __forceinline__ void long_block_load(const uint8_t* p, uint32_t len, uint32_t g,
+template <class Src>
+__device__ __forceinline__ void long_block_load(const Src& p, uint32_t len, uint32_t g,
                                                 uint32_t t, bool act, Block& b) {
   const uint32_t nb = len >> 10, nbS = (len & 1023) >> 6;
-  const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(p) & 3);
-  const uint8_t* q = p - m + 1024 * g + 16 * t;
   b.mask = 0;
 #pragma unroll
   for (uint32_t k = 0; k < 4; ++k) {
     const uint32_t st = (t >> 2) + 4 * k;
     b.d0[k] = b.d1[k] = 0;
     if (act && (g < nb || (g == nb && st < nbS))) {
-      ld16u(q + 256 * k, m, b.d0[k], b.d1[k]);
+      p.ld16(1024 * g + 16 * t + 256 * k, b.d0[k], b.d1[k]);
       b.mask |= 1u << k;
     }
   }
 }
 // the last stripe (len - 64 + 16 (t%4), xxph3.h:1539-1542), when len % 64
-__device__ __forceinline__ void long_last_load(const uint8_t* p, uint32_t len, uint32_t t, bool act,
+template <class Src>
+__device__ __forceinline__ void long_last_load(const Src& p, uint32_t len, uint32_t t, bool act,
                                                uint64_t& l0, uint64_t& l1) {
   l0 = l1 = 0;
-  if (act && (len & 63)) {
-    const uint8_t* lp = p + len - 64 + 16 * (t & 3);
-    const uint32_t ml = static_cast<uint32_t>(reinterpret_cast<uint64_t>(lp) & 3);
-    ld16u(lp - ml, ml, l0, l1);
-  }
+  if (act && (len & 63)) p.ld16(len - 64 + 16 * (t & 3), l0, l1);
 }
 
 // Row-wide XXPH3 of a > 240-byte field (xxph3.h:1514-1583, 1630-1637) whose
@@ -212,8 +243,8 @@ __device__ __forceinline__ uint32_t long_sec_off(uint32_t t, uint32_t j) {
 
 // TAB: T = lane t's kLongSec words for `seed`, precomputed in LDS (the value
 // seed: every round's long value), else derived from S here (keys)
-template <bool TAB>
-__device__ uint64_t row_long(const uint64_t* S, const uint64_t* T, const uint8_t* p, uint32_t len,
+template <bool TAB, class Src>
+__device__ uint64_t row_long(const uint64_t* S, const uint64_t* T, const Src& p, uint32_t len,
                              uint64_t seed, bool act, uint32_t t, Block& b, uint64_t l0,
                              uint64_t l1) {
   const uint32_t pp = t & 3;
@@ -347,6 +378,16 @@ __device__ __forceinline__ uint32_t decode_mem_entry(const KvArgs& a, uint64_t p
   return in_range(co, a.prot_bytes, a.base_len) ? kMemOk : kMemOutOfRange;
 }
 
+// sub-tiles (kv_kernel): kSub entries, their bytes staged in LDS when they
+// span at most kStage bytes (4 workgroups of 4 waves per CU fit the LDS)
+#ifndef FORST_KV_STAGE
+#define FORST_KV_STAGE 1
+#endif
+constexpr uint32_t kSub = 8;
+constexpr uint64_t kSubMask = (1ull << kSub) - 1;
+constexpr uint32_t kStage = 8704;
+constexpr uint32_t kStageChunks = (kStage + 1023) / 1024;
+
 // field classes
 constexpr uint32_t kTiny = 0, kShort = 1, kLong = 2, kNone = 3;
 __device__ __forceinline__ uint32_t field_class(bool valid, uint32_t len) {
@@ -355,10 +396,11 @@ __device__ __forceinline__ uint32_t field_class(bool valid, uint32_t len) {
 
 // MODE: kKvHash (Hash64 per buffer), kKvProtect, kKvVerify
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
+__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(4) kv_kernel(KvArgs a) {
   __shared__ uint64_t s_sec[kSecWords];
   __shared__ uint64_t s_slot[kWaves][64];
   __shared__ uint64_t s_vsec[16 * kLongSec];  // the value seed's long-field secrets per t
+  __shared__ u32x4 s_stage[kWaves][(kStage + 32) / 16];  // per wave: a sub-tile's bytes
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
   const uint32_t t = lane & 15;
@@ -373,6 +415,11 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
   // this lane's mix16B secret pair (seed applied per field)
   const uint64_t SA = psec(S, term_secret(t), 0), SB = psec(S, term_secret(t) + 8, 0);
   uint64_t* slot = s_slot[wave];
+  const uint32_t* stage = reinterpret_cast<const uint32_t*>(s_stage[wave]);
+  uint8_t* stage_w = reinterpret_cast<uint8_t*>(s_stage[wave]);
+  // staging needs 16-byte alignment of the buffer and one buffer for keys and values
+  const bool stage_ok = FORST_KV_STAGE && a.key_base == nullptr &&
+                        (reinterpret_cast<uint64_t>(a.base) & 15) == 0;
 
   const uint64_t stride = static_cast<uint64_t>(gridDim.x) * kWaves * 64;
   for (uint64_t b0 = (static_cast<uint64_t>(blockIdx.x) * kWaves + wave) * 64; b0 < a.n;
@@ -418,11 +465,22 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       }
     }
     const uint64_t vmask = __ballot(valid);
+    // the bytes this lane's fields cover (the sub-tile spans below)
+    uint64_t flo = ~0ull, fhi = 0;
+    if (valid) {
+      flo = ko;
+      fhi = ko + kl;
+      if (MODE != kKvHash) {
+        flo = vo < flo ? vo : flo;
+        fhi = vo + vl > fhi ? vo + vl : fhi;
+      }
+    }
 
-    // ---- 16 rounds: row R hashes the key and value of entry 16R + r
-    for (uint32_t r = 0; r < 16; ++r) {
-      const uint32_t src = (lane & 48) | r;
-      if (!(vmask & (0x0001000100010001ull << r))) continue;  // (wave-uniform)
+    // ---- one round: row R hashes the key and value of entry src (ST: the
+    // bytes from the wave's stage, which holds [sb, ...) of the buffer)
+    auto round = [&](uint32_t src, auto stc, uint64_t sb) {
+      constexpr bool ST = decltype(stc)::value;
+      using Src = std::conditional_t<ST, LSrc, GSrc>;
       const bool rv = (vmask >> src) & 1;
       const uint64_t rko = shfl64(ko, src);
       const uint32_t rkl = __shfl(kl, src);
@@ -435,8 +493,14 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       }
       const uint32_t kc = field_class(rv, rkl);
       const uint32_t vc = MODE == kKvHash ? kNone : field_class(rv, rvl);
-      const uint8_t* kp = (a.key_base ? a.key_base : a.base) + rko;
-      const uint8_t* vp = a.base + rvo;
+      Src kp, vp;
+      if constexpr (ST) {
+        kp = LSrc{stage, static_cast<uint32_t>(rko - sb)};
+        vp = LSrc{stage, static_cast<uint32_t>(rvo - sb)};
+      } else {
+        kp = GSrc{(a.key_base ? a.key_base : a.base) + rko};
+        vp = GSrc{a.base + rvo};
+      }
 
       // -- every load of the round, issued before any of it is used
       uint64_t kd0 = 0, kd1 = 0, vd0 = 0, vd1 = 0;
@@ -444,16 +508,12 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       const bool kterm = kc == kShort && term_at(t, rkl, dk);
       const bool vterm = vc == kShort && term_at(t, rvl, dv);
       if (kterm) {
-        const uint8_t* e = kp + dk;
-        const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(e) & 3);
-        ld16u(e - m, m, kd0, kd1);
+        kp.ld16(dk, kd0, kd1);
       } else if (kc == kTiny && t == 7) {
         tiny_load(kp, rkl, kd0, kd1);
       }
       if (vterm) {
-        const uint8_t* e = vp + dv;
-        const uint32_t m = static_cast<uint32_t>(reinterpret_cast<uint64_t>(e) & 3);
-        ld16u(e - m, m, vd0, vd1);
+        vp.ld16(dv, vd0, vd1);
       } else if (vc == kTiny && t == 6) {
         tiny_load(vp, rvl, vd0, vd1);
       }
@@ -462,17 +522,9 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
       long_block_load(vp, rvl, 0, t, vc == kLong, vb);
       long_last_load(vp, rvl, t, vc == kLong, vl0, vl1);
 
-      // -- 17..240-byte fields: the row's terms
+      // -- 17..240-byte fields: the row's terms (each class's code only when
+      // one of the wave's four rows needs it)
       uint64_t h = 0;
-#ifdef FORST_KV_PROBE  // diagnostics: the round's loads only (no hashing)
-      h = kd0 ^ kd1 ^ vd0 ^ vd1 ^ vl0 ^ vl1;
-#pragma unroll
-      for (int k = 0; k < 4; ++k) h ^= vb.d0[k] ^ vb.d1[k];
-      h ^= row_ror64<8>(h);
-      if (t == 7) slot[src] = h;
-      continue;
-#endif
-      // (each class's code only when one of the wave's four rows needs it)
       if (__ballot(kc == kShort)) {
         const uint64_t tk = kterm ? mul128_fold64(kd0 ^ (SA + rks), kd1 ^ (SB - rks)) : 0;
         const uint64_t fk = short_finish(tk, rkl);
@@ -505,6 +557,52 @@ __global__ void __launch_bounds__(kThreads) kv_kernel(KvArgs a) {
         if (kc == kLong) h ^= hl;
       }
       if (t == 7) slot[src] = h;
+    };
+
+    // ---- sub-tiles of kSub entries.  A sub-tile whose keys and values lie
+    // in one span of at most kStage bytes (packed entries: kv_checksum's
+    // key | value | protection layout, memtable entries) is loaded into the
+    // wave's stage with coalesced 16-byte loads, 1 KiB per instruction, and
+    // its rounds read the stage; any other sub-tile's rounds load from global
+    // memory.  Round r of sub-tile j: row R hashes entry kSub j + 4 r + R.
+#pragma unroll 1
+    for (uint32_t j = 0; j < 64 / kSub; ++j) {
+      if (!((vmask >> (kSub * j)) & kSubMask)) continue;  // (wave-uniform)
+      uint64_t lo = flo, hi = fhi;
+#pragma unroll
+      for (uint32_t o = 1; o < kSub; o <<= 1) {
+        const uint64_t l2 = shfl_xor64(lo, o), h2 = shfl_xor64(hi, o);
+        lo = l2 < lo ? l2 : lo;
+        hi = h2 > hi ? h2 : hi;
+      }
+      lo = uniform64(shfl64(lo, kSub * j));
+      hi = uniform64(shfl64(hi, kSub * j));
+      const uint64_t sb = lo & ~15ull, se = (hi + 15) & ~15ull;
+      if (stage_ok && se - sb <= kStage && se <= a.base_len) {
+        const uint32_t nbytes = static_cast<uint32_t>(se - sb);
+        // (chunks past the span re-read the first one: the loads are not
+        // predicated, so the compiler keeps them all in flight)
+        u32x4a4 v[kStageChunks];
+#pragma unroll
+        for (uint32_t c = 0; c < kStageChunks; ++c) {
+          const uint32_t o = 1024 * c + 16 * lane;
+          v[c] = ld16_a4(a.base + sb + (o < nbytes ? o : 16 * lane) + vzero());
+        }
+#pragma unroll
+        for (uint32_t c = 0; c < kStageChunks; ++c) {
+          const uint32_t o = 1024 * c + 16 * lane;
+          if (o < nbytes) *reinterpret_cast<u32x4*>(stage_w + o) = u32x4{v[c].x, v[c].y, v[c].z, v[c].w};
+        }
+        wave_lds_sync();
+#pragma unroll 1
+        for (uint32_t r = 0; r < kSub / 4; ++r)
+          round(kSub * j + 4 * r + (lane >> 4), std::true_type{}, sb);
+        wave_lds_sync();  // (the next sub-tile rewrites the stage)
+      } else {
+#pragma unroll 1
+        for (uint32_t r = 0; r < kSub / 4; ++r)
+          round(kSub * j + 4 * r + (lane >> 4), std::false_type{}, 0);
+      }
     }
     wave_lds_sync();
     uint64_t h = valid ? hs ^ slot[lane] : 0;
@@ -557,7 +655,7 @@ hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char**
   if (a.n == 0) return hipSuccess;
   const uint64_t per_wg = uint64_t(kWaves) * 64;
 #ifndef FORST_KV_WG_PER_CU
-#define FORST_KV_WG_PER_CU 8  // (build knob for the A/B: workgroups per CU in the grid)
+#define FORST_KV_WG_PER_CU 4  // (build knob for the A/B: workgroups per CU in the grid)
 #endif
   const uint32_t wg_per_cu = FORST_KV_WG_PER_CU;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(

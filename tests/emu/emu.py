@@ -217,8 +217,9 @@ def _kv_arrays(ko, ks, vo, vs, ops, seqs, cfs):
              None if cfs is None else np.ascontiguousarray(cfs, np.uint32)])
 
 
-def kv_protect(base, ko, ks, vo, vs, ops=None, seqs=None, cfs=None):
-    base = _aligned(base)
+def kv_protect(base, ko, ks, vo, vs, ops=None, seqs=None, cfs=None, misalign=0):
+    base = _aligned(base) if not misalign else _aligned(
+        np.concatenate([np.zeros(misalign, np.uint8), base]))[misalign:]
     arrs, opt = _kv_arrays(ko, ks, vo, vs, ops, seqs, cfs)
     out = np.zeros(len(arrs[0]), np.uint64)
     _chk(lib().forst_kv_protect_batch(_p(base), base.nbytes, *[_p(a) for a in arrs],

@@ -325,6 +325,37 @@ def test_emu_kv_protect_verify(prot_bytes, flags):
     assert set(np.nonzero(ok == 0)[0].tolist()) == want_bad and bad == len(want_bad)
 
 
+def test_emu_kv_staged_and_direct_subtiles():
+    """kv_kernel's sub-tiles: packed entries of small values (their 8-entry
+    spans fit the LDS stage), entries with 3-6 KiB values (spans over it:
+    global loads), entries in reverse buffer order, the buffer ending at the
+    last entry's checksum (the last span may not be staged), and a base that
+    is not 16-byte aligned (no staging) -- every hash equal to the oracle's"""
+    rng = np.random.default_rng(77)
+    n = 400
+    ks = rng.integers(0, 90, n).astype(np.uint32)
+    vs = rng.integers(0, 900, n).astype(np.uint32)
+    vs[rng.integers(0, n, 25)] = rng.integers(3000, 6000, 25)
+    ks[rng.integers(0, n, 5)] = rng.integers(241, 700, 5)
+    ko = np.zeros(n, np.uint64)
+    vo = np.zeros(n, np.uint64)
+    pos = 3
+    for i in range(n):
+        ko[i] = pos
+        pos += int(ks[i])
+        vo[i] = pos
+        pos += int(vs[i]) + 8
+    base = rng.integers(0, 256, pos, dtype=np.uint8)
+    ops = rng.integers(0, 26, n).astype(np.uint8)
+    seqs = rng.integers(0, 2**63, n, dtype=np.uint64)
+    want = O.kv_protect_batch(base, ko, ks, vo, vs, ops, seqs, None)
+    assert (emu.kv_protect(base, ko, ks, vo, vs, ops, seqs) == want).all()
+    r = np.arange(n)[::-1].copy()
+    got = emu.kv_protect(base, ko[r], ks[r], vo[r], vs[r], ops[r], seqs[r])
+    assert (got == want[r]).all()
+    assert (emu.kv_protect(base, ko, ks, vo, vs, ops, seqs, misalign=4) == want).all()
+
+
 def test_emu_crc32c_buffer():
     """whole-buffer CRC: 64 KiB chunk CRCs folded with the combine identity"""
     rng = np.random.default_rng(31)

@@ -383,9 +383,15 @@ __device__ __forceinline__ uint32_t decode_mem_entry(const KvArgs& a, uint64_t p
 #ifndef FORST_KV_STAGE
 #define FORST_KV_STAGE 1
 #endif
+#ifndef FORST_KV_WAVES_PER_EU
+#define FORST_KV_WAVES_PER_EU 4
+#endif
 constexpr uint32_t kSub = 8;
 constexpr uint64_t kSubMask = (1ull << kSub) - 1;
-constexpr uint32_t kStage = 8704;
+#ifndef FORST_KV_STAGE_BYTES
+#define FORST_KV_STAGE_BYTES 8704
+#endif
+constexpr uint32_t kStage = FORST_KV_STAGE_BYTES;
 constexpr uint32_t kStageChunks = (kStage + 1023) / 1024;
 
 // field classes
@@ -396,7 +402,7 @@ __device__ __forceinline__ uint32_t field_class(bool valid, uint32_t len) {
 
 // MODE: kKvHash (Hash64 per buffer), kKvProtect, kKvVerify
 template <int MODE>
-__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(4) kv_kernel(KvArgs a) {
+__global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES_PER_EU) kv_kernel(KvArgs a) {
   __shared__ uint64_t s_sec[kSecWords];
   __shared__ uint64_t s_slot[kWaves][64];
   __shared__ uint64_t s_vsec[16 * kLongSec];  // the value seed's long-field secrets per t

@@ -1,11 +1,11 @@
 #!/bin/bash
-# round-5 evidence at the current build: the whole -m gpu suite and smoke,
+# evidence at the current build: the whole -m gpu suite and smoke,
 # rocprofv3 kernel trace + FETCH/WRITE passes for the configs (C5 split by
 # call site), then the default bench line.  TAG names the profiles.
 set -eo pipefail
 cd "${GRAFT_REPO_ROOT:-/root/repo}"
 export TMPDIR=/tmp
-TAG=${TAG:-r05x}
+TAG=${TAG:-r06z}
 OUT=gpurun_out/final_$TAG
 mkdir -p "$OUT"
 if [ -z "$NOTEST" ]; then

@@ -503,9 +503,9 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES_PE
       if constexpr (ST) {
         kp = LSrc{stage, static_cast<uint32_t>(rko - sb)};
         vp = LSrc{stage, static_cast<uint32_t>(rvo - sb)};
-      } else {
-        kp = GSrc{(a.key_base ? a.key_base : a.base) + rko};
-        vp = GSrc{a.base + rvo};
+      } else {  // (rows without a valid entry load nothing: no pointer from their offsets)
+        kp = GSrc{(a.key_base ? a.key_base : a.base) + (rv ? rko : 0)};
+        vp = GSrc{a.base + (rv ? rvo : 0)};
       }
 
       // -- every load of the round, issued before any of it is used
@@ -584,15 +584,16 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES_PE
       lo = uniform64(shfl64(lo, kSub * j));
       hi = uniform64(shfl64(hi, kSub * j));
       const uint64_t sb = lo & ~15ull, se = (hi + 15) & ~15ull;
-      if (stage_ok && se - sb <= kStage && se <= a.base_len) {
+      if (stage_ok && se > sb && se - sb <= kStage && se <= a.base_len) {
         const uint32_t nbytes = static_cast<uint32_t>(se - sb);
-        // (chunks past the span re-read the first one: the loads are not
-        // predicated, so the compiler keeps them all in flight)
+        // (chunks past the span re-read its first 16 bytes: the loads are
+        // not predicated, so the compiler keeps them all in flight, and no
+        // load leaves [sb, se))
         u32x4a4 v[kStageChunks];
 #pragma unroll
         for (uint32_t c = 0; c < kStageChunks; ++c) {
           const uint32_t o = 1024 * c + 16 * lane;
-          v[c] = ld16_a4(a.base + sb + (o < nbytes ? o : 16 * lane) + vzero());
+          v[c] = ld16_a4(a.base + sb + (o < nbytes ? o : 0u) + vzero());
         }
 #pragma unroll
         for (uint32_t c = 0; c < kStageChunks; ++c) {

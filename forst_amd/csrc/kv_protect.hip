@@ -500,9 +500,9 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES_PE
       const uint32_t kc = field_class(rv, rkl);
       const uint32_t vc = MODE == kKvHash ? kNone : field_class(rv, rvl);
       Src kp, vp;
-      if constexpr (ST) {
-        kp = LSrc{stage, static_cast<uint32_t>(rko - sb)};
-        vp = LSrc{stage, static_cast<uint32_t>(rvo - sb)};
+      if constexpr (ST) {  // (rows without a valid entry, and hash64's absent values, read at 0)
+        kp = LSrc{stage, rv ? static_cast<uint32_t>(rko - sb) : 0u};
+        vp = LSrc{stage, rv && MODE != kKvHash ? static_cast<uint32_t>(rvo - sb) : 0u};
       } else {  // (rows without a valid entry load nothing: no pointer from their offsets)
         kp = GSrc{(a.key_base ? a.key_base : a.base) + (rv ? rko : 0)};
         vp = GSrc{a.base + (rv ? rvo : 0)};
@@ -542,7 +542,7 @@ __global__ void __launch_bounds__(kThreads) FORST_WAVES_PER_EU(FORST_KV_WAVES_PE
         if (vc == kShort) h ^= fv;
       }
       // -- 0..16-byte fields: lane 7 the key's, lane 6 the value's
-      {
+      if (__ballot(kc == kTiny || vc == kTiny)) {
         const bool k7 = t == 7 && kc == kTiny, v6 = t == 6 && vc == kTiny;
         const uint64_t x = tiny_hash(k7 ? kd0 : vd0, k7 ? kd1 : vd1, k7 ? rkl : rvl,
                                      k7 ? rks : kSeedV);

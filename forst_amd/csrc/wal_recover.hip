@@ -1207,6 +1207,20 @@ __global__ void rw_recycled_kernel(RecoverArgs a, uint32_t* flag) {
   *flag = a.log_len >= kLogHdr && recyclable_type(a.log[6]) ? 1u : 0u;
 }
 
+// the count pass's scalars gathered on the device, read back with ONE copy
+// (six 8-byte copies to the host cost ~20 us each: round 6's recovery trace)
+__global__ void rw_pick_kernel(uint64_t* o, const uint64_t* v) { *o = *v; }
+__global__ void rw_counts_kernel(uint64_t* o, const uint64_t* rep_total,
+                                 const unsigned long long* ctl_n,
+                                 const unsigned long long* live_over, const uint8_t* last_kind,
+                                 const uint64_t* last_pos) {
+  o[1] = *rep_total;
+  o[2] = *ctl_n;
+  o[3] = *live_over;
+  o[4] = last_kind ? *last_kind : 0u;
+  o[5] = last_pos ? *last_pos : 0u;
+}
+
 size_t up256(size_t b) { return (b + 255) & ~size_t(255); }
 
 dim3 grid_for(uint64_t n) { return dim3(static_cast<uint32_t>((n + kLanes - 1) / kLanes ? (n + kLanes - 1) / kLanes : 1)); }
@@ -1629,21 +1643,30 @@ hipError_t launch_wal_recover(const uint8_t* log, uint64_t log_len, uint32_t log
   uint64_t last_pos = 0;
   // the state machine's counts (emitted records, reports), the control-record
   // count and the stop token (one sync)
+  void* cov = nullptr;
+  if ((e = alloc(256, &cov)) != hipSuccess) return fail(e);
+  uint64_t* counts = static_cast<uint64_t*>(cov);
   auto count_pass = [&]() -> hipError_t {
     hipLaunchKernelGGL(rw_emit_kernel<false>, tg, dim3(kLanes), 0, st, t, n_tok, f, mode, q.n_emit,
                        q.n_rep, nullptr, nullptr, cr, no_recs, 0, no_reps, 0, nullptr, nullptr,
                        nullptr, nullptr, nullptr);
     scan_u64(q.n_emit, n_tok, q.tiles2, q.emit_at, st);
-    hipError_t r = hipMemcpyAsync(&tot[0], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
-    scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (after the copy above, stream order)
-    if (r == hipSuccess) r = hipMemcpyAsync(&tot[1], q.tiles2 + ntl, 8, hipMemcpyDeviceToHost, st);
-    if (r == hipSuccess) r = hipMemcpyAsync(&n_ctl, q1.ctl_n, 8, hipMemcpyDeviceToHost, st);
-    if (r == hipSuccess) r = hipMemcpyAsync(&live_over, q.live_over, 8, hipMemcpyDeviceToHost, st);
-    if (r == hipSuccess && n_tok)
-      r = hipMemcpyAsync(&last_kind, t.kind + n_tok - 1, 1, hipMemcpyDeviceToHost, st);
-    if (r == hipSuccess && n_tok)
-      r = hipMemcpyAsync(&last_pos, t.pos + n_tok - 1, 8, hipMemcpyDeviceToHost, st);
+    hipLaunchKernelGGL(rw_pick_kernel, dim3(1), dim3(1), 0, st, counts, q.tiles2 + ntl);
+    scan_u64(q.n_rep, n_tok, q.tiles2, q.rep_at, st);  // (reuses the tiles: after the pick)
+    hipLaunchKernelGGL(rw_counts_kernel, dim3(1), dim3(1), 0, st, counts, q.tiles2 + ntl, q1.ctl_n,
+                       q.live_over, n_tok ? t.kind + n_tok - 1 : nullptr,
+                       n_tok ? t.pos + n_tok - 1 : nullptr);
+    uint64_t h[6];
+    hipError_t r = hipMemcpyAsync(h, counts, sizeof(h), hipMemcpyDeviceToHost, st);
     if (r == hipSuccess) r = hipStreamSynchronize(st);
+    if (r == hipSuccess) {
+      tot[0] = h[0];
+      tot[1] = h[1];
+      n_ctl = h[2];
+      live_over = h[3];
+      last_kind = static_cast<uint8_t>(h[4]);
+      last_pos = h[5];
+    }
     return r;
   };
   if ((e = count_pass()) != hipSuccess) return fail(e);

@@ -166,10 +166,12 @@ def test_compressed_blocks_with_lying_size_preambles():
 
 @pytest.mark.parametrize("ctype", [1, 2, 4, 5, 7])
 def test_random_bytes_as_compressed_blocks(ctype):
-    """2000 random byte strings per codec (Snappy, zlib, LZ4, ZSTD, BZip2
-    where the runtime library exists): decoded or rejected, no crash"""
+    """500 random byte strings per codec (Snappy, zlib, LZ4, ZSTD, BZip2
+    where the runtime library exists): decoded or rejected, no crash.  (A
+    random size preamble can state up to 4 GiB, which the codecs allocate
+    and zero as the reference allocates it: some calls take 0.1 s.)"""
     rng = np.random.default_rng(ctype)
-    for i in range(2000):
+    for i in range(500):
         n = int(rng.integers(0, 300))
         b = rng.integers(0, 256, n, np.uint8).tobytes()
         if i % 3 == 0 and n:

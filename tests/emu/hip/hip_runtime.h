@@ -166,6 +166,7 @@ inline unsigned long long __ballot(int pred) {
   return m;
 }
 inline int __popcll(unsigned long long v) { return __builtin_popcountll(v); }
+inline int __ffsll(long long v) { return __builtin_ffsll(v); }
 // v_mbcnt_lo / hi: acc + the bits of mask below this lane (lo: lanes 0..31 of
 // the mask, hi: lanes 32..63)
 inline uint32_t __builtin_amdgcn_mbcnt_lo(uint32_t m, uint32_t acc) {
@@ -239,6 +240,12 @@ inline emu_u32x2 __builtin_amdgcn_permlane32_swap(uint32_t old, uint32_t src, bo
   r[1] = hi ? src : o_partner;
   return r;
 }
+// scoped atomics (the scan's look-back words: clang's __hip_atomic_* builtins
+// also compile for the host) and the wave sleep hint
+#ifndef __HIP_MEMORY_SCOPE_AGENT
+#define __HIP_MEMORY_SCOPE_AGENT 3
+#endif
+inline void __builtin_amdgcn_s_sleep(int) { std::this_thread::yield(); }
 inline uint32_t atomicXor(uint32_t* p, uint32_t v) { return __atomic_fetch_xor(p, v, __ATOMIC_RELAXED); }
 inline unsigned long long atomicAdd(unsigned long long* p, unsigned long long v) {
   return __atomic_fetch_add(p, v, __ATOMIC_RELAXED);

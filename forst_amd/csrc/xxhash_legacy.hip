@@ -263,6 +263,16 @@ constexpr uint32_t kLThreads = kLWaves * 64;
 #ifndef FORST_LANE_WG_PER_CU
 #define FORST_LANE_WG_PER_CU 1
 #endif
+#ifndef FORST_LANE_TRL_STAGE
+#define FORST_LANE_TRL_STAGE 1
+#endif
+#ifndef FORST_LANE_TRL_CAP
+#define FORST_LANE_TRL_CAP 8192
+#endif
+constexpr uint32_t kTrlCap = FORST_LANE_TRL_CAP;  // staged trailers per workgroup (64 KiB of LDS)
+struct TrlEntry {
+  uint32_t i, c;  // descriptor, checksum
+};
 constexpr uint32_t kLStep = 256;          // bytes per message and step: 16 lanes x 16
 constexpr uint32_t kLSlot = kLStep + 16;  // LDS bytes per lane: a step's row, or the
                                           // < kLStep + 11 tail bytes (16-byte multiple)
@@ -279,6 +289,13 @@ __device__ __forceinline__ uint64_t slot64(const uint8_t* sl, uint32_t o) {
 template <int MODE, bool X64>
 __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
   __shared__ __attribute__((aligned(16))) uint32_t slots[kLThreads * kLSlot / 4];
+  // trailer mode: (descriptor, checksum) pairs written after the loop
+  __shared__ TrlEntry s_trl[FORST_LANE_TRL_STAGE && MODE == kModeTrailer ? kTrlCap : 1];
+  __shared__ uint32_t s_ntrl;
+  if (FORST_LANE_TRL_STAGE && MODE == kModeTrailer) {
+    if (threadIdx.x == 0) s_ntrl = 0;
+    __syncthreads();
+  }
   constexpr uint32_t S = X64 ? 32 : 16;  // stripe bytes
   const uint32_t lane = threadIdx.x & 63;
   const uint32_t wave = uniform(threadIdx.x >> 6);
@@ -548,12 +565,32 @@ __global__ void __launch_bounds__(kLThreads) xxhash_lane_kernel(BlockArgs a) {
         const uint32_t c = h + mod;
         if (a.out32) a.out32[i] = c;
         if (MODE == kModeTrailer) {
-          uint8_t* wp = a.base_w + off + size;
-          wp[0] = static_cast<uint8_t>(vb);
-          stu32_bytes(wp + 1, c);
+          uint32_t slot = kTrlCap;
+          if (FORST_LANE_TRL_STAGE && (i >> 32) == 0) slot = atomicAdd(&s_ntrl, 1u);
+          if (slot < kTrlCap) {
+            s_trl[slot] = TrlEntry{static_cast<uint32_t>(i), c};
+          } else {  // (the staging area is full: stored here)
+            uint8_t* wp = a.base_w + off + size;
+            wp[0] = static_cast<uint8_t>(vb);
+            stu32_bytes(wp + 1, c);
+          }
         }
       }
       have = false;
+    }
+  }
+  if (FORST_LANE_TRL_STAGE && MODE == kModeTrailer) {
+    // the staged trailers, stored once every wave of the workgroup is done
+    // (stores share vmcnt with the loads: inside the loop every later step
+    // waited for them); the type byte is the caller's (last_bytes) or the
+    // one already in memory
+    __syncthreads();
+    const uint32_t m = s_ntrl < kTrlCap ? s_ntrl : kTrlCap;
+    for (uint32_t j = threadIdx.x; j < m; j += kLThreads) {
+      const TrlEntry e = s_trl[j];
+      uint8_t* wp = a.base_w + a.offsets[e.i] + a.sizes[e.i];
+      if (a.last_bytes) wp[0] = a.last_bytes[e.i];
+      stu32_bytes(wp + 1, e.c);
     }
   }
 }

@@ -244,6 +244,31 @@ def test_trailer_then_verify_roundtrip_and_corruption(ctype):
         assert set(np.nonzero(~okh)[0].tolist()) == set(victims)
 
 
+@pytest.mark.parametrize("ctype", [CT.kxxHash, CT.kxxHash64])
+def test_lane_kernel_trailer_staging_overflow(ctype):
+    """4 M short kxxHash blocks: a workgroup of the lane kernel finishes more
+    than its 8,192 staged trailers (xxhash_legacy.hip), so the overflow path
+    stores directly -- every trailer byte and checksum against the oracle"""
+    rng = np.random.default_rng(61)
+    sizes = rng.integers(0, 120, 4 << 20).astype(np.uint32)
+    base, offs, sizes = _host_layout(sizes, 7)
+    types = rng.integers(0, 8, len(sizes), dtype=np.uint8)
+    dbase = d(base)
+    out = torch.empty(len(sizes), dtype=torch.uint32, device=DEV)
+    engine.block_trailer_batch(ctype, dbase, d(offs), d(sizes.astype(np.int32)), d(types),
+                               None, out)
+    want = O.block_checksum_batch(int(ctype), base, offs, sizes, last_bytes=types,
+                                  nthreads=O.host_threads())
+    assert (host(out).astype(np.uint64) == want.astype(np.uint64)).all()
+    hb = host(dbase)
+    end = (offs + sizes.astype(np.int64))
+    assert (hb[end] == types).all()
+    stored = np.zeros(len(sizes), np.uint32)
+    for k in range(4):
+        stored |= hb[end + 1 + k].astype(np.uint32) << np.uint32(8 * k)
+    assert (stored == want.astype(np.uint32)).all()
+
+
 def test_out_of_range_descriptors_are_reported_not_read():
     base = d(np.zeros(1000, dtype=np.uint8))
     offs = d(np.array([0, 990, 5000, 100], dtype=np.int64))

@@ -1410,6 +1410,9 @@ __device__ __forceinline__ bool raw_long(uint64_t off, uint32_t size) {
   return size >= kRawSplit && (off >> 58) == 0;
 }
 
+#ifndef FORST_RAW_RING
+#define FORST_RAW_RING 1
+#endif
 template <int MODE, int PROBE, int DEPTH, bool RAW_WG = false, bool FILT = false>
 __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
   static_assert(!FILT || (MODE == kModeRaw && !RAW_WG), "length split: raw global feed only");
@@ -1452,6 +1455,21 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
                           PROBE == 0;
   __shared__ uint32_t st_out[kStage ? kStageW : 1];
   __shared__ uint8_t st_ok[kStage ? kStageW : 4];
+  // raw mode: each wave's results collected in an LDS ring and stored 64 per
+  // instruction when it fills and after the loop (stores share vmcnt with the
+  // loads, so a store per finishing row delayed the next step's data)
+  constexpr bool kRing = FORST_RAW_RING && MODE == kModeRaw && PROBE == 0 && DEPTH == 1;
+  constexpr uint32_t kRingN = 224;  // per wave (16 waves: 28 KiB beside the 128 KiB of tables)
+  __shared__ uint32_t ring_i[kRing ? kWaves * kRingN : 1], ring_v[kRing ? kWaves * kRingN : 1];
+  uint32_t* const ri = ring_i + (kRing ? wave * kRingN : 0);
+  uint32_t* const rv = ring_v + (kRing ? wave * kRingN : 0);
+  uint32_t rcount = 0;  // (wave-uniform)
+  auto ring_flush = [&]() {
+    wave_lds_sync();
+    for (uint32_t j = lane; j < rcount; j += 64) a.out32[ri[j]] = rv[j];
+    wave_lds_sync();
+    rcount = 0;
+  };
   if (!kStage && cg >= a.n) return;
   uint32_t clen = feed.len;  // entries of cb / nb (a batch holds up to 64)
   uint64_t ng = 0;
@@ -1717,7 +1735,22 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
 #ifdef FORST_RAW_STORE_PROBE  // timing only: the store path kept but (almost) never taken
         if (mine && differs && a.out32 && v == 0x9e3779b9u) a.out32[i] = valid ? v : 0u;
 #else
-        if (mine && differs && a.out32) a.out32[i] = valid ? v : 0u;
+        if constexpr (kRing) {
+          const bool put = mine && differs && a.out32 != nullptr;
+          const uint64_t pm = __ballot(put);
+          if (pm) {
+            const uint32_t at = rcount + __builtin_amdgcn_mbcnt_hi(
+                static_cast<uint32_t>(pm >> 32), __builtin_amdgcn_mbcnt_lo(static_cast<uint32_t>(pm), 0u));
+            if (put) {
+              ri[at] = static_cast<uint32_t>(i);
+              rv[at] = valid ? v : 0u;
+            }
+            rcount += static_cast<uint32_t>(__popcll(pm));
+            if (rcount > kRingN - 64) ring_flush();
+          }
+        } else {
+          if (mine && differs && a.out32) a.out32[i] = valid ? v : 0u;
+        }
 #endif
       } else if (MODE == kModeVerify) {
         const uint32_t computed = crc_mask(crc);  // reader_common.cc:36-47
@@ -1793,6 +1826,9 @@ __device__ __forceinline__ void crc32c_rows_body(const BlockArgs& a) {
 #ifdef FORST_DIAG
   if (lane == 0 && gw < kDiagWaves) g_wave_t1[gw] = wall_clock64();
 #endif
+  if constexpr (kRing) {
+    if (rcount) ring_flush();
+  }
   if constexpr (kStage) {  // the staged results, coalesced
     __syncthreads();
     const uint64_t lo = feed.wlo, hi = feed.whi;

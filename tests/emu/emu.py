@@ -188,13 +188,14 @@ def wal_record_crc(log, header_offsets, write_in_place=True):
 
 
 def wal_record_crc_lengths(log, header_offsets, payload_lengths, recyclable=False,
-                           write_in_place=True):
+                           write_in_place=True, with_out=True):
     log = _aligned(log)
     offs = np.ascontiguousarray(header_offsets, dtype=np.uint64)
     lens = np.ascontiguousarray(payload_lengths, dtype=np.uint32)
     out = np.zeros(len(offs), np.uint32)
     _chk(lib().forst_wal_record_crc_lengths(_p(log), log.nbytes, _p(offs), _p(lens), len(offs),
-                                            int(recyclable), int(write_in_place), _p(out), None))
+                                            int(recyclable), int(write_in_place),
+                                            _p(out) if with_out else None, None))
     return out, log
 
 

@@ -514,6 +514,9 @@ def test_emu_raw_split_short_and_long(recyclable):
     assert (img[:len(buf)] == buf).all()
     assert (crcs == np.frombuffer(b"".join(buf[int(o):int(o) + 4].tobytes() for o in poffs),
                                   np.uint32)).all()
+    # in place only (no CRC array): the kernels' own header stores
+    _, img = emu.wal_record_crc_lengths(w, poffs, plens, recyclable=recyclable, with_out=False)
+    assert (img[:len(buf)] == buf).all()
     b = buf.copy()
     hs = 11 if recyclable else 7
     short = [k for k in range(len(poffs)) if 0 < plens[k] < 400]

@@ -662,7 +662,8 @@ hipError_t launch_kv(int mode, const KvArgs& a, hipStream_t stream, const char**
   if (a.n == 0) return hipSuccess;
   const uint64_t per_wg = uint64_t(kWaves) * 64;
 #ifndef FORST_KV_WG_PER_CU
-#define FORST_KV_WG_PER_CU 4  // (build knob for the A/B: workgroups per CU in the grid)
+#define FORST_KV_WG_PER_CU 16  // (grid: 4 resident per CU by LDS, the rest queue behind them: the grid-stride
+                               // tiles end more evenly; A/B 4 / 8 / 16 in profiles/ab_r06/kv_grid_r06m.log)
 #endif
   const uint32_t wg_per_cu = FORST_KV_WG_PER_CU;
   const uint32_t grid = static_cast<uint32_t>(std::max<uint64_t>(
